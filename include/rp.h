@@ -1,0 +1,212 @@
+/*
+ * rp.h -- C-ABI of the MI355X path-tracing hot path (librp.so).
+ *
+ * Drop-in boundary for alucas2/raytracing-potato ("scaling-potato", crate raytracing2).
+ * The reference has no FFI; its seam is the per-pixel worker loop
+ *   main.rs:61-92  (make_uv_jitter -> Camera::shoot -> trace_path -> accumulate -> average)
+ * calling
+ *   render.rs:94-146 trace_path / trace_path_first / trace_path_continue
+ * over the scene types
+ *   hittable.rs:10-15 (Hittable), mesh.rs:18-22 (Mesh), material.rs:19-91 (Scatter/Emit/Absorb/Material),
+ *   texture.rs:10-18 (Texture), render.rs:10-25 (SceneData, Camera).
+ * rp_render() replaces that whole per-pixel loop for one frame (or one shard of it); the host keeps
+ * scene construction, OBJ/TGA loading and image output (example_scenes.rs, mesh.rs:145, image.rs:73,116).
+ *
+ * Conventions
+ *   - Plain C types only; no HIP/C++ types or exceptions cross this boundary.
+ *   - Every function returning int returns RP_OK (0) or a negative rp_status; rp_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.  Nothing aborts or panics.
+ *   - Ownership: the caller owns every buffer it passes.  rp_scene_create deep-copies the scene into
+ *     device memory (HBM); the scene is immutable afterwards.
+ *   - Determinism (the RNG contract): pixel (i, j) is rendered with its own
+ *     StdRng::seed_from_u64(params.seed + j*width + i) (rand 0.8 StdRng = ChaCha12) and the unchanged
+ *     per-pixel body of main.rs:70-87.  Output depends only on (scene, camera, seed, width, height, spp,
+ *     max_bounce) -- never on tiling, sharding, device count or scheduling.
+ *   - Arithmetic is IEEE binary64 throughout, as the reference (utility.rs:14 `type Real = f64`).
+ *   - Image layout: row-major, pixel (i, j) at index j*width + i, row j = 0 is the BOTTOM row
+ *     (image.rs:31-33, main.rs:119, tga::save writes bottom-left origin).  RGB are linear f64 averages
+ *     (main.rs:86), i.e. before to_srgb_u8 (utility.rs:212).
+ */
+#ifndef RP_H
+#define RP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RP_ABI_VERSION 1
+
+typedef enum rp_status {
+  RP_OK = 0,
+  RP_EINVAL = -1,    /* bad argument / malformed scene (the reference would panic: index out of range, etc.) */
+  RP_EHIP = -2,      /* HIP runtime error */
+  RP_ENOMEM = -3,    /* host or device allocation failed */
+  RP_ENODEV = -4,    /* no usable gfx950 device */
+  RP_EINTERNAL = -5  /* kernel reported an internal error (e.g. traversal stack overflow) */
+} rp_status;
+
+/* ---------------------------------------------------------------- scene description ----------- */
+
+/* hittable.rs:10-15.  List/Bvh aggregates are expressed by rp_scene_desc.root_kind. */
+enum { RP_HITTABLE_SPHERE = 0, RP_HITTABLE_TRIANGLE = 1 };
+
+typedef struct rp_hittable {
+  uint32_t kind;       /* RP_HITTABLE_* */
+  uint32_t material;   /* Sphere {material: MaterialId} */
+  uint32_t mesh;       /* Triangle {mesh: MeshId} */
+  uint32_t triangle;   /* Triangle {triangle: TriangleId} = offset of the first of 3 indices (mesh.rs:33) */
+  double center[3];    /* Sphere {center} */
+  double radius;       /* Sphere {radius} */
+} rp_hittable;
+
+/* mesh.rs:7-22: Vertex {position, normal, uv} stored as three interleaved arrays. */
+typedef struct rp_mesh {
+  uint32_t n_vertices;
+  uint32_t n_indices;      /* multiple of 3 */
+  const double* positions; /* 3 * n_vertices (x, y, z per vertex) */
+  const double* normals;   /* 3 * n_vertices */
+  const double* uvs;       /* 2 * n_vertices */
+  const uint32_t* indices; /* n_indices */
+  uint32_t material;       /* Mesh.material (MaterialId) */
+  uint32_t reserved;
+} rp_mesh;
+
+/* material.rs:19-24 */
+enum { RP_SCATTER_NONE = 0, RP_SCATTER_LAMBERT = 1, RP_SCATTER_METAL = 2, RP_SCATTER_DIELECTRIC = 3 };
+/* material.rs:66-71 */
+enum { RP_ABSORB_BLACK_BODY = 0, RP_ABSORB_WHITE_BODY = 1, RP_ABSORB_ALBEDO = 2, RP_ABSORB_ALBEDO_MAP = 3 };
+/* material.rs:40-46 */
+enum { RP_EMIT_NONE = 0, RP_EMIT_DEBUG_NORMALS = 1, RP_EMIT_COLOR = 2, RP_EMIT_SKY_GRADIENT = 3,
+       RP_EMIT_SKY_SPHERE = 4 };
+/* texture.rs:10-18 */
+enum { RP_TEXTURE_MISSING = 0, RP_TEXTURE_DEBUG_UVS = 1, RP_TEXTURE_SOLID = 2, RP_TEXTURE_IMAGE = 3,
+       RP_TEXTURE_CHECKER = 4, RP_TEXTURE_NOISE = 5, RP_TEXTURE_PERLIN = 6 };
+
+typedef struct rp_scatter {
+  uint32_t kind;       /* RP_SCATTER_* */
+  uint32_t reserved;
+  double param;        /* Metal {fuzziness} | Dielectric {refraction_index} */
+} rp_scatter;
+
+typedef struct rp_absorb {
+  uint32_t kind;       /* RP_ABSORB_* */
+  uint32_t texture;    /* AlbedoMap(TextureId) */
+  double color[3];     /* Albedo(Color) */
+} rp_absorb;
+
+typedef struct rp_emit {
+  uint32_t kind;       /* RP_EMIT_* */
+  uint32_t texture;    /* SkySphere(TextureId) */
+  double color[3];     /* Color(Color) */
+} rp_emit;
+
+/* material.rs:87-91; evaluation order scatter -> absorb -> emit (material.rs:104-110) */
+typedef struct rp_material {
+  rp_scatter scatter;
+  rp_absorb absorb;
+  rp_emit emit;
+} rp_material;
+
+typedef struct rp_texture {
+  uint32_t kind;         /* RP_TEXTURE_* */
+  uint32_t odd, even;    /* Checker {odd, even} (TextureId) */
+  uint32_t width, height;/* Image: Array2d<[u8;4]> dimensions */
+  uint32_t reserved;
+  int64_t seed;          /* Noise {seed} | Perlin {seed} (isize) */
+  double color[3];       /* Solid(Color) */
+  const uint8_t* rgba;   /* Image: width*height*4 bytes, texel (i, j) at 4*(i + j*width), j = 0 bottom row */
+} rp_texture;
+
+enum { RP_ROOT_BVH = 0, RP_ROOT_LIST = 1 };
+
+/* render.rs:10-14 SceneData + example_scenes.rs:14-19 root/background. */
+typedef struct rp_scene_desc {
+  uint32_t root_kind;                  /* Hittable::Bvh (any tree shape) or Hittable::List */
+  uint32_t n_hittables;
+  const rp_hittable* hittables;
+  uint32_t n_meshes;
+  const rp_mesh* meshes;
+  uint32_t n_materials;
+  const rp_material* materials;
+  uint32_t n_textures;
+  const rp_texture* textures;
+  rp_emit background;
+} rp_scene_desc;
+
+/* render.rs:19-25 + utility.rs:160-163.  orientation is column-major as nalgebra's Matrix3
+ * (columns x, y, z of Transformation::lookat, utility.rs:172-177). */
+typedef struct rp_camera {
+  double aspect_ratio, fov, focal_dist, lens_radius;
+  double orientation[9];
+  double position[3];
+} rp_camera;
+
+/* One frame (or one shard of it).  The frame is cut into tile_w x tile_h tiles in row-major tile
+ * order (image.rs:151-167); shard s of S renders tiles t with t % S == s (interleaved, balances sky
+ * against bunny cost across GPUs). */
+typedef struct rp_render_params {
+  uint32_t width, height;   /* Multisampler {width, height} */
+  uint32_t spp;             /* Multisampler {num_samples} */
+  uint32_t max_bounce;      /* trace_path depth (main.rs:25); >= 1 (render.rs:97) */
+  uint64_t seed;            /* base seed of the RNG contract */
+  uint32_t tile_w, tile_h;  /* 0 -> 32 (main.rs:26) */
+  uint32_t shard, num_shards;/* num_shards 0 -> 1 */
+} rp_render_params;
+
+typedef struct rp_stats {
+  uint64_t rays;      /* root scene.hit() calls, primary + secondary (render.rs:105,133) */
+  uint64_t samples;   /* camera samples traced */
+  uint64_t pixels;    /* pixels written */
+  double seconds;     /* device time of the render (HIP events) */
+} rp_stats;
+
+typedef struct rp_scene rp_scene;   /* opaque: device-resident scene + acceleration structure */
+
+/* Library / device queries. */
+int rp_abi_version(void);
+const char* rp_last_error(void);
+int rp_device_count(int* count);
+
+/* Build the acceleration structure and copy the scene to device `device`.  Validates every index the
+ * reference would bounds-check (material/mesh/texture ids, triangle offsets, checker recursion). */
+int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out);
+void rp_scene_destroy(rp_scene* scene);
+/* Acceleration-structure statistics: node count, leaf count, max depth, primitive count. */
+int rp_scene_info(const rp_scene* scene, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth,
+                  uint64_t* n_prims, uint64_t* device_bytes);
+
+/* Number of pixels in shard params->shard (the length of the compact shard buffer). */
+int rp_shard_pixel_count(const rp_render_params* params, uint64_t* count);
+/* Scatter a compact shard buffer (shard order: its tiles in increasing tile index, row-major inside a
+ * tile) into a full frame; `channels` values per pixel. */
+int rp_shard_unpack(const rp_render_params* params, const double* shard_buf, uint32_t channels,
+                    double* frame);
+
+/* Render synchronously into host memory.  out_rgb: width*height*3 doubles (only the shard's pixels are
+ * written).  out_foreground (nullable): width*height floats, fraction of samples whose first ray hit
+ * geometry (main.rs:81-87).  stats nullable. */
+int rp_render(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
+              double* out_rgb, float* out_foreground, rp_stats* stats);
+
+/* Asynchronous device-resident render on `stream` (a hipStream_t, NULL = default stream) of the scene's
+ * device.  d_shard_rgb: shard_pixel_count*3 doubles in device memory, compact shard order.
+ * d_shard_fg (nullable): shard_pixel_count floats.  d_counters (nullable): 4 uint64 in device memory
+ * that receive {rays, samples, pixels, status}; they are zeroed on the stream before the launch.
+ * No host synchronisation, allocation or copy happens inside: safe to capture in a hipGraph. */
+int rp_render_device(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
+                     double* d_shard_rgb, float* d_shard_fg, uint64_t* d_counters, void* stream);
+
+/* Closest-hit query (Hittable::hit on the root, hittable.rs:18 / bvh.rs:121) for n rays, synchronous,
+ * host buffers.  rays: n * 8 doubles {origin xyz, direction xyz, t_min, t_max} (utility.rs:52-57).
+ * out_hit: n * 9 doubles {t, position xyz, normal xyz, u, v} (utility.rs:84-89), t = +inf on a miss.
+ * out_material: n uint32 (MaterialId, 0xffffffff on a miss).  Used to test the traversal in isolation. */
+int rp_intersect(rp_scene* scene, const double* rays, uint64_t n, double* out_hit, uint32_t* out_material);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RP_H */

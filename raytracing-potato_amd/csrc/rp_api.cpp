@@ -1,0 +1,383 @@
+// rp_api.cpp -- implementation of the C-ABI in include/rp.h (librp.so).
+//
+// Host side of the drop-in: validates the reference-shaped scene (rp_scene_desc mirrors hittable.rs,
+// mesh.rs, material.rs, texture.rs), builds the acceleration structure (rp_bvh.cpp), copies it to HBM
+// once, and launches the persistent render kernel (rp_kernel.hip) per frame / shard.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rp.h"
+#include "rp_bvh.h"
+#include "rp_kernel.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define RP_HIP(call)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (call);                                                                 \
+    if (e_ != hipSuccess) return fail(RP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class T>
+int upload(const std::vector<T>& v, T** out) {
+  size_t bytes = sizeof(T) * (v.empty() ? 1 : v.size());
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(out), bytes);
+  if (e != hipSuccess) return fail(RP_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  if (!v.empty()) {
+    e = hipMemcpy(*out, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(RP_EHIP, std::string("hipMemcpy: ") + hipGetErrorString(e));
+  }
+  return RP_OK;
+}
+
+}  // namespace
+
+struct rp_scene {
+  int device = 0;
+  rpk::KScene ks{};
+  rpl::Node2* d_nodes = nullptr;
+  rpl::Prim* d_prims = nullptr;
+  double* d_vnrm = nullptr;
+  double* d_vuv = nullptr;
+  rpl::Material* d_mats = nullptr;
+  rpl::Texture* d_texs = nullptr;
+  uint32_t* d_texels = nullptr;
+  uint64_t* d_ws = nullptr;  // default counter block (8 x u64)
+  uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
+  uint32_t max_depth = 0;
+  int num_cu = 0;
+  int blocks_per_cu = 0;
+};
+
+namespace {
+
+struct Tiling {
+  uint32_t tw, th, shards, shard, tiles_x, tiles_y, n_tiles, n_shard_tiles;
+  uint64_t n_slots;
+};
+
+int make_tiling(const rp_render_params* p, Tiling& t) {
+  if (!p) return fail(RP_EINVAL, "params is NULL");
+  if (p->width == 0 || p->height == 0) return fail(RP_EINVAL, "width and height must be >= 1");
+  t.tw = p->tile_w ? p->tile_w : 32;
+  t.th = p->tile_h ? p->tile_h : 32;
+  t.shards = p->num_shards ? p->num_shards : 1;
+  t.shard = p->shard;
+  if (t.shard >= t.shards) return fail(RP_EINVAL, "shard must be < num_shards");
+  t.tiles_x = (p->width + t.tw - 1) / t.tw;
+  t.tiles_y = (p->height + t.th - 1) / t.th;
+  t.n_tiles = t.tiles_x * t.tiles_y;
+  t.n_shard_tiles = t.n_tiles > t.shard ? (t.n_tiles - t.shard + t.shards - 1) / t.shards : 0;
+  t.n_slots = (uint64_t)t.n_shard_tiles * t.tw * t.th;
+  if (t.n_slots >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel slots)");
+  return RP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rp_abi_version(void) { return RP_ABI_VERSION; }
+
+const char* rp_last_error(void) { return g_err.c_str(); }
+
+int rp_device_count(int* count) {
+  if (!count) return fail(RP_EINVAL, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(RP_ENODEV, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return RP_OK;
+}
+
+void rp_scene_destroy(rp_scene* s) {
+  if (!s) return;
+  DeviceGuard g(s->device);
+  for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
+                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws})
+    if (p) (void)hipFree(p);
+  delete s;
+}
+
+int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  *out = nullptr;
+  std::string err;
+  int rc = rpb::validate(desc, err);
+  if (rc != RP_OK) return fail(rc, err);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RP_ENODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RP_EINVAL, "device index out of range");
+  hipDeviceProp_t prop;
+  RP_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RP_ENODEV, std::string("librp.so is built for gfx950, device is ") + prop.gcnArchName);
+
+  rpb::PackedScene ps;
+  rpb::BuildOptions opt;
+  rc = rpb::build(desc, opt, ps, err);
+  if (rc != RP_OK) return fail(rc, err);
+
+  DeviceGuard g(device);
+  rp_scene* s = new rp_scene();
+  s->device = device;
+  s->num_cu = prop.multiProcessorCount;
+  auto bail = [&](int code) { rp_scene_destroy(s); return code; };
+  if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
+      (rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
+      (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
+      (rc = upload(ps.texels, &s->d_texels)))
+    return bail(rc);
+  if (hipMalloc(reinterpret_cast<void**>(&s->d_ws), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess)
+    return bail(fail(RP_ENOMEM, "hipMalloc workspace"));
+  s->ks.nodes = s->d_nodes;
+  s->ks.prims = s->d_prims;
+  s->ks.vnrm = s->d_vnrm;
+  s->ks.vuv = s->d_vuv;
+  s->ks.mats = s->d_mats;
+  s->ks.texs = s->d_texs;
+  s->ks.texels = s->d_texels;
+  s->ks.background = ps.background;
+  s->ks.root = ps.root;
+  s->ks.stack_depth = ps.max_depth + 2;
+  s->n_nodes = ps.nodes.size();
+  s->n_leaves = ps.n_leaves;
+  s->n_prims = desc->n_hittables;
+  s->max_depth = ps.max_depth;
+  s->device_bytes = sizeof(rpl::Node2) * ps.nodes.size() + sizeof(rpl::Prim) * ps.prims.size() +
+                    sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
+                    sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
+  int bpc = 0;
+  if (rpk::render_blocks_per_cu(s->ks.stack_depth, &bpc) != 0 || bpc < 1) bpc = 1;
+  s->blocks_per_cu = bpc;
+  *out = s;
+  return RP_OK;
+}
+
+int rp_scene_info(const rp_scene* s, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth, uint64_t* n_prims,
+                  uint64_t* device_bytes) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (n_nodes) *n_nodes = s->n_nodes;
+  if (n_leaves) *n_leaves = s->n_leaves;
+  if (max_depth) *max_depth = s->max_depth;
+  if (n_prims) *n_prims = s->n_prims;
+  if (device_bytes) *device_bytes = s->device_bytes;
+  return RP_OK;
+}
+
+int rp_shard_pixel_count(const rp_render_params* p, uint64_t* count) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!count) return fail(RP_EINVAL, "count is NULL");
+  *count = t.n_slots;
+  return RP_OK;
+}
+
+int rp_shard_unpack(const rp_render_params* p, const double* shard_buf, uint32_t channels, double* frame) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!shard_buf || !frame || channels == 0) return fail(RP_EINVAL, "NULL buffer or zero channels");
+  const uint64_t tile_px = (uint64_t)t.tw * t.th;
+  for (uint32_t k = 0; k < t.n_shard_tiles; k++) {
+    uint32_t tile = t.shard + k * t.shards;
+    uint32_t ox = (tile % t.tiles_x) * t.tw, oy = (tile / t.tiles_x) * t.th;
+    for (uint32_t lj = 0; lj < t.th; lj++) {
+      uint32_t j = oy + lj;
+      if (j >= p->height) break;
+      for (uint32_t li = 0; li < t.tw; li++) {
+        uint32_t i = ox + li;
+        if (i >= p->width) break;
+        const double* src = shard_buf + (k * tile_px + (uint64_t)lj * t.tw + li) * channels;
+        double* dst = frame + ((uint64_t)j * p->width + i) * channels;
+        for (uint32_t c = 0; c < channels; c++) dst[c] = src[c];
+      }
+    }
+  }
+  return RP_OK;
+}
+
+int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* d_rgb, float* d_fg,
+                     uint64_t* d_counters, void* stream) {
+  if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (p->max_bounce < 1) return fail(RP_EINVAL, "max_bounce must be >= 1 (render.rs:97 assert!(depth >= 1))");
+  DeviceGuard g(s->device);
+  uint64_t* ctr = d_counters ? d_counters : s->d_ws;
+  hipStream_t st = (hipStream_t)stream;
+  RP_HIP(hipMemsetAsync(ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+  if (t.n_slots == 0) return RP_OK;
+  if (p->spp == 0) {
+    // main.rs:86-87 with num_samples = 0: (0,0,0) / 0 and 0 / 0 are NaN; all-ones bits are a NaN.
+    RP_HIP(hipMemsetAsync(d_rgb, 0xff, sizeof(double) * 3 * t.n_slots, st));
+    if (d_fg) RP_HIP(hipMemsetAsync(d_fg, 0xff, sizeof(float) * t.n_slots, st));
+    return RP_OK;
+  }
+  rpk::KParams kp{};
+  std::memcpy(kp.orient, cam->orientation, sizeof kp.orient);
+  std::memcpy(kp.pos, cam->position, sizeof kp.pos);
+  kp.aspect = cam->aspect_ratio;
+  kp.tan_fov = std::tan(0.5 * cam->fov);  // render.rs:33, hoisted: a per-camera constant
+  kp.focal = cam->focal_dist;
+  kp.lens = cam->lens_radius;
+  kp.seed = p->seed;
+  kp.W = p->width;
+  kp.H = p->height;
+  kp.spp = p->spp;
+  kp.max_bounce = p->max_bounce;
+  kp.tw = t.tw;
+  kp.th = t.th;
+  kp.shard = t.shard;
+  kp.nshards = t.shards;
+  kp.tiles_x = t.tiles_x;
+  kp.n_shard_tiles = t.n_shard_tiles;
+  kp.n_slots = t.n_slots;
+  uint64_t want = (t.n_slots + 255) / 256;
+  uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
+  int grid = (int)(want < resident ? want : resident);
+  if (grid < 1) grid = 1;
+  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid, stream);
+  if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+  return RP_OK;
+}
+
+int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* out_rgb, float* out_fg,
+              rp_stats* stats) {
+  if (!s || !cam || !out_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  DeviceGuard g(s->device);
+  double* d_rgb = nullptr;
+  float* d_fg = nullptr;
+  uint64_t* d_ctr = nullptr;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int result = RP_OK;
+  std::vector<double> shard(3 * (t.n_slots ? t.n_slots : 1));
+  std::vector<float> shard_fg(out_fg ? (t.n_slots ? t.n_slots : 1) : 0);
+  uint64_t ctr[rpk::CTR_N] = {0};
+  float ms = 0.f;
+  do {
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { result = fail(RP_EHIP, "stream"); break; }
+    if (hipMalloc(reinterpret_cast<void**>(&d_rgb), sizeof(double) * shard.size()) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+        (out_fg && hipMalloc(reinterpret_cast<void**>(&d_fg), sizeof(float) * shard_fg.size()) != hipSuccess)) {
+      result = fail(RP_ENOMEM, "hipMalloc output");
+      break;
+    }
+    if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { result = fail(RP_EHIP, "event"); break; }
+    (void)hipEventRecord(e0, st);
+    result = rp_render_device(s, cam, p, d_rgb, d_fg, d_ctr, st);
+    if (result) break;
+    (void)hipEventRecord(e1, st);
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) { result = fail(RP_EHIP, std::string("render: ") + hipGetErrorString(e)); break; }
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (hipMemcpy(shard.data(), d_rgb, sizeof(double) * shard.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost) != hipSuccess ||
+        (out_fg && hipMemcpy(shard_fg.data(), d_fg, sizeof(float) * shard_fg.size(), hipMemcpyDeviceToHost) != hipSuccess)) {
+      result = fail(RP_EHIP, "copy back");
+      break;
+    }
+  } while (0);
+  if (d_rgb) (void)hipFree(d_rgb);
+  if (d_fg) (void)hipFree(d_fg);
+  if (d_ctr) (void)hipFree(d_ctr);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  if (result) return result;
+  if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
+  if (t.n_slots) {
+    rp_shard_unpack(p, shard.data(), 3, out_rgb);
+    if (out_fg) {
+      const uint64_t tile_px = (uint64_t)t.tw * t.th;
+      for (uint32_t k = 0; k < t.n_shard_tiles; k++) {
+        uint32_t tile = t.shard + k * t.shards;
+        uint32_t ox = (tile % t.tiles_x) * t.tw, oy = (tile / t.tiles_x) * t.th;
+        for (uint32_t lj = 0; lj < t.th && oy + lj < p->height; lj++)
+          for (uint32_t li = 0; li < t.tw && ox + li < p->width; li++)
+            out_fg[(uint64_t)(oy + lj) * p->width + ox + li] = shard_fg[k * tile_px + (uint64_t)lj * t.tw + li];
+      }
+    }
+  }
+  if (stats) {
+    stats->rays = ctr[rpk::CTR_RAYS];
+    stats->samples = ctr[rpk::CTR_SAMPLES];
+    stats->pixels = ctr[rpk::CTR_PIXELS];
+    stats->seconds = ms * 1e-3;
+  }
+  return RP_OK;
+}
+
+int rp_intersect(rp_scene* s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_material) {
+  if (!s || (n && (!rays || !out_hit || !out_material))) return fail(RP_EINVAL, "NULL argument");
+  if (n == 0) return RP_OK;
+  DeviceGuard g(s->device);
+  double *d_rays = nullptr, *d_hit = nullptr;
+  uint32_t* d_mat = nullptr;
+  uint64_t* d_ctr = nullptr;
+  int result = RP_OK;
+  uint64_t ctr[rpk::CTR_N] = {0};
+  do {
+    if (hipMalloc(reinterpret_cast<void**>(&d_rays), sizeof(double) * 8 * n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_hit), sizeof(double) * 9 * n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_mat), sizeof(uint32_t) * n) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess) {
+      result = fail(RP_ENOMEM, "hipMalloc");
+      break;
+    }
+    if (hipMemcpy(d_rays, rays, sizeof(double) * 8 * n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(d_ctr, 0, sizeof(uint64_t) * rpk::CTR_N) != hipSuccess) {
+      result = fail(RP_EHIP, "hipMemcpy");
+      break;
+    }
+    int e = rpk::launch_intersect(s->ks, d_rays, n, d_hit, d_mat, d_ctr, nullptr);
+    if (e) { result = fail(RP_EHIP, std::string("intersect launch: ") + hipGetErrorString((hipError_t)e)); break; }
+    hipError_t he = hipDeviceSynchronize();
+    if (he != hipSuccess) { result = fail(RP_EHIP, std::string("intersect: ") + hipGetErrorString(he)); break; }
+    if (hipMemcpy(out_hit, d_hit, sizeof(double) * 9 * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(out_material, d_mat, sizeof(uint32_t) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost) != hipSuccess) {
+      result = fail(RP_EHIP, "copy back");
+      break;
+    }
+  } while (0);
+  for (void* p : {(void*)d_rays, (void*)d_hit, (void*)d_mat, (void*)d_ctr})
+    if (p) (void)hipFree(p);
+  if (result) return result;
+  if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
+  return RP_OK;
+}
+
+}  // extern "C"

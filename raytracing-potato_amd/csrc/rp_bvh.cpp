@@ -1,0 +1,473 @@
+// rp_bvh.cpp -- scene validation, binned-SAH BVH2 build, packing into rp_layout.h records.
+#include "rp_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+namespace rpb {
+
+namespace {
+
+struct Box {
+  double lo[3], hi[3];
+  void reset() {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::numeric_limits<double>::infinity();
+      hi[k] = -std::numeric_limits<double>::infinity();
+    }
+  }
+  // AABB::union (utility.rs:130-135): exact min/max, so parents contain children bit-exactly.
+  void grow(const Box& b) {
+    for (int k = 0; k < 3; k++) {
+      lo[k] = std::fmin(lo[k], b.lo[k]);
+      hi[k] = std::fmax(hi[k], b.hi[k]);
+    }
+  }
+  double area() const {
+    double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Ref {
+  Box box;
+  double c[3];
+  uint32_t id;
+};
+
+struct Builder {
+  const BuildOptions& opt;
+  std::vector<Ref>& refs;
+  std::vector<rpl::Node2>& nodes;
+  std::vector<uint32_t>& order;  // leaf-ordered hittable ids
+  uint32_t max_depth = 0;
+  uint64_t n_leaves = 0;
+
+  struct Child {
+    Box box;
+    int32_t child;
+    uint32_t count;
+  };
+
+  Child make_leaf(uint32_t b, uint32_t e, const Box& box) {
+    Child c;
+    c.box = box;
+    c.child = (int32_t)order.size();
+    c.count = e - b;
+    for (uint32_t i = b; i < e; i++) order.push_back(refs[i].id);
+    n_leaves++;
+    return c;
+  }
+
+  // Returns the split position m in (b, e) or b when the range should be a leaf.
+  uint32_t split(uint32_t b, uint32_t e, const Box& box) {
+    uint32_t n = e - b;
+    Box cb;
+    cb.reset();
+    for (uint32_t i = b; i < e; i++)
+      for (int k = 0; k < 3; k++) {
+        cb.lo[k] = std::fmin(cb.lo[k], refs[i].c[k]);
+        cb.hi[k] = std::fmax(cb.hi[k], refs[i].c[k]);
+      }
+    const uint32_t NB = std::max(2u, std::min(opt.bins, n));
+    double best_cost = std::numeric_limits<double>::infinity();
+    int best_axis = -1;
+    uint32_t best_bin = 0;
+    std::vector<Box> bb(NB);
+    std::vector<uint32_t> bn(NB);
+    std::vector<double> right_area(NB);
+    std::vector<uint32_t> right_n(NB);
+    for (int ax = 0; ax < 3; ax++) {
+      double ext = cb.hi[ax] - cb.lo[ax];
+      if (!(ext > 0.0)) continue;
+      double scale = (double)NB / ext;
+      for (uint32_t k = 0; k < NB; k++) { bb[k].reset(); bn[k] = 0; }
+      for (uint32_t i = b; i < e; i++) {
+        int k = (int)((refs[i].c[ax] - cb.lo[ax]) * scale);
+        k = std::min<int>(std::max(k, 0), (int)NB - 1);
+        bb[k].grow(refs[i].box);
+        bn[k]++;
+      }
+      Box acc;
+      acc.reset();
+      uint32_t cnt = 0;
+      for (int k = (int)NB - 1; k >= 1; k--) {
+        acc.grow(bb[k]);
+        cnt += bn[k];
+        right_area[k] = acc.area();
+        right_n[k] = cnt;
+      }
+      acc.reset();
+      cnt = 0;
+      for (uint32_t k = 0; k + 1 < NB; k++) {
+        acc.grow(bb[k]);
+        cnt += bn[k];
+        if (cnt == 0 || right_n[k + 1] == 0) continue;
+        double cost = acc.area() * cnt + right_area[k + 1] * right_n[k + 1];
+        if (cost < best_cost) { best_cost = cost; best_axis = ax; best_bin = k; }
+      }
+    }
+    double parent_area = box.area();
+    double leaf_cost = opt.cost_intersect * n;
+    if (best_axis >= 0) {
+      double split_cost = opt.cost_traverse +
+                          (parent_area > 0.0 ? opt.cost_intersect * best_cost / parent_area : opt.cost_intersect * n);
+      if (n <= opt.max_leaf && leaf_cost <= split_cost) return b;
+      double ext = cb.hi[best_axis] - cb.lo[best_axis];
+      double scale = (double)NB / ext;
+      auto mid = std::partition(refs.begin() + b, refs.begin() + e, [&](const Ref& r) {
+        int k = (int)((r.c[best_axis] - cb.lo[best_axis]) * scale);
+        k = std::min<int>(std::max(k, 0), (int)NB - 1);
+        return (uint32_t)k <= best_bin;
+      });
+      uint32_t m = (uint32_t)(mid - refs.begin());
+      if (m > b && m < e) return m;
+    }
+    if (n <= opt.max_leaf) return b;
+    // Degenerate centroids (or a failed partition): object median on the longest centroid axis.
+    int ax = 0;
+    for (int k = 1; k < 3; k++)
+      if (cb.hi[k] - cb.lo[k] > cb.hi[ax] - cb.lo[ax]) ax = k;
+    uint32_t m = b + n / 2;
+    std::nth_element(refs.begin() + b, refs.begin() + m, refs.begin() + e, [ax](const Ref& x, const Ref& y) {
+      if (x.c[ax] != y.c[ax]) return x.c[ax] < y.c[ax];
+      return x.id < y.id;
+    });
+    return m;
+  }
+
+  // Builds range [b, e) whose box is `box`; returns its child descriptor for the parent.
+  Child build(uint32_t b, uint32_t e, const Box& box, uint32_t depth) {
+    uint32_t m = split(b, e, box);
+    if (m == b) return make_leaf(b, e, box);
+    Child c;
+    c.box = box;
+    c.count = 0;
+    c.child = (int32_t)nodes.size();
+    emit_node(b, m, e, depth);
+    return c;
+  }
+
+  void emit_node(uint32_t b, uint32_t m, uint32_t e, uint32_t depth) {
+    if (depth > max_depth) max_depth = depth;
+    uint32_t self = (uint32_t)nodes.size();
+    nodes.emplace_back();
+    Box lb, rb;
+    lb.reset();
+    rb.reset();
+    for (uint32_t i = b; i < m; i++) lb.grow(refs[i].box);
+    for (uint32_t i = m; i < e; i++) rb.grow(refs[i].box);
+    Child l = build(b, m, lb, depth + 1);
+    Child r = build(m, e, rb, depth + 1);
+    set_child(self, 0, l);
+    set_child(self, 1, r);
+  }
+
+  void set_child(uint32_t node, int slot, const Child& c) {
+    rpl::Node2& n = nodes[node];
+    n.lo_x[slot] = c.box.lo[0]; n.hi_x[slot] = c.box.hi[0];
+    n.lo_y[slot] = c.box.lo[1]; n.hi_y[slot] = c.box.hi[1];
+    n.lo_z[slot] = c.box.lo[2]; n.hi_z[slot] = c.box.hi[2];
+    n.child[slot] = c.child;
+    n.count[slot] = c.count;
+  }
+};
+
+Box hittable_box(const rp_scene_desc* d, const rp_hittable& h) {
+  Box b;
+  if (h.kind == RP_HITTABLE_SPHERE) {
+    // hittable.rs:124-129
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = h.center[k] - h.radius;
+      b.hi[k] = h.center[k] + h.radius;
+    }
+  } else {
+    // hittable.rs:131-140
+    const rp_mesh& m = d->meshes[h.mesh];
+    const double* a = m.positions + 3 * (size_t)m.indices[h.triangle];
+    const double* bb = m.positions + 3 * (size_t)m.indices[h.triangle + 1];
+    const double* c = m.positions + 3 * (size_t)m.indices[h.triangle + 2];
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = std::fmin(std::fmin(a[k], bb[k]), c[k]);
+      b.hi[k] = std::fmax(std::fmax(a[k], bb[k]), c[k]);
+    }
+  }
+  return b;
+}
+
+}  // namespace
+
+int validate(const rp_scene_desc* d, std::string& err) {
+  auto fail = [&](const std::string& m) { err = m; return (int)RP_EINVAL; };
+  if (!d) return fail("scene description is NULL");
+  if (d->root_kind != RP_ROOT_BVH && d->root_kind != RP_ROOT_LIST) return fail("unknown root_kind");
+  if (d->root_kind == RP_ROOT_BVH && d->n_hittables == 0)
+    return fail("Bvh::new over zero hittables (bvh.rs:40 unreachable!())");
+  if (d->n_hittables && !d->hittables) return fail("hittables is NULL");
+  if (d->n_meshes && !d->meshes) return fail("meshes is NULL");
+  if (d->n_materials && !d->materials) return fail("materials is NULL");
+  if (d->n_textures && !d->textures) return fail("textures is NULL");
+  auto check_tex = [&](uint32_t t, const char* what) -> bool {
+    if (t >= d->n_textures) { err = std::string(what) + ": TextureId out of range"; return false; }
+    return true;
+  };
+  for (uint32_t i = 0; i < d->n_textures; i++) {
+    const rp_texture& t = d->textures[i];
+    if (t.kind > RP_TEXTURE_PERLIN) return fail("texture " + std::to_string(i) + ": unknown kind");
+    if (t.kind == RP_TEXTURE_IMAGE && (!t.rgba || t.width == 0 || t.height == 0))
+      return fail("texture " + std::to_string(i) + ": empty image");
+    if (t.kind == RP_TEXTURE_CHECKER) {
+      if (!check_tex(t.odd, "checker odd") || !check_tex(t.even, "checker even")) return RP_EINVAL;
+    }
+  }
+  // Checker chains must terminate (the reference would recurse forever).
+  for (uint32_t i = 0; i < d->n_textures; i++) {
+    std::vector<uint32_t> stack{i};
+    std::vector<uint8_t> seen(d->n_textures, 0);
+    uint64_t steps = 0;
+    while (!stack.empty()) {
+      uint32_t t = stack.back();
+      stack.pop_back();
+      if (++steps > 64ull * d->n_textures + 64) return fail("checker textures form a cycle");
+      if (d->textures[t].kind == RP_TEXTURE_CHECKER) {
+        if (seen[t]) return fail("checker textures form a cycle");
+        seen[t] = 1;
+        stack.push_back(d->textures[t].odd);
+        stack.push_back(d->textures[t].even);
+      }
+    }
+  }
+  for (uint32_t i = 0; i < d->n_materials; i++) {
+    const rp_material& m = d->materials[i];
+    if (m.scatter.kind > RP_SCATTER_DIELECTRIC) return fail("material " + std::to_string(i) + ": bad scatter");
+    if (m.absorb.kind > RP_ABSORB_ALBEDO_MAP) return fail("material " + std::to_string(i) + ": bad absorb");
+    if (m.emit.kind > RP_EMIT_SKY_SPHERE) return fail("material " + std::to_string(i) + ": bad emit");
+    if (m.absorb.kind == RP_ABSORB_ALBEDO_MAP && !check_tex(m.absorb.texture, "AlbedoMap")) return RP_EINVAL;
+    if (m.emit.kind == RP_EMIT_SKY_SPHERE && !check_tex(m.emit.texture, "SkySphere")) return RP_EINVAL;
+  }
+  if (d->background.kind > RP_EMIT_SKY_SPHERE) return fail("background: bad emit kind");
+  if (d->background.kind == RP_EMIT_SKY_SPHERE && !check_tex(d->background.texture, "background SkySphere"))
+    return RP_EINVAL;
+  for (uint32_t i = 0; i < d->n_meshes; i++) {
+    const rp_mesh& m = d->meshes[i];
+    if (m.n_vertices && (!m.positions || !m.normals || !m.uvs)) return fail("mesh " + std::to_string(i) + ": NULL arrays");
+    if (m.n_indices && !m.indices) return fail("mesh " + std::to_string(i) + ": NULL indices");
+    if (m.material >= d->n_materials) return fail("mesh " + std::to_string(i) + ": MaterialId out of range");
+    for (uint32_t k = 0; k < m.n_indices; k++)
+      if (m.indices[k] >= m.n_vertices) return fail("mesh " + std::to_string(i) + ": vertex index out of range");
+  }
+  for (uint32_t i = 0; i < d->n_hittables; i++) {
+    const rp_hittable& h = d->hittables[i];
+    if (h.kind == RP_HITTABLE_SPHERE) {
+      if (h.material >= d->n_materials) return fail("sphere " + std::to_string(i) + ": MaterialId out of range");
+    } else if (h.kind == RP_HITTABLE_TRIANGLE) {
+      if (h.mesh >= d->n_meshes) return fail("triangle " + std::to_string(i) + ": MeshId out of range");
+      if ((uint64_t)h.triangle + 2 >= d->meshes[h.mesh].n_indices)
+        return fail("triangle " + std::to_string(i) + ": TriangleId out of range");
+    } else {
+      return fail("hittable " + std::to_string(i) + ": unknown kind");
+    }
+  }
+  return RP_OK;
+}
+
+int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std::string& err) {
+  out = PackedScene();
+  // ---- shading tables
+  std::vector<uint64_t> vbase(d->n_meshes + 1, 0);
+  for (uint32_t i = 0; i < d->n_meshes; i++) vbase[i + 1] = vbase[i] + d->meshes[i].n_vertices;
+  if (vbase[d->n_meshes] > 0xffffffffull) { err = "too many vertices"; return RP_EINVAL; }
+  out.vnrm.resize(3 * vbase[d->n_meshes] + 3);
+  out.vuv.resize(2 * vbase[d->n_meshes] + 2);
+  for (uint32_t i = 0; i < d->n_meshes; i++) {
+    const rp_mesh& m = d->meshes[i];
+    if (m.n_vertices) {
+      std::memcpy(&out.vnrm[3 * vbase[i]], m.normals, sizeof(double) * 3 * m.n_vertices);
+      std::memcpy(&out.vuv[2 * vbase[i]], m.uvs, sizeof(double) * 2 * m.n_vertices);
+    }
+  }
+  for (uint32_t i = 0; i < d->n_materials; i++) {
+    const rp_material& s = d->materials[i];
+    rpl::Material m{};
+    m.scatter_kind = s.scatter.kind;
+    m.scatter_param = s.scatter.param;
+    m.absorb_kind = s.absorb.kind;
+    m.absorb_tex = s.absorb.texture;
+    m.emit_kind = s.emit.kind;
+    m.emit_tex = s.emit.texture;
+    for (int k = 0; k < 3; k++) {
+      m.absorb_color[k] = s.absorb.color[k];
+      m.emit_color[k] = s.emit.color[k];
+    }
+    out.materials.push_back(m);
+  }
+  if (out.materials.empty()) out.materials.push_back(rpl::Material{});
+  for (uint32_t i = 0; i < d->n_textures; i++) {
+    const rp_texture& s = d->textures[i];
+    rpl::Texture t{};
+    t.kind = s.kind;
+    t.odd = s.odd;
+    t.even = s.even;
+    t.width = s.width;
+    t.height = s.height;
+    t.seed = s.seed;
+    for (int k = 0; k < 3; k++) t.color[k] = s.color[k];
+    t.texel_offset = out.texels.size();
+    if (s.kind == RP_TEXTURE_IMAGE) {
+      size_t n = (size_t)s.width * s.height;
+      size_t off = out.texels.size();
+      out.texels.resize(off + n);
+      std::memcpy(&out.texels[off], s.rgba, n * 4);
+    }
+    out.textures.push_back(t);
+  }
+  if (out.textures.empty()) out.textures.push_back(rpl::Texture{});
+  if (out.texels.empty()) out.texels.push_back(0);
+  out.background.kind = d->background.kind;
+  out.background.tex = d->background.texture;
+  for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
+
+  // ---- BVH over all hittables (a List root is served by the same tree: closest hit is
+  //      independent of visit order except exact-t ties)
+  uint32_t n = d->n_hittables;
+  std::vector<Ref> refs(n);
+  for (uint32_t i = 0; i < n; i++) {
+    refs[i].box = hittable_box(d, d->hittables[i]);
+    for (int k = 0; k < 3; k++) refs[i].c[k] = 0.5 * (refs[i].box.lo[k] + refs[i].box.hi[k]);
+    refs[i].id = i;
+  }
+  std::vector<uint32_t> order;
+  order.reserve(n);
+  Builder B{opt, refs, out.nodes, order};
+  out.nodes.reserve(n ? 2 * (size_t)n / std::max(1u, opt.max_leaf) + 4 : 4);
+  if (n == 0) {
+    rpl::Node2 root{};
+    for (int s = 0; s < 2; s++) { root.child[s] = -1; root.count[s] = 0; }
+    out.nodes.push_back(root);
+  } else {
+    Box all;
+    all.reset();
+    for (auto& r : refs) all.grow(r.box);
+    uint32_t m = B.split(0, n, all);
+    if (m == 0) {
+      // Whole scene fits one leaf: root record with the leaf in slot 0 and an empty slot 1.
+      out.nodes.emplace_back();
+      Builder::Child c = B.make_leaf(0, n, all);
+      B.set_child(0, 0, c);
+      out.nodes[0].child[1] = -1;
+      out.nodes[0].count[1] = 0;
+      for (double* p : {&out.nodes[0].lo_x[1], &out.nodes[0].lo_y[1], &out.nodes[0].lo_z[1]})
+        *p = std::numeric_limits<double>::infinity();
+      for (double* p : {&out.nodes[0].hi_x[1], &out.nodes[0].hi_y[1], &out.nodes[0].hi_z[1]})
+        *p = -std::numeric_limits<double>::infinity();
+    } else {
+      B.emit_node(0, m, n, 0);
+    }
+  }
+  out.root = 0;
+  out.max_depth = B.max_depth;
+  out.n_leaves = B.n_leaves;
+
+  // ---- primitives in leaf order
+  out.prims.resize(order.size() ? order.size() : 1);
+  std::memset(out.prims.data(), 0, sizeof(rpl::Prim) * out.prims.size());
+  for (size_t k = 0; k < order.size(); k++) {
+    const rp_hittable& h = d->hittables[order[k]];
+    rpl::Prim& p = out.prims[k];
+    p.src = order[k];
+    if (h.kind == RP_HITTABLE_SPHERE) {
+      p.kind = rpl::PRIM_SPHERE;
+      p.material = h.material;
+      for (int c = 0; c < 3; c++) p.g[c] = h.center[c];
+      p.g[3] = h.radius;
+    } else {
+      const rp_mesh& m = d->meshes[h.mesh];
+      uint32_t i0 = m.indices[h.triangle], i1 = m.indices[h.triangle + 1], i2 = m.indices[h.triangle + 2];
+      const double* a = m.positions + 3 * (size_t)i0;
+      const double* b = m.positions + 3 * (size_t)i1;
+      const double* c = m.positions + 3 * (size_t)i2;
+      p.kind = rpl::PRIM_TRIANGLE;
+      p.material = m.material;
+      for (int k2 = 0; k2 < 3; k2++) {
+        p.g[k2] = a[k2];
+        p.g[3 + k2] = a[k2] - b[k2];  // ba, hittable.rs:71 (same IEEE subtraction as on the device)
+        p.g[6 + k2] = a[k2] - c[k2];  // ca, hittable.rs:72
+      }
+      p.v[0] = (uint32_t)(vbase[h.mesh] + i0);
+      p.v[1] = (uint32_t)(vbase[h.mesh] + i1);
+      p.v[2] = (uint32_t)(vbase[h.mesh] + i2);
+    }
+  }
+  return RP_OK;
+}
+
+int check(const PackedScene& s, std::string& err) {
+  size_t np = 0;
+  std::vector<uint8_t> used(s.prims.size(), 0);
+  std::vector<uint8_t> visited(s.nodes.size(), 0);
+  struct Item { uint32_t node; uint32_t depth; };
+  std::vector<Item> st{{s.root, 0}};
+  while (!st.empty()) {
+    Item it = st.back();
+    st.pop_back();
+    if (it.node >= s.nodes.size()) { err = "node index out of range"; return RP_EINTERNAL; }
+    if (visited[it.node]) { err = "node visited twice"; return RP_EINTERNAL; }
+    visited[it.node] = 1;
+    if (it.depth > s.max_depth) { err = "depth exceeds max_depth"; return RP_EINTERNAL; }
+    const rpl::Node2& n = s.nodes[it.node];
+    for (int c = 0; c < 2; c++) {
+      if (n.count[c] == 0) {
+        if (n.child[c] < 0) continue;
+        const rpl::Node2& ch = s.nodes[(size_t)n.child[c]];
+        for (int g = 0; g < 2; g++) {
+          if (ch.count[g] == 0 && ch.child[g] < 0) continue;
+          if (ch.lo_x[g] < n.lo_x[c] || ch.lo_y[g] < n.lo_y[c] || ch.lo_z[g] < n.lo_z[c] ||
+              ch.hi_x[g] > n.hi_x[c] || ch.hi_y[g] > n.hi_y[c] || ch.hi_z[g] > n.hi_z[c]) {
+            err = "child box not contained in parent slot";
+            return RP_EINTERNAL;
+          }
+        }
+        st.push_back({(uint32_t)n.child[c], it.depth + 1});
+      } else {
+        for (uint32_t k = 0; k < n.count[c]; k++) {
+          size_t pi = (size_t)n.child[c] + k;
+          if (pi >= s.prims.size() || used[pi]) { err = "primitive referenced twice or out of range"; return RP_EINTERNAL; }
+          used[pi] = 1;
+          np++;
+          const rpl::Prim& p = s.prims[pi];
+          double lo[3], hi[3];
+          if (p.kind == rpl::PRIM_SPHERE) {
+            for (int q = 0; q < 3; q++) { lo[q] = p.g[q] - p.g[3]; hi[q] = p.g[q] + p.g[3]; }
+          } else {
+            for (int q = 0; q < 3; q++) {
+              double a = p.g[q], b = a - p.g[3 + q], cc = a - p.g[6 + q];
+              // a - (a - b) may differ from b by rounding; allow that slack in the check only.
+              lo[q] = std::fmin(std::fmin(a, b), cc);
+              hi[q] = std::fmax(std::fmax(a, b), cc);
+              double slack = 4.0 * std::numeric_limits<double>::epsilon() * (std::fabs(a) + std::fabs(p.g[3 + q]) + std::fabs(p.g[6 + q]));
+              lo[q] += slack;
+              hi[q] -= slack;
+            }
+          }
+          if (lo[0] < n.lo_x[c] || lo[1] < n.lo_y[c] || lo[2] < n.lo_z[c] || hi[0] > n.hi_x[c] ||
+              hi[1] > n.hi_y[c] || hi[2] > n.hi_z[c]) {
+            err = "primitive outside its leaf box";
+            return RP_EINTERNAL;
+          }
+        }
+      }
+    }
+  }
+  size_t real = 0;
+  for (auto& p : s.prims) (void)p, real++;
+  if (np != real && !(np == 0 && s.prims.size() == 1)) {
+    err = "primitive count mismatch";
+    return RP_EINTERNAL;
+  }
+  return RP_OK;
+}
+
+}  // namespace rpb

@@ -1,0 +1,49 @@
+// rp_kernel.h -- host-visible interface of the HIP kernels (rp_kernel.hip).  No HIP types.
+#pragma once
+#include <stdint.h>
+
+#include "rp_layout.h"
+
+namespace rpk {
+
+struct KScene {
+  const rpl::Node2* nodes;
+  const rpl::Prim* prims;
+  const double* vnrm;
+  const double* vuv;
+  const rpl::Material* mats;
+  const rpl::Texture* texs;
+  const uint32_t* texels;
+  rpl::Emit background;
+  uint32_t root;
+  uint32_t stack_depth;  // LDS traversal stack entries per lane (>= max_depth + 2)
+};
+
+struct KParams {
+  double orient[9];
+  double pos[3];
+  double aspect, tan_fov, focal, lens;
+  uint64_t seed;
+  uint32_t W, H, spp, max_bounce;
+  uint32_t tw, th, shard, nshards;
+  uint32_t tiles_x, n_shard_tiles;
+  uint64_t n_slots;  // n_shard_tiles * tw * th
+};
+
+// Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.
+enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_QUEUE = 4, CTR_N = 8 };
+enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
+
+// Launch the persistent render kernel on `stream` (hipStream_t).  `counters` must have been zeroed on
+// the same stream.  Returns a hipError_t as int.
+int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
+                  int grid, void* stream);
+
+// Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
+int render_blocks_per_cu(uint32_t stack_depth, int* blocks);
+
+// Closest-hit query kernel (one ray per thread).
+int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,
+                     uint64_t* counters, void* stream);
+
+}  // namespace rpk

@@ -1,0 +1,691 @@
+// rp_kernel.hip -- gfx950 path-tracing megakernel (the hot path of alucas2/raytracing-potato).
+//
+// One lane = one pixel's path state.  Each lane loops
+//     [fetch pixel] -> [new sample: jitter + Camera::shoot] -> traverse -> shade -> ...
+// as a single flat loop (path regeneration), so every live lane of a wave executes the SAME traversal
+// code each iteration whatever bounce or sample it is on; lanes that finish a pixel refetch from a
+// device-wide atomic queue (persistent threads; the compiler folds the per-lane atomicAdd into one
+// wave atomic via ballot + mbcnt).  Traversal stacks live in LDS, lane-major ([depth][lane]) so a
+// wave's push/pop is bank-conflict-free whatever depth each lane is at.
+//
+// Arithmetic is IEEE binary64 in the reference's exact operation order (no contraction: this file is
+// compiled with -ffp-contract=off and the pragma below), so paths -- and the RNG draws they consume --
+// are the reference's.  References: render.rs:32-146, bvh.rs:93-124, hittable.rs:39-108,
+// material.rs:27-179, texture.rs:21-118, randomness.rs:9-110, utility.rs:67-154.
+#include <hip/hip_runtime.h>
+
+#include "rp_kernel.h"
+
+#pragma clang fp contract(off)
+
+namespace rpk {
+
+#define RPK_INLINE __device__ __forceinline__
+
+static constexpr int BLOCK = 256;
+static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
+static constexpr double SMOL = 1e-7;         // utility.rs:31
+static constexpr double PI_ = 3.14159265358979323846;
+static constexpr double TAU_ = 6.28318530717958647692;
+static constexpr double INF = __builtin_huge_val();
+
+// ------------------------------------------------------------------ RNG (rand 0.8 StdRng) -------
+
+RPK_INLINE uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+#define RPK_QR(a, b, c, d)              \
+  a += b; d ^= a; d = rotl(d, 16);      \
+  c += d; b ^= c; b = rotl(b, 12);      \
+  a += b; d ^= a; d = rotl(d, 8);       \
+  c += d; b ^= c; b = rotl(b, 7);
+
+// ChaCha12 block (rand_chacha 0.3: 64-bit block counter in words 12-13, zero nonce).
+RPK_INLINE void chacha12(const uint32_t k[8], uint32_t ctr, uint32_t o[16]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = ctr, x13 = 0, x14 = 0, x15 = 0;
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    RPK_QR(x0, x4, x8, x12);
+    RPK_QR(x1, x5, x9, x13);
+    RPK_QR(x2, x6, x10, x14);
+    RPK_QR(x3, x7, x11, x15);
+    RPK_QR(x0, x5, x10, x15);
+    RPK_QR(x1, x6, x11, x12);
+    RPK_QR(x2, x7, x8, x13);
+    RPK_QR(x3, x4, x9, x14);
+  }
+  o[0] = x0 + 0x61707865u; o[1] = x1 + 0x3320646eu; o[2] = x2 + 0x79622d32u; o[3] = x3 + 0x6b206574u;
+  o[4] = x4 + k[0]; o[5] = x5 + k[1]; o[6] = x6 + k[2]; o[7] = x7 + k[3];
+  o[8] = x8 + k[4]; o[9] = x9 + k[5]; o[10] = x10 + k[6]; o[11] = x11 + k[7];
+  o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
+}
+
+// rand_core 0.6 seed_from_u64: PCG32 expansion of the u64 into the 8 key words.
+RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    state = state * 6364136223846793005ull + 11634580027462260723ull;
+    uint32_t xs = (uint32_t)(((state >> 18) ^ state) >> 27);
+    uint32_t rot = (uint32_t)(state >> 59);
+    key[c] = (xs >> rot) | (xs << ((32 - rot) & 31));
+  }
+}
+
+// Main stream of one pixel.  All draws on the path are u64 (Standard f64), so consuming the keystream
+// one 16-word block at a time yields exactly rand_chacha's 4-block-buffered stream.  The current block
+// lives in LDS (8 u64 per lane, lane-major: a wave's ds_read_b64 is conflict-free whatever word each
+// lane is at), which keeps 16 VGPRs out of the traversal's register budget.
+struct Rng {
+  uint32_t key[8];
+  uint32_t ctr;         // next block
+  uint32_t idx;         // next u64 in the block, 8 = empty
+  uint64_t* buf;        // LDS: buf[k * BLOCK] = k-th u64 of the current block
+};
+
+RPK_INLINE uint64_t next_u64(Rng& r) {
+  if (r.idx >= 8) {
+    uint32_t b[16];
+    chacha12(r.key, r.ctr, b);
+#pragma unroll
+    for (int k = 0; k < 8; k++) r.buf[k * BLOCK] = ((uint64_t)b[2 * k + 1] << 32) | b[2 * k];
+    r.ctr++;
+    r.idx = 0;
+  }
+  return r.buf[(r.idx++) * BLOCK];
+}
+
+// rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
+RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
+RPK_INLINE double gen_f64(Rng& r) { return u64_to_f64(next_u64(r)); }
+
+// ------------------------------------------------------------------ math -------------------------
+
+struct V3 { double x, y, z; };
+RPK_INLINE V3 v3(double x, double y, double z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+RPK_INLINE V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RPK_INLINE V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RPK_INLINE V3 mulc(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RPK_INLINE V3 smul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+RPK_INLINE double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }    // nalgebra dot
+RPK_INLINE double norm2(V3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }         // norm_squared
+RPK_INLINE V3 normalize(V3 a) { double n = sqrt(norm2(a)); return v3(a.x / n, a.y / n, a.z / n); }
+RPK_INLINE V3 reflect(V3 i, V3 n) { return sub(i, smul(2.0 * dot(i, n), n)); }         // utility.rs:106
+
+// Rust `as` casts saturate, NaN -> 0
+RPK_INLINE uint32_t sat_u32(double x) {
+  if (!(x > 0.0)) return 0u;
+  if (x >= 4294967295.0) return 4294967295u;
+  return (uint32_t)x;
+}
+RPK_INLINE int64_t sat_i64(double x) {
+  if (x != x) return 0;
+  if (x >= 9223372036854775807.0) return INT64_MAX;
+  if (x <= -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)x;
+}
+
+// randomness.rs:91-105 (wrapping isize, arithmetic >> 13)
+RPK_INLINE int64_t noise_integer(int64_t x, int64_t y, int64_t z, int64_t seed) {
+  uint64_t h = 0x369E6D3B899E43CFull * (uint64_t)x + 0x53F89E7FFDA3B07Dull * (uint64_t)y +
+               0x3B13C1CA4937E629ull * (uint64_t)z + 0x577C2C6E4019D645ull * (uint64_t)seed;
+  h = (uint64_t)((int64_t)h >> 13) ^ h;
+  h = h * (h * h * 60493ull + 19990303ull) + 1376312589ull;
+  return (int64_t)h;
+}
+RPK_INLINE double noise_real(int64_t x, int64_t y, int64_t z, int64_t seed) {
+  return (double)noise_integer(x, y, z, seed) / 9223372036854775807.0;
+}
+
+// ------------------------------------------------------------------ traversal --------------------
+
+struct HitRec {
+  double t, u, v;  // u, v: barycentrics of hittable.rs:89-95 (triangles)
+  int32_t prim;    // -1 = miss
+};
+
+// Closest hit over the BVH (Hittable::Bvh::hit, bvh.rs:121-124 / hit_node bvh.rs:93-119).  Every
+// primitive is box-tested (in its parent's record) before its exact test, as the reference does, and
+// t_max shrinks to the closest hit so far; acceptance is `t <= t_max`, so an equal-t primitive tested
+// later wins (hittable.rs:52,99).  stk: this lane's LDS stack column, entries `stride` apart.
+RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
+                         HitRec& hr, bool& overflow) {
+  const double ix = 1.0 / d.x, iy = 1.0 / d.y, iz = 1.0 / d.z;  // utility.rs:71-77 expand
+  double best = tmax;
+  int32_t bestp = -1;
+  double bu = 0.0, bv = 0.0;
+  uint32_t node = S.root;
+  uint32_t sp = 0;
+  for (;;) {
+    const rpl::Node2* n = S.nodes + node;
+    const double2 lx = *reinterpret_cast<const double2*>(n->lo_x);
+    const double2 hx = *reinterpret_cast<const double2*>(n->hi_x);
+    const double2 ly = *reinterpret_cast<const double2*>(n->lo_y);
+    const double2 hy = *reinterpret_cast<const double2*>(n->hi_y);
+    const double2 lz = *reinterpret_cast<const double2*>(n->lo_z);
+    const double2 hz = *reinterpret_cast<const double2*>(n->hi_z);
+    const int4 cc = *reinterpret_cast<const int4*>(n->child);  // child[0], child[1], count[0], count[1]
+    // AABB::collide for both children (utility.rs:137-154), f64 min/max ignore NaN (0 * inf)
+    double a0 = (lx.x - o.x) * ix, b0 = (hx.x - o.x) * ix;
+    double a1 = (ly.x - o.y) * iy, b1 = (hy.x - o.y) * iy;
+    double a2 = (lz.x - o.z) * iz, b2 = (hz.x - o.z) * iz;
+    const double tn0 = fmax(fmax(fmax(tmin, fmin(a0, b0)), fmin(a1, b1)), fmin(a2, b2));
+    const double tf0 = fmin(fmin(fmin(best, fmax(a0, b0)), fmax(a1, b1)), fmax(a2, b2));
+    a0 = (lx.y - o.x) * ix; b0 = (hx.y - o.x) * ix;
+    a1 = (ly.y - o.y) * iy; b1 = (hy.y - o.y) * iy;
+    a2 = (lz.y - o.z) * iz; b2 = (hz.y - o.z) * iz;
+    const double tn1 = fmax(fmax(fmax(tmin, fmin(a0, b0)), fmin(a1, b1)), fmin(a2, b2));
+    const double tf1 = fmin(fmin(fmin(best, fmax(a0, b0)), fmax(a1, b1)), fmax(a2, b2));
+    const bool h0 = tf0 >= tn0 && (cc.z != 0 || cc.x >= 0);
+    const bool h1 = tf1 >= tn1 && (cc.w != 0 || cc.y >= 0);
+    // Leaves: exact primitive tests now.
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+      const bool hc = c == 0 ? h0 : h1;
+      const uint32_t cnt = (uint32_t)(c == 0 ? cc.z : cc.w);
+      if (!(hc && cnt)) continue;
+      const uint32_t first = (uint32_t)(c == 0 ? cc.x : cc.y);
+      for (uint32_t k = first; k < first + cnt; k++) {
+        const rpl::Prim* p = S.prims + k;
+        const double2 g01 = *reinterpret_cast<const double2*>(p->g);
+        const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
+        const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
+        const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
+        const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
+        const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+        if (kind == rpl::PRIM_TRIANGLE) {
+          // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
+          const V3 a = v3(g01.x, g01.y, g23.x);
+          const V3 ba = v3(g23.y, g45.x, g45.y);
+          const V3 ca = v3(g67.x, g67.y, g8k.x);
+          const V3 pa = sub(a, o);
+          const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                           - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
+          if (fabs(det) < SMOL) continue;
+          const double inv_det = 1.0 / det;
+          const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                          + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                          + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+          const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                          + pa.y * (ca.z * d.x - ca.x * d.z)
+                          + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+          const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                          + pa.y * (ba.x * d.z - ba.z * d.x)
+                          + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
+          const double w = 1.0 - u - v;
+          if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
+          best = t; bestp = (int32_t)k; bu = u; bv = v;
+        } else {
+          // hittable.rs:39-57
+          const V3 c = v3(g01.x, g01.y, g23.x);
+          const double radius = g23.y;
+          const V3 tc = sub(o, c);
+          const double a = norm2(d);
+          const double half_b = dot(d, tc);
+          const double cq = norm2(tc) - radius * radius;
+          const double delta = half_b * half_b - a * cq;
+          if (delta <= 0.0) continue;
+          const double sq = sqrt(delta);
+          double t = (-half_b - sq) / a;
+          if (t < tmin || t > best) {
+            t = (-half_b + sq) / a;
+            if (t < tmin || t > best) continue;
+          }
+          best = t; bestp = (int32_t)k;
+        }
+      }
+    }
+    const bool i0 = h0 && cc.z == 0;
+    const bool i1 = h1 && cc.w == 0;
+    if (i0 && i1) {
+      const bool near0 = tn0 <= tn1;
+      const uint32_t nearc = (uint32_t)(near0 ? cc.x : cc.y);
+      const uint32_t farc = (uint32_t)(near0 ? cc.y : cc.x);
+      if (sp < S.stack_depth) {
+        stk[sp * stride] = farc;
+        sp++;
+      } else {
+        overflow = true;
+      }
+      node = nearc;
+    } else if (i0) {
+      node = (uint32_t)cc.x;
+    } else if (i1) {
+      node = (uint32_t)cc.y;
+    } else {
+      if (sp == 0) break;
+      sp--;
+      node = stk[sp * stride];
+    }
+  }
+  hr.t = best;
+  hr.u = bu;
+  hr.v = bv;
+  hr.prim = bestp;
+}
+
+// Hit record of the closest primitive (hittable.rs:59-62, 103-107).
+struct Surf {
+  V3 p, n;
+  double u, v;
+  uint32_t material;
+};
+
+RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s) {
+  const rpl::Prim* p = S.prims + hr.prim;
+  s.p = add(o, smul(hr.t, d));  // Ray::at (utility.rs:67)
+  s.material = p->material;
+  if (p->kind == rpl::PRIM_TRIANGLE) {
+    const double u = hr.u, v = hr.v, w = 1.0 - u - v;
+    const uint32_t i0 = p->v[0], i1 = p->v[1], i2 = p->v[2];
+    const V3 n0 = v3(S.vnrm[3 * i0], S.vnrm[3 * i0 + 1], S.vnrm[3 * i0 + 2]);
+    const V3 n1 = v3(S.vnrm[3 * i1], S.vnrm[3 * i1 + 1], S.vnrm[3 * i1 + 2]);
+    const V3 n2 = v3(S.vnrm[3 * i2], S.vnrm[3 * i2 + 1], S.vnrm[3 * i2 + 2]);
+    s.n = add(add(smul(w, n0), smul(u, n1)), smul(v, n2));
+    s.u = (w * S.vuv[2 * i0] + u * S.vuv[2 * i1]) + v * S.vuv[2 * i2];
+    s.v = (w * S.vuv[2 * i0 + 1] + u * S.vuv[2 * i1 + 1]) + v * S.vuv[2 * i2 + 1];
+  } else {
+    const V3 c = v3(p->g[0], p->g[1], p->g[2]);
+    s.n = normalize(sub(s.p, c));
+    s.u = 0.5 - atan2(s.n.z, s.n.x) / TAU_;
+    s.v = asin(s.n.y) / PI_ + 0.5;
+  }
+}
+
+// ------------------------------------------------------------------ shading ----------------------
+
+// texture.rs:21-118 (Checker recursion unrolled into a walk; validate() guarantees it terminates)
+RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
+  for (;;) {
+    const rpl::Texture& t = S.texs[tid];
+    switch (t.kind) {
+      case 1:  // DebugUVs
+        return v3(h.u, h.v, 0.0);
+      case 2:  // Solid
+        return v3(t.color[0], t.color[1], t.color[2]);
+      case 3: {  // Image (texture.rs:40-49): clamp then saturating `as u32`
+        const double w = (double)t.width, hh = (double)t.height;
+        double x = h.u * w, y = h.v * hh;
+        if (x < 0.0) x = 0.0;
+        if (x > w - 1.0) x = w - 1.0;
+        if (y < 0.0) y = 0.0;
+        if (y > hh - 1.0) y = hh - 1.0;
+        const uint32_t i = sat_u32(x), j = sat_u32(y);
+        const uint32_t px = S.texels[t.texel_offset + (uint64_t)i + (uint64_t)j * t.width];
+        return v3((double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0,
+                  (double)((px >> 16) & 0xffu) / 255.0);
+      }
+      case 4: {  // Checker (texture.rs:51-60)
+        const double s = floor(h.p.x) + floor(h.p.y) + floor(h.p.z);
+        tid = fmod(s, 2.0) == 0.0 ? t.even : t.odd;
+        continue;
+      }
+      case 5: {  // Noise (texture.rs:62-68)
+        double x = noise_real(sat_i64(floor(h.p.x)), sat_i64(floor(h.p.y)), sat_i64(floor(h.p.z)), t.seed);
+        x = 0.5 * x + 0.5;
+        return v3(x, x, x);
+      }
+      case 6: {  // Perlin (texture.rs:83-118)
+        const V3 p = h.p;
+        const V3 fp = v3(floor(p.x), floor(p.y), floor(p.z));
+        const int64_t fx = sat_i64(fp.x), fy = sat_i64(fp.y), fz = sat_i64(fp.z);
+        const int64_t cx = (int64_t)((uint64_t)fx + 1), cy = (int64_t)((uint64_t)fy + 1),
+                      cz = (int64_t)((uint64_t)fz + 1);
+        const int64_t s1 = (int64_t)((uint64_t)t.seed + 1), s2 = (int64_t)((uint64_t)t.seed + 2),
+                      s3 = (int64_t)((uint64_t)t.seed + 3);
+        double k[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int64_t X = (q & 1) ? cx : fx, Y = (q & 2) ? cy : fy, Z = (q & 4) ? cz : fz;
+          const V3 g = v3(noise_real(X, Y, Z, s1), noise_real(X, Y, Z, s2), noise_real(X, Y, Z, s3));
+          k[q] = dot(sub(p, v3((double)X, (double)Y, (double)Z)), g);
+        }
+        V3 tt = sub(p, fp);
+        tt.x = (tt.x * (tt.x * 6.0 - 15.0) + 10.0) * tt.x * tt.x * tt.x;
+        tt.y = (tt.y * (tt.y * 6.0 - 15.0) + 10.0) * tt.y * tt.y * tt.y;
+        tt.z = (tt.z * (tt.z * 6.0 - 15.0) + 10.0) * tt.z * tt.z * tt.z;
+        const double k12 = (k[1] - k[0]) * tt.x + k[0], k34 = (k[3] - k[2]) * tt.x + k[2];
+        const double k56 = (k[5] - k[4]) * tt.x + k[4], k78 = (k[7] - k[6]) * tt.x + k[6];
+        const double k1234 = (k34 - k12) * tt.y + k12, k5678 = (k78 - k56) * tt.y + k56;
+        const double kk = (k5678 - k1234) * tt.z + k1234;
+        const double x = 0.5 * kk + 0.5;
+        return v3(x, x, x);
+      }
+      default:  // Missing
+        return v3(0.0, 0.0, 0.0);
+    }
+  }
+}
+
+// material.rs:49-60 Emit::evaluate
+RPK_INLINE V3 emit_eval(const KScene& S, uint32_t kind, uint32_t tex, const double* color, V3 d, const Surf& h) {
+  switch (kind) {
+    case 1: return h.n;                                  // DebugNormals
+    case 2: return v3(color[0], color[1], color[2]);     // Color
+    case 3: {                                            // SkyGradient
+      const double t = 0.5 * (d.y / sqrt(norm2(d)) + 1.0);
+      return add(smul(1.0 - t, v3(1.0, 1.0, 1.0)), smul(t, v3(0.5, 0.7, 1.0)));
+    }
+    case 4: return tex_sample(S, tex, h);                // SkySphere
+    default: return v3(0.0, 0.0, 0.0);                   // None
+  }
+}
+
+// material.rs:74-81 Absorb::evaluate
+RPK_INLINE V3 absorb_eval(const KScene& S, const rpl::Material& m, const Surf& h) {
+  switch (m.absorb_kind) {
+    case 1: return v3(1.0, 1.0, 1.0);
+    case 2: return v3(m.absorb_color[0], m.absorb_color[1], m.absorb_color[2]);
+    case 3: return tex_sample(S, m.absorb_tex, h);
+    default: return v3(0.0, 0.0, 0.0);
+  }
+}
+
+// material.rs:27-34, 115-179 Scatter::evaluate.  Returns true and the new direction when scattered.
+RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, V3& nd) {
+  switch (m.scatter_kind) {
+    case 1: {  // Lambert (material.rs:115-130)
+      if (dot(h.n, d) > 0.0) return false;
+      double x, y, s;
+      do {  // UnitSphere (randomness.rs:58-73)
+        x = 2.0 * gen_f64(rng) - 1.0;
+        y = 2.0 * gen_f64(rng) - 1.0;
+        s = x * x + y * y;
+      } while (!(s < 1.0));
+      const double q = 2.0 * sqrt(1.0 - s);
+      nd = normalize(add(h.n, v3(x * q, y * q, 1.0 - 2.0 * s)));
+      return true;
+    }
+    case 2: {  // Metal (material.rs:132-152)
+      if (dot(h.n, d) > 0.0) return false;
+      double x, y, z;
+      do {  // UnitBall (randomness.rs:39-53)
+        x = 2.0 * gen_f64(rng) - 1.0;
+        y = 2.0 * gen_f64(rng) - 1.0;
+        z = 2.0 * gen_f64(rng) - 1.0;
+      } while (!((x * x + y * y) + z * z < 1.0));
+      const V3 r = normalize(add(reflect(d, h.n), smul(m.scatter_param, v3(x, y, z))));
+      if (dot(h.n, r) < 0.0) return false;
+      nd = r;
+      return true;
+    }
+    case 3: {  // Dielectric (material.rs:154-179)
+      double eta;
+      V3 n;
+      if (dot(h.n, d) > 0.0) { eta = m.scatter_param; n = v3(-h.n.x, -h.n.y, -h.n.z); }
+      else { eta = 1.0 / m.scatter_param; n = h.n; }
+      double r0 = (1.0 - eta) / (1.0 + eta);
+      r0 = r0 * r0;                                  // powi(2)
+      const double x = 1.0 + dot(n, d);
+      const double x2 = x * x;
+      const double reflectance = r0 + (1.0 - r0) * (x * (x2 * x2));  // powi(5), LLVM binary expansion
+      if (gen_f64(rng) < reflectance) {              // Bernoulli (randomness.rs:78-82)
+        nd = reflect(d, n);
+      } else {
+        const double cos_theta = dot(n, d);          // refract (utility.rs:111-119)
+        const double k = 1.0 - eta * eta * (1.0 - cos_theta * cos_theta);
+        if (k < 0.0) nd = reflect(d, n);
+        else nd = sub(smul(eta, d), smul(eta * cos_theta + sqrt(k), n));
+      }
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
+// ------------------------------------------------------------------ render kernel ----------------
+
+RPK_INLINE V3 matvec(const double* m, V3 v) {  // nalgebra Matrix3 * Vector3 (column axpy)
+  return v3((v.x * m[0] + v.y * m[3]) + v.z * m[6], (v.x * m[1] + v.y * m[4]) + v.z * m[7],
+            (v.x * m[2] + v.y * m[5]) + v.z * m[8]);
+}
+
+// All launch arguments in one kernarg struct.  The persistent loop re-reads the fields it needs through
+// a laundered pointer to the kernarg segment (scalar loads, served by the constant cache) instead of
+// keeping ~70 uniform values live in SGPRs for the whole kernel: that SGPR pressure otherwise spills
+// into VGPR lanes and halves the wave occupancy of this register-bound kernel.
+struct KArgs {
+  KScene S;
+  KParams P;
+  double* out;
+  float* out_fg;
+  unsigned long long* ctr;
+};
+typedef const __attribute__((address_space(4))) KArgs* KArgsPtr;
+
+RPK_INLINE KScene load_scene(KArgsPtr A) {
+  KScene S;
+  S.nodes = A->S.nodes;
+  S.prims = A->S.prims;
+  S.vnrm = A->S.vnrm;
+  S.vuv = A->S.vuv;
+  S.mats = A->S.mats;
+  S.texs = A->S.texs;
+  S.texels = A->S.texels;
+  S.background.kind = A->S.background.kind;
+  S.background.tex = A->S.background.tex;
+  S.background.color[0] = A->S.background.color[0];
+  S.background.color[1] = A->S.background.color[1];
+  S.background.color[2] = A->S.background.color[2];
+  S.root = A->S.root;
+  S.stack_depth = A->S.stack_depth;
+  return S;
+}
+
+RPK_INLINE KArgsPtr kargs() {
+  KArgsPtr p = (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+__global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
+  extern __shared__ uint32_t lds_stack[];
+  __shared__ unsigned long long blk_ctr[3];
+  __shared__ uint64_t rng_lds[8 * BLOCK];
+  if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t* stk = lds_stack + threadIdx.x;
+
+  uint32_t n_rays = 0, n_samples = 0, n_pixels = 0;
+  bool overflow = false;
+
+  // lane state
+  uint32_t slot = 0, pi = 0, pj = 0, s = 0, depth = 0;
+  bool need_pixel = true, new_sample = true, first = true;
+  Rng rng;
+  rng.buf = rng_lds + threadIdx.x;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 1), T = v3(0, 0, 0), L = v3(0, 0, 0), sum = v3(0, 0, 0);
+  uint32_t hits = 0;
+
+  for (;;) {
+    if (need_pixel) {
+      KArgsPtr A = kargs();
+      unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
+      const uint32_t tw = A->P.tw, th = A->P.th, tile_px = tw * th;
+      bool found = false;
+      while (!found) {
+        slot = atomicAdd(queue, 1u);
+        if ((uint64_t)slot >= A->P.n_slots) break;
+        const uint32_t k = slot / tile_px, local = slot - k * tile_px;
+        const uint32_t t = A->P.shard + k * A->P.nshards;
+        const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
+        pi = tx * tw + local % tw;
+        pj = ty * th + local / tw;
+        found = pi < A->P.W && pj < A->P.H;
+      }
+      if (!found) break;  // queue drained: this lane retires
+      seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);  // RNG contract
+      rng.ctr = 0;
+      rng.idx = 8;
+      s = 0;
+      sum = v3(0.0, 0.0, 0.0);
+      hits = 0;
+      need_pixel = false;
+      new_sample = true;
+    }
+    if (new_sample) {
+      KArgsPtr A = kargs();
+      // make_uv_jitter (render.rs:74-82): draws 2s, 2s+1 of a CLONE of the pixel-start stream =
+      // words 4s..4s+3 = block s/4, offset 4*(s%4).
+      uint32_t jb[16];
+      chacha12(rng.key, s >> 2, jb);
+      const uint32_t off = (s & 3u) * 4u;
+      uint32_t w0 = jb[0], w1 = jb[1], w2 = jb[2], w3 = jb[3];
+#pragma unroll
+      for (int q = 1; q < 4; q++) {
+        const bool m = off == 4u * q;
+        w0 = m ? jb[4 * q] : w0;
+        w1 = m ? jb[4 * q + 1] : w1;
+        w2 = m ? jb[4 * q + 2] : w2;
+        w3 = m ? jb[4 * q + 3] : w3;
+      }
+      const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
+      const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
+      // Camera::shoot (render.rs:32-52); tan(fov/2) computed on the host (same libm as the reference)
+      double dx, dy;
+      do {  // UnitDisk (randomness.rs:21-34), drawn even when lens_radius == 0
+        dx = 2.0 * gen_f64(rng) - 1.0;
+        dy = 2.0 * gen_f64(rng) - 1.0;
+      } while (!(dx * dx + dy * dy < 1.0));
+      A = kargs();
+      const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
+      const V3 lo = v3(lens * dx, lens * dy, 0.0);
+      const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
+      double m[9];
+#pragma unroll
+      for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
+      d = matvec(m, dl);
+      o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
+      T = v3(1.0, 1.0, 1.0);
+      L = v3(0.0, 0.0, 0.0);
+      depth = A->P.max_bounce;
+      first = true;
+      new_sample = false;
+    }
+
+    // ---- trace (every live lane) ----
+    HitRec hr;
+    {
+      KArgsPtr A = kargs();
+      const KScene S = load_scene(A);
+      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
+    }
+    n_rays++;
+    bool end_sample = true;
+    if (hr.prim >= 0) {
+      KArgsPtr A = kargs();
+      const KScene S = load_scene(A);
+      Surf h;
+      surface(S, hr, o, d, h);
+      const rpl::Material& m = S.mats[h.material];
+      V3 nd;
+      const bool scattered = scatter_eval(m, d, h, rng, nd);   // order: scatter, absorb, emit
+      const V3 ab = absorb_eval(S, m, h);
+      const V3 em = emit_eval(S, m.emit_kind, m.emit_tex, m.emit_color, d, h);
+      if (first) hits++;
+      L = add(L, mulc(T, em));  // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142)
+      if (scattered) {
+        T = mulc(T, ab);
+        o = h.p;
+        d = nd;
+        depth--;
+        end_sample = depth == 0;  // trace_path_continue(depth 0) is black (render.rs:128-131)
+      }
+    } else {
+      // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
+      KArgsPtr A = kargs();
+      const KScene S = load_scene(A);
+      Surf h;
+      h.p = d;
+      h.n = d;
+      h.u = 0.5 - atan2(d.z, d.x) / TAU_;
+      h.v = asin(d.y) / PI_ + 0.5;
+      const V3 em = emit_eval(S, S.background.kind, S.background.tex, S.background.color, d, h);
+      L = add(L, mulc(T, em));
+    }
+    first = false;
+    if (end_sample) {
+      sum = add(sum, L);  // main.rs:80
+      s++;
+      n_samples++;
+      new_sample = true;
+      KArgsPtr A = kargs();
+      if (s == A->P.spp) {   // main.rs:86-87
+        const double spp = (double)A->P.spp;
+        double* out = A->out;
+        out[3 * (uint64_t)slot + 0] = sum.x / spp;
+        out[3 * (uint64_t)slot + 1] = sum.y / spp;
+        out[3 * (uint64_t)slot + 2] = sum.z / spp;
+        if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+        n_pixels++;
+        need_pixel = true;
+      }
+    }
+  }
+
+  atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);
+  atomicAdd(&blk_ctr[1], (unsigned long long)n_samples);
+  atomicAdd(&blk_ctr[2], (unsigned long long)n_pixels);
+  unsigned long long* ctr = kargs()->ctr;
+  if (overflow) atomicOr(&ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
+  __syncthreads();
+  if (threadIdx.x < 3) atomicAdd(&ctr[CTR_RAYS + threadIdx.x], blk_ctr[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const double* __restrict__ rays, uint64_t n,
+                                                         double* __restrict__ out_hit, uint32_t* __restrict__ out_mat,
+                                                         unsigned long long* __restrict__ ctr) {
+  extern __shared__ uint32_t lds_stack[];
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const double* q = rays + 8 * i;
+  const V3 o = v3(q[0], q[1], q[2]), d = v3(q[3], q[4], q[5]);
+  const double tmin = q[6], tmax = q[7];
+  HitRec hr;
+  bool overflow = false;
+  traverse(S, lds_stack + threadIdx.x, BLOCK, o, d, tmin, tmax, hr, overflow);
+  double* oh = out_hit + 9 * i;
+  if (hr.prim >= 0) {
+    Surf h;
+    surface(S, hr, o, d, h);
+    oh[0] = hr.t; oh[1] = h.p.x; oh[2] = h.p.y; oh[3] = h.p.z;
+    oh[4] = h.n.x; oh[5] = h.n.y; oh[6] = h.n.z; oh[7] = h.u; oh[8] = h.v;
+    out_mat[i] = h.material;
+  } else {
+    oh[0] = INF;
+    for (int k = 1; k < 9; k++) oh[k] = 0.0;
+    out_mat[i] = 0xffffffffu;
+  }
+  if (overflow) atomicOr(&ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
+}
+
+int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters, int grid,
+                  void* stream) {
+  const size_t lds = (size_t)s.stack_depth * BLOCK * sizeof(uint32_t);
+  KArgs a;
+  a.S = s;
+  a.P = p;
+  a.out = out_rgb;
+  a.out_fg = out_fg;
+  a.ctr = reinterpret_cast<unsigned long long*>(counters);
+  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+int render_blocks_per_cu(uint32_t stack_depth, int* blocks) {
+  const size_t lds = (size_t)stack_depth * BLOCK * sizeof(uint32_t);
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel, BLOCK, lds);
+}
+
+int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,
+                     uint64_t* counters, void* stream) {
+  if (n == 0) return 0;
+  const size_t lds = (size_t)s.stack_depth * BLOCK * sizeof(uint32_t);
+  const uint64_t grid = (n + BLOCK - 1) / BLOCK;
+  hipLaunchKernelGGL(intersect_kernel, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s, rays, n,
+                     out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
+  return (int)hipGetLastError();
+}
+
+}  // namespace rpk

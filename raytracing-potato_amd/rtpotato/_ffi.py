@@ -1,0 +1,192 @@
+"""ctypes bindings of include/rp.h (librp.so, the HIP hot path) and include/rp_host.h (librp_host.so).
+
+librp.so must share the HIP runtime with PyTorch when both live in one process: torch's own
+libamdhip64.so is loaded under the NEEDED name "libamdhip64.so" and would not be recognised as the
+same library if librp.so (NEEDED "libamdhip64.so.7") pulled /opt/rocm's copy in first.  So `import
+torch` happens before librp.so is opened (SONAMEs match, the loader then reuses torch's runtime).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int, c_int64, c_uint8, c_uint32,
+                    c_uint64, c_void_p)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+
+RP_OK, RP_EINVAL, RP_EHIP, RP_ENOMEM, RP_ENODEV, RP_EINTERNAL = 0, -1, -2, -3, -4, -5
+RP_HITTABLE_SPHERE, RP_HITTABLE_TRIANGLE = 0, 1
+RP_SCATTER_NONE, RP_SCATTER_LAMBERT, RP_SCATTER_METAL, RP_SCATTER_DIELECTRIC = 0, 1, 2, 3
+RP_ABSORB_BLACK_BODY, RP_ABSORB_WHITE_BODY, RP_ABSORB_ALBEDO, RP_ABSORB_ALBEDO_MAP = 0, 1, 2, 3
+(RP_EMIT_NONE, RP_EMIT_DEBUG_NORMALS, RP_EMIT_COLOR, RP_EMIT_SKY_GRADIENT, RP_EMIT_SKY_SPHERE) = range(5)
+(RP_TEXTURE_MISSING, RP_TEXTURE_DEBUG_UVS, RP_TEXTURE_SOLID, RP_TEXTURE_IMAGE, RP_TEXTURE_CHECKER,
+ RP_TEXTURE_NOISE, RP_TEXTURE_PERLIN) = range(7)
+RP_ROOT_BVH, RP_ROOT_LIST = 0, 1
+RP_COUNTERS_LEN = 8  # device counter block: rays, samples, pixels, status, queue, reserved x3
+
+
+class rp_hittable(Structure):
+    _fields_ = [("kind", c_uint32), ("material", c_uint32), ("mesh", c_uint32), ("triangle", c_uint32),
+                ("center", c_double * 3), ("radius", c_double)]
+
+
+class rp_mesh(Structure):
+    _fields_ = [("n_vertices", c_uint32), ("n_indices", c_uint32), ("positions", c_void_p),
+                ("normals", c_void_p), ("uvs", c_void_p), ("indices", c_void_p), ("material", c_uint32),
+                ("reserved", c_uint32)]
+
+
+class rp_scatter(Structure):
+    _fields_ = [("kind", c_uint32), ("reserved", c_uint32), ("param", c_double)]
+
+
+class rp_absorb(Structure):
+    _fields_ = [("kind", c_uint32), ("texture", c_uint32), ("color", c_double * 3)]
+
+
+class rp_emit(Structure):
+    _fields_ = [("kind", c_uint32), ("texture", c_uint32), ("color", c_double * 3)]
+
+
+class rp_material(Structure):
+    _fields_ = [("scatter", rp_scatter), ("absorb", rp_absorb), ("emit", rp_emit)]
+
+
+class rp_texture(Structure):
+    _fields_ = [("kind", c_uint32), ("odd", c_uint32), ("even", c_uint32), ("width", c_uint32),
+                ("height", c_uint32), ("reserved", c_uint32), ("seed", c_int64), ("color", c_double * 3),
+                ("rgba", c_void_p)]
+
+
+class rp_scene_desc(Structure):
+    _fields_ = [("root_kind", c_uint32), ("n_hittables", c_uint32), ("hittables", c_void_p),
+                ("n_meshes", c_uint32), ("meshes", POINTER(rp_mesh)), ("n_materials", c_uint32),
+                ("materials", POINTER(rp_material)), ("n_textures", c_uint32),
+                ("textures", POINTER(rp_texture)), ("background", rp_emit)]
+
+
+class rp_camera(Structure):
+    _fields_ = [("aspect_ratio", c_double), ("fov", c_double), ("focal_dist", c_double),
+                ("lens_radius", c_double), ("orientation", c_double * 9), ("position", c_double * 3)]
+
+
+class rp_render_params(Structure):
+    _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_bounce", c_uint32),
+                ("seed", c_uint64), ("tile_w", c_uint32), ("tile_h", c_uint32), ("shard", c_uint32),
+                ("num_shards", c_uint32)]
+
+
+class rp_stats(Structure):
+    _fields_ = [("rays", c_uint64), ("samples", c_uint64), ("pixels", c_uint64), ("seconds", c_double)]
+
+
+class rph_mesh(Structure):
+    _fields_ = [("n_vertices", c_uint32), ("n_indices", c_uint32), ("positions", POINTER(c_double)),
+                ("normals", POINTER(c_double)), ("uvs", POINTER(c_double)), ("indices", POINTER(c_uint32))]
+
+
+# numpy dtype with exactly rp_hittable's layout (48 B), so large meshes never become Python objects
+def hittable_dtype():
+    import numpy as np
+    return np.dtype({"names": ["kind", "material", "mesh", "triangle", "center", "radius"],
+                     "formats": ["<u4", "<u4", "<u4", "<u4", ("<f8", (3,)), "<f8"],
+                     "offsets": [0, 4, 8, 12, 16, 40], "itemsize": 48})
+
+
+class RPError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"rp error {code}: {message}")
+        self.code = code
+
+
+_rp = None
+_host = None
+
+RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_create", "rp_scene_destroy",
+              "rp_scene_info", "rp_shard_pixel_count", "rp_shard_unpack", "rp_render", "rp_render_device",
+              "rp_intersect"]
+HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
+                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_last_error"]
+
+
+def rp_lib_path() -> str:
+    return os.path.join(LIB_DIR, "librp.so")
+
+
+def host_lib_path() -> str:
+    return os.path.join(LIB_DIR, "librp_host.so")
+
+
+def rp() -> ctypes.CDLL:
+    """librp.so (the HIP hot path).  Raises if it is missing: there is no CPU fallback."""
+    global _rp
+    if _rp is not None:
+        return _rp
+    path = rp_lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make -C raytracing-potato_amd` "
+                           "(or __graft_entry__.build()); there is no CPU fallback for the render path")
+    try:
+        import torch  # noqa: F401  (share torch's HIP runtime, see module docstring)
+    except Exception:
+        pass
+    lib = ctypes.CDLL(path)
+    lib.rp_abi_version.restype = c_int
+    lib.rp_last_error.restype = c_char_p
+    lib.rp_device_count.argtypes = [POINTER(c_int)]
+    lib.rp_scene_create.argtypes = [POINTER(rp_scene_desc), c_int, POINTER(c_void_p)]
+    lib.rp_scene_destroy.argtypes = [c_void_p]
+    lib.rp_scene_destroy.restype = None
+    lib.rp_scene_info.argtypes = [c_void_p, POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint32),
+                                  POINTER(c_uint64), POINTER(c_uint64)]
+    lib.rp_shard_pixel_count.argtypes = [POINTER(rp_render_params), POINTER(c_uint64)]
+    lib.rp_shard_unpack.argtypes = [POINTER(rp_render_params), c_void_p, c_uint32, c_void_p]
+    lib.rp_render.argtypes = [c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p, c_void_p,
+                              POINTER(rp_stats)]
+    lib.rp_render_device.argtypes = [c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p, c_void_p,
+                                     c_void_p, c_void_p]
+    lib.rp_intersect.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
+    _rp = lib
+    return lib
+
+
+def host() -> ctypes.CDLL:
+    global _host
+    if _host is not None:
+        return _host
+    path = host_lib_path()
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make -C raytracing-potato_amd`")
+    lib = ctypes.CDLL(path)
+    lib.rph_obj_load.argtypes = [c_char_p, POINTER(rph_mesh)]
+    lib.rph_mesh_free.argtypes = [POINTER(rph_mesh)]
+    lib.rph_mesh_free.restype = None
+    lib.rph_tga_load.argtypes = [c_char_p, POINTER(c_uint32), POINTER(c_uint32), POINTER(POINTER(c_uint8))]
+    lib.rph_tga_save.argtypes = [c_char_p, c_uint32, c_uint32, c_void_p]
+    lib.rph_free.argtypes = [c_void_p]
+    lib.rph_free.restype = None
+    lib.rph_to_srgb_u8.argtypes = [c_void_p, c_uint64, c_void_p]
+    lib.rph_to_srgb_u8.restype = None
+    lib.rph_lookat.argtypes = [c_double * 3, c_double * 3, c_double * 3, c_double * 9]
+    lib.rph_lookat.restype = None
+    lib.rph_sky_panorama.argtypes = [c_uint32, c_uint32, c_void_p]
+    lib.rph_bvh_selfcheck.argtypes = [POINTER(rp_scene_desc), POINTER(c_uint64)]
+    lib.rph_last_error.restype = c_char_p
+    _host = lib
+    return lib
+
+
+def check(code: int, lib: ctypes.CDLL | None = None) -> None:
+    if code != RP_OK:
+        lib = lib or rp()
+        fn = lib.rp_last_error if hasattr(lib, "rp_last_error") else lib.rph_last_error
+        raise RPError(code, (fn() or b"").decode(errors="replace"))
+
+
+def check_host(code: int) -> None:
+    if code != RP_OK:
+        raise RPError(code, (host().rph_last_error() or b"").decode(errors="replace"))
+
+
+__all__ = [n for n in dir() if not n.startswith("__")]

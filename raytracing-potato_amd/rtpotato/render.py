@@ -1,0 +1,108 @@
+"""render(): the drop-in for the reference's per-pixel worker loop (main.rs:61-92 calling
+render.rs:94 trace_path), on MI355X through librp.so.  No CPU fallback: a missing or failing HIP
+library raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _ffi as F
+from .scene import RenderParams, Scene, shard_slot_count
+
+
+class DeviceScene:
+    """rp_scene: the scene's acceleration structure and tables resident in one GPU's HBM."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        self.scene = scene
+        self.device = device
+        self._desc = scene.desc()
+        h = ctypes.c_void_p()
+        F.check(F.rp().rp_scene_create(self._desc.ptr(), device, ctypes.byref(h)))
+        self.handle = h
+
+    def info(self) -> dict:
+        nn, nl, np_, nb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        md = ctypes.c_uint32()
+        F.check(F.rp().rp_scene_info(self.handle, ctypes.byref(nn), ctypes.byref(nl), ctypes.byref(md),
+                                     ctypes.byref(np_), ctypes.byref(nb)))
+        return {"nodes": nn.value, "leaves": nl.value, "max_depth": md.value, "prims": np_.value,
+                "device_bytes": nb.value}
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            F.rp().rp_scene_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- synchronous host-buffer render -----------------------------------------------------------
+    def render(self, params: RenderParams, camera=None, foreground: bool = False):
+        """Full frame (only the shard's pixels written, others zero): (rgb (h, w, 3) f64,
+        foreground (h, w) f32 or None, stats dict)."""
+        cam = (camera or self.scene.camera).to_c()
+        p = params.to_c()
+        rgb = np.zeros((params.height, params.width, 3), dtype=np.float64)
+        fg = np.zeros((params.height, params.width), dtype=np.float32) if foreground else None
+        st = F.rp_stats()
+        F.check(F.rp().rp_render(self.handle, ctypes.byref(cam), ctypes.byref(p), rgb.ctypes.data,
+                                 fg.ctypes.data if fg is not None else None, ctypes.byref(st)))
+        return rgb, fg, {"rays": st.rays, "samples": st.samples, "pixels": st.pixels, "seconds": st.seconds}
+
+    # ---- asynchronous device render (torch tensors, torch's current stream) ------------------------
+    def render_device(self, params: RenderParams, out, counters, fg=None, camera=None, stream=None) -> None:
+        """Render the shard into `out` (torch f64 tensor, >= shard_slot_count*3 elements) on `stream`
+        (torch stream; default: current).  counters: torch int64 tensor of 8 elements."""
+        import torch
+        cam = (camera or self.scene.camera).to_c()
+        p = params.to_c()
+        assert out.dtype == torch.float64 and out.is_cuda and out.numel() >= 3 * shard_slot_count(params)
+        assert counters.dtype == torch.int64 and counters.numel() >= F.RP_COUNTERS_LEN
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        F.check(F.rp().rp_render_device(self.handle, ctypes.byref(cam), ctypes.byref(p), out.data_ptr(),
+                                        fg.data_ptr() if fg is not None else None, counters.data_ptr(),
+                                        ctypes.c_void_p(s.cuda_stream)))
+
+    def intersect(self, rays: np.ndarray):
+        """Hittable::hit on the root for (n, 8) rays -> ((n, 9) hits, (n,) material ids)."""
+        r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
+        hits = np.empty((len(r), 9), dtype=np.float64)
+        mats = np.empty(len(r), dtype=np.uint32)
+        F.check(F.rp().rp_intersect(self.handle, r.ctypes.data, len(r), hits.ctypes.data, mats.ctypes.data))
+        return hits, mats
+
+
+def unpack_shard(params: RenderParams, shard_buf: np.ndarray, channels: int = 3,
+                 frame: np.ndarray | None = None) -> np.ndarray:
+    """Scatter a compact shard buffer into a full (h, w, channels) frame (rp_shard_unpack)."""
+    if frame is None:
+        frame = np.zeros((params.height, params.width, channels), dtype=np.float64)
+    src = np.ascontiguousarray(shard_buf, dtype=np.float64)
+    p = params.to_c()
+    F.check(F.rp().rp_shard_unpack(ctypes.byref(p), src.ctypes.data, channels, frame.ctypes.data))
+    return frame
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    rc = F.rp().rp_device_count(ctypes.byref(n))
+    return n.value if rc == F.RP_OK else 0
+
+
+def render(scene: Scene, params: RenderParams, device: int = 0, foreground: bool = False):
+    """One-shot: upload the scene, render the frame, return (rgb, fg, stats)."""
+    with DeviceScene(scene, device) as ds:
+        return ds.render(params, foreground=foreground)
