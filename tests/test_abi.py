@@ -1,0 +1,84 @@
+"""The C-ABI libraries load on a CPU-only host and export every function their headers declare.
+(No compute call: librp.so needs a gfx950 device for that; rp_device_count must still answer.)"""
+import ctypes
+import os
+import re
+
+from conftest import PKG, REPO
+
+
+def _declared(header):
+    src = open(os.path.join(REPO, "include", header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rph?_[a-z0-9_]+)\s*\(", src)))
+
+
+def _exports(lib):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_librp_exports_all_rp_h_symbols():
+    lib = os.path.join(PKG, "lib", "librp.so")
+    names = _declared("rp.h")
+    assert "rp_render" in names and "rp_render_device" in names and len(names) >= 11
+    missing = set(names) - _exports(lib)
+    assert not missing, missing
+    from rtpotato import _ffi as F
+    assert set(F.RP_SYMBOLS) == set(names)
+
+
+def test_librp_host_exports_all_rp_host_h_symbols():
+    lib = os.path.join(PKG, "lib", "librp_host.so")
+    names = _declared("rp_host.h")
+    missing = set(names) - _exports(lib)
+    assert not missing, missing
+    from rtpotato import _ffi as F
+    assert set(F.HOST_SYMBOLS) == set(names)
+
+
+def test_librp_loads_and_reports_without_gpu():
+    from rtpotato import _ffi as F
+    L = F.rp()
+    assert L.rp_abi_version() == 1
+    n = ctypes.c_int(-1)
+    rc = L.rp_device_count(ctypes.byref(n))
+    assert rc in (F.RP_OK, F.RP_ENODEV) and n.value >= 0
+
+
+def test_struct_layouts_match_c():
+    """ctypes mirrors of rp.h structs have the C sizes (checked against a tiny C program)."""
+    import subprocess
+    import tempfile
+    from rtpotato import _ffi as F
+    code = r'''
+#include <stdio.h>
+#include "rp.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rp_hittable), sizeof(rp_mesh), sizeof(rp_material),
+         sizeof(rp_texture), sizeof(rp_scene_desc), sizeof(rp_camera), sizeof(rp_render_params), sizeof(rp_stats));
+  return 0;
+}'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(code)
+        exe = os.path.join(d, "s")
+        subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
+        sizes = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
+    ours = [ctypes.sizeof(t) for t in (F.rp_hittable, F.rp_mesh, F.rp_material, F.rp_texture, F.rp_scene_desc,
+                                        F.rp_camera, F.rp_render_params, F.rp_stats)]
+    assert sizes == ours
+    assert F.hittable_dtype().itemsize == ctypes.sizeof(F.rp_hittable)
+
+
+def test_no_oracle_in_product():
+    """The product (librp.so, the package) never links or imports the oracle."""
+    import subprocess
+    for lib in ("librp.so", "librp_host.so"):
+        out = subprocess.run(["ldd", os.path.join(PKG, "lib", lib)], capture_output=True, text=True).stdout
+        assert "oracle" not in out
+    for root, _, files in os.walk(os.path.join(PKG, "rtpotato")):
+        for f in files:
+            if f.endswith(".py"):
+                assert "oracle" not in open(os.path.join(root, f)).read().replace("no oracle", "")
