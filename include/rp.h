@@ -205,6 +205,12 @@ int rp_render_device(rp_scene* scene, const rp_camera* camera, const rp_render_p
  * out_material: n uint32 (MaterialId, 0xffffffff on a miss).  Used to test the traversal in isolation. */
 int rp_intersect(rp_scene* scene, const double* rays, uint64_t n, double* out_hit, uint32_t* out_material);
 
+/* Diagnostic counters accumulated by renders since the last reset (non-zero only in the diagnostic
+ * build lib/librp_diag.so, whose kernel carries s_memtime phase stamps): wave-cycles per phase
+ * {fetch, new sample, traverse, shade, tail}, wave loop iterations, active lanes at traversal,
+ * traversal wave-trips, lane node visits, lane primitive tests.  Synchronises the device. */
+int rp_diagnostics(rp_scene* scene, uint64_t* out, uint32_t n, int reset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,6 +53,10 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba);
  * {nodes, leaves, max_depth, primitives}. */
 int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats);
 
+/* CPU model of the device traversal over the same packed tree (diagnostics): for n rays (layout of
+ * rp_intersect) writes n x 3 {node records visited, primitive tests, closest hittable id or 2^64-1}. */
+int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray);
+
 const char* rph_last_error(void);
 
 #ifdef __cplusplus

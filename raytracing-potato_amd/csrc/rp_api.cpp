@@ -66,6 +66,7 @@ struct rp_scene {
   rpl::Texture* d_texs = nullptr;
   uint32_t* d_texels = nullptr;
   uint64_t* d_ws = nullptr;  // default counter block (8 x u64)
+  uint64_t* d_diag = nullptr;  // diagnostic counters (rpk::DIAG_N)
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
   uint32_t max_depth = 0;
   int num_cu = 0;
@@ -120,7 +121,7 @@ void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
-                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws})
+                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -154,8 +155,11 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
       (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
     return bail(rc);
-  if (hipMalloc(reinterpret_cast<void**>(&s->d_ws), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess)
+  if (hipMalloc(reinterpret_cast<void**>(&s->d_ws), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s->d_diag), sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess ||
+      hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
     return bail(fail(RP_ENOMEM, "hipMalloc workspace"));
+  s->ks.diag = s->d_diag;
   s->ks.nodes = s->d_nodes;
   s->ks.prims = s->d_prims;
   s->ks.vnrm = s->d_vnrm;
@@ -337,6 +341,17 @@ int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, doub
     stats->pixels = ctr[rpk::CTR_PIXELS];
     stats->seconds = ms * 1e-3;
   }
+  return RP_OK;
+}
+
+int rp_diagnostics(rp_scene* s, uint64_t* out, uint32_t n, int reset) {
+  if (!s || (!out && n)) return fail(RP_EINVAL, "NULL argument");
+  DeviceGuard g(s->device);
+  uint64_t buf[rpk::DIAG_N];
+  RP_HIP(hipDeviceSynchronize());
+  RP_HIP(hipMemcpy(buf, s->d_diag, sizeof buf, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n; i++) out[i] = i < (uint32_t)rpk::DIAG_N ? buf[i] : 0;
+  if (reset) RP_HIP(hipMemset(s->d_diag, 0, sizeof buf));
   return RP_OK;
 }
 

@@ -17,7 +17,13 @@ struct KScene {
   rpl::Emit background;
   uint32_t root;
   uint32_t stack_depth;  // LDS traversal stack entries per lane (>= max_depth + 2)
+  uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
 };
+
+// Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
+// tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
+// lane primitive tests.
+enum { DIAG_N = 16 };
 
 struct KParams {
   double orient[9];

@@ -22,6 +22,22 @@ namespace rpk {
 
 #define RPK_INLINE __device__ __forceinline__
 
+// Diagnostic build (-DRPK_DIAG, lib/librp_diag.so only): per-wave s_memtime phase stamps and lane
+// utilisation counters into KArgs::diag.  The product build compiles none of it.
+#ifdef RPK_DIAG
+#define DIAG(...) __VA_ARGS__
+RPK_INLINE uint64_t stamp() {
+#ifdef RPK_DIAG_NOSTAMP
+  return 0;
+#endif
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): s_memtime returns through the LGKM counter
+  return t;
+}
+#else
+#define DIAG(...)
+#endif
+
 static constexpr int BLOCK = 256;
 static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
 static constexpr double SMOL = 1e-7;         // utility.rs:31
@@ -148,8 +164,12 @@ struct HitRec {
 // primitive is box-tested (in its parent's record) before its exact test, as the reference does, and
 // t_max shrinks to the closest hit so far; acceptance is `t <= t_max`, so an equal-t primitive tested
 // later wins (hittable.rs:52,99).  stk: this lane's LDS stack column, entries `stride` apart.
+struct TravDiag {
+  uint32_t visits = 0, tests = 0, trips = 0;
+};
+
 RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
-                         HitRec& hr, bool& overflow) {
+                         HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
   const double ix = 1.0 / d.x, iy = 1.0 / d.y, iz = 1.0 / d.z;  // utility.rs:71-77 expand
   double best = tmax;
   int32_t bestp = -1;
@@ -157,6 +177,7 @@ RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, 
   uint32_t node = S.root;
   uint32_t sp = 0;
   for (;;) {
+    DIAG(if (td) td->visits++;)
     const rpl::Node2* n = S.nodes + node;
     const double2 lx = *reinterpret_cast<const double2*>(n->lo_x);
     const double2 hx = *reinterpret_cast<const double2*>(n->hi_x);
@@ -186,6 +207,7 @@ RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, 
       if (!(hc && cnt)) continue;
       const uint32_t first = (uint32_t)(c == 0 ? cc.x : cc.y);
       for (uint32_t k = first; k < first + cnt; k++) {
+        DIAG(if (td) td->tests++;)
         const rpl::Prim* p = S.prims + k;
         const double2 g01 = *reinterpret_cast<const double2*>(p->g);
         const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
@@ -451,6 +473,7 @@ struct KArgs {
   double* out;
   float* out_fg;
   unsigned long long* ctr;
+  unsigned long long* diag;  // RPK_DIAG builds only (DIAG_N counters)
 };
 typedef const __attribute__((address_space(4))) KArgs* KArgsPtr;
 
@@ -483,6 +506,8 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
   __shared__ uint64_t rng_lds[8 * BLOCK];
+  DIAG(__shared__ uint32_t wave_max[BLOCK / 64]; __shared__ unsigned long long wmax[BLOCK / 64][8];
+       if (threadIdx.x < BLOCK / 64 * 8) wmax[threadIdx.x / 8][threadIdx.x % 8] = 0;)
   if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
   __syncthreads();
   uint32_t* stk = lds_stack + threadIdx.x;
@@ -497,8 +522,10 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   rng.buf = rng_lds + threadIdx.x;
   V3 o = v3(0, 0, 0), d = v3(0, 0, 1), T = v3(0, 0, 0), L = v3(0, 0, 0), sum = v3(0, 0, 0);
   uint32_t hits = 0;
+  DIAG(uint64_t ph[5] = {0, 0, 0, 0, 0}; uint64_t iters = 0, active = 0; TravDiag td; uint64_t t_prev = stamp();)
 
   for (;;) {
+    DIAG(iters++;)
     if (need_pixel) {
       KArgsPtr A = kargs();
       unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
@@ -524,6 +551,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       need_pixel = false;
       new_sample = true;
     }
+    DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
     if (new_sample) {
       KArgsPtr A = kargs();
       // make_uv_jitter (render.rs:74-82): draws 2s, 2s+1 of a CLONE of the pixel-start stream =
@@ -564,13 +592,29 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       new_sample = false;
     }
 
+    DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; active += 1; })
     // ---- trace (every live lane) ----
     HitRec hr;
     {
       KArgsPtr A = kargs();
       const KScene S = load_scene(A);
+#ifdef RPK_DIAG
+      const uint32_t v_before = td.visits;
+#ifdef RPK_DIAG_NOTD
       traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
+#else
+      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow, &td);
+#endif
+      wave_max[threadIdx.x >> 6] = 0;
+      __builtin_amdgcn_wave_barrier();
+      atomicMax(&wave_max[threadIdx.x >> 6], td.visits - v_before);
+      __builtin_amdgcn_wave_barrier();
+      td.trips += wave_max[threadIdx.x >> 6];
+#else
+      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
+#endif
     }
+    DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
     n_rays++;
     bool end_sample = true;
     if (hr.prim >= 0) {
@@ -604,6 +648,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       const V3 em = emit_eval(S, S.background.kind, S.background.tex, S.background.color, d, h);
       L = add(L, mulc(T, em));
     }
+    DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
     first = false;
     if (end_sample) {
       sum = add(sum, L);  // main.rs:80
@@ -624,6 +669,26 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
     }
   }
 
+#ifdef RPK_DIAG
+  {
+    // per-wave maxima over lanes (a lane stops counting when it retires), then summed over waves
+    unsigned long long* dg = kargs()->diag;
+    const uint64_t t = stamp();
+    ph[4] += t - t_prev;
+    const int w = threadIdx.x >> 6;
+    for (int q = 0; q < 5; q++) atomicMax(&wmax[w][q], (unsigned long long)ph[q]);
+    atomicMax(&wmax[w][5], (unsigned long long)iters);
+    atomicMax(&wmax[w][6], (unsigned long long)td.trips);
+    atomicAdd(&dg[8], (unsigned long long)td.visits);
+    atomicAdd(&dg[9], (unsigned long long)td.tests);
+    atomicAdd(&dg[6], (unsigned long long)active);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+      for (int q = 0; q < 6; q++) atomicAdd(&dg[q], wmax[w][q]);
+      atomicAdd(&dg[7], wmax[w][6]);
+    }
+  }
+#endif
   atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);
   atomicAdd(&blk_ctr[1], (unsigned long long)n_samples);
   atomicAdd(&blk_ctr[2], (unsigned long long)n_pixels);
@@ -669,6 +734,7 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.out = out_rgb;
   a.out_fg = out_fg;
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
+  a.diag = reinterpret_cast<unsigned long long*>(s.diag);
   hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

@@ -105,9 +105,9 @@ _host = None
 
 RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_create", "rp_scene_destroy",
               "rp_scene_info", "rp_shard_pixel_count", "rp_shard_unpack", "rp_render", "rp_render_device",
-              "rp_intersect"]
+              "rp_intersect", "rp_diagnostics"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
-                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_last_error"]
+                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_last_error"]
 
 
 def rp_lib_path() -> str:
@@ -123,7 +123,7 @@ def rp() -> ctypes.CDLL:
     global _rp
     if _rp is not None:
         return _rp
-    path = rp_lib_path()
+    path = os.environ.get("RP_LIB") or rp_lib_path()  # RP_LIB: e.g. lib/librp_diag.so
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `make -C raytracing-potato_amd` "
                            "(or __graft_entry__.build()); there is no CPU fallback for the render path")
@@ -147,6 +147,7 @@ def rp() -> ctypes.CDLL:
     lib.rp_render_device.argtypes = [c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p, c_void_p,
                                      c_void_p, c_void_p]
     lib.rp_intersect.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
+    lib.rp_diagnostics.argtypes = [c_void_p, c_void_p, c_uint32, c_int]
     _rp = lib
     return lib
 
@@ -172,6 +173,7 @@ def host() -> ctypes.CDLL:
     lib.rph_lookat.restype = None
     lib.rph_sky_panorama.argtypes = [c_uint32, c_uint32, c_void_p]
     lib.rph_bvh_selfcheck.argtypes = [POINTER(rp_scene_desc), POINTER(c_uint64)]
+    lib.rph_bvh_traversal_stats.argtypes = [POINTER(rp_scene_desc), c_void_p, c_uint64, c_void_p]
     lib.rph_last_error.restype = c_char_p
     _host = lib
     return lib

@@ -1,0 +1,50 @@
+"""Diagnostic run (not a benchmark): phase breakdown of the render kernel from the RPK_DIAG build.
+
+    RP_LIB=raytracing-potato_amd/lib/librp_diag.so python tools/diag.py [--config C3] [--spp 32]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracing-potato_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--spp", type=int, default=32)
+    a = ap.parse_args()
+    os.environ.setdefault("RP_LIB", os.path.join(REPO, "raytracing-potato_amd", "lib", "librp_diag.so"))
+    from dataclasses import replace
+    from rtpotato import _ffi as F, scenes
+    from rtpotato.render import DeviceScene
+    scene, params = scenes.config_scene(a.config)
+    params = replace(params, spp=a.spp)
+    ds = DeviceScene(scene)
+    ds.render(replace(params, spp=1))  # warm
+    buf = (ctypes.c_uint64 * 16)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 16, 1))
+    _, _, st = ds.render(params)
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 16, 1))
+    d = list(buf)
+    ph = d[:5]
+    tot = sum(ph)
+    iters, active, trips, visits, tests = d[5], d[6], d[7], d[8], d[9]
+    out = {
+        "config": a.config, "spp": a.spp, "rays": st["rays"], "seconds": st["seconds"],
+        "phase_share": {k: round(v / tot, 4) for k, v in zip(["fetch", "new_sample", "traverse", "shade", "tail"], ph)},
+        "wave_iterations": iters, "lanes_active_at_traverse": round(active / max(1, iters) / 64, 4),
+        "visits_per_ray": round(visits / st["rays"], 3), "prim_tests_per_ray": round(tests / st["rays"], 3),
+        "traversal_lane_util": round(visits / max(1, trips * 64), 4),
+        "trips_per_wave_iteration": round(trips / max(1, iters), 2),
+        "wave_cycles_per_iteration": round(tot / max(1, iters), 1),
+        "traverse_cycles_per_trip": round(ph[2] / max(1, trips), 1),
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
