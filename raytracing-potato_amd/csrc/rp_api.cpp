@@ -58,7 +58,7 @@ int upload(const std::vector<T>& v, T** out) {
 struct rp_scene {
   int device = 0;
   rpk::KScene ks{};
-  rpl::Node2* d_nodes = nullptr;
+  rpl::Node4* d_nodes = nullptr;
   rpl::Prim* d_prims = nullptr;
   double* d_vnrm = nullptr;
   double* d_vuv = nullptr;
@@ -169,12 +169,13 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->ks.texels = s->d_texels;
   s->ks.background = ps.background;
   s->ks.root = ps.root;
-  s->ks.stack_depth = ps.max_depth + 2;
+  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root
+  s->ks.stack_depth = 3 * ps.max_depth + 4;
   s->n_nodes = ps.nodes.size();
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
   s->max_depth = ps.max_depth;
-  s->device_bytes = sizeof(rpl::Node2) * ps.nodes.size() + sizeof(rpl::Prim) * ps.prims.size() +
+  s->device_bytes = sizeof(rpl::Node4) * ps.nodes.size() + sizeof(rpl::Prim) * ps.prims.size() +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
   int bpc = 0;

@@ -38,29 +38,20 @@ struct Ref {
   uint32_t id;
 };
 
+// Binary SAH tree (intermediate): built top-down with binned SAH, then collapsed into 4-wide nodes.
+struct BinNode {
+  Box box;
+  int32_t left = -1, right = -1;  // inner: children indices
+  uint32_t first = 0, count = 0;  // leaf: primitives [first, first + count) of `order`
+  bool leaf() const { return count > 0; }
+};
+
 struct Builder {
   const BuildOptions& opt;
   std::vector<Ref>& refs;
-  std::vector<rpl::Node2>& nodes;
+  std::vector<BinNode>& bin;
   std::vector<uint32_t>& order;  // leaf-ordered hittable ids
-  uint32_t max_depth = 0;
   uint64_t n_leaves = 0;
-
-  struct Child {
-    Box box;
-    int32_t child;
-    uint32_t count;
-  };
-
-  Child make_leaf(uint32_t b, uint32_t e, const Box& box) {
-    Child c;
-    c.box = box;
-    c.child = (int32_t)order.size();
-    c.count = e - b;
-    for (uint32_t i = b; i < e; i++) order.push_back(refs[i].id);
-    n_leaves++;
-    return c;
-  }
 
   // Returns the split position m in (b, e) or b when the range should be a leaf.
   uint32_t split(uint32_t b, uint32_t e, const Box& box) {
@@ -139,40 +130,90 @@ struct Builder {
     return m;
   }
 
-  // Builds range [b, e) whose box is `box`; returns its child descriptor for the parent.
-  Child build(uint32_t b, uint32_t e, const Box& box, uint32_t depth) {
-    uint32_t m = split(b, e, box);
-    if (m == b) return make_leaf(b, e, box);
-    Child c;
-    c.box = box;
-    c.count = 0;
-    c.child = (int32_t)nodes.size();
-    emit_node(b, m, e, depth);
-    return c;
-  }
-
-  void emit_node(uint32_t b, uint32_t m, uint32_t e, uint32_t depth) {
-    if (depth > max_depth) max_depth = depth;
-    uint32_t self = (uint32_t)nodes.size();
-    nodes.emplace_back();
+  // Builds range [b, e) whose box is `box` into bin[]; returns its index.
+  int32_t build(uint32_t b, uint32_t e, const Box& box) {
+    const int32_t self = (int32_t)bin.size();
+    bin.emplace_back();
+    bin[self].box = box;
+    const uint32_t m = split(b, e, box);
+    if (m == b) {
+      bin[self].first = (uint32_t)order.size();
+      bin[self].count = e - b;
+      for (uint32_t i = b; i < e; i++) order.push_back(refs[i].id);
+      n_leaves++;
+      return self;
+    }
     Box lb, rb;
     lb.reset();
     rb.reset();
     for (uint32_t i = b; i < m; i++) lb.grow(refs[i].box);
     for (uint32_t i = m; i < e; i++) rb.grow(refs[i].box);
-    Child l = build(b, m, lb, depth + 1);
-    Child r = build(m, e, rb, depth + 1);
-    set_child(self, 0, l);
-    set_child(self, 1, r);
+    const int32_t l = build(b, m, lb);
+    const int32_t r = build(m, e, rb);
+    bin[self].left = l;
+    bin[self].right = r;
+    return self;
   }
+};
 
-  void set_child(uint32_t node, int slot, const Child& c) {
-    rpl::Node2& n = nodes[node];
-    n.lo_x[slot] = c.box.lo[0]; n.hi_x[slot] = c.box.hi[0];
-    n.lo_y[slot] = c.box.lo[1]; n.hi_y[slot] = c.box.hi[1];
-    n.lo_z[slot] = c.box.lo[2]; n.hi_z[slot] = c.box.hi[2];
-    n.child[slot] = c.child;
-    n.count[slot] = c.count;
+// f64 -> f32 rounded towards -inf / +inf (conservative box bounds)
+float down32(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+  return f;
+}
+float up32(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+  return f;
+}
+
+// Collapse the binary tree into 4-wide nodes: each wide node takes its binary node's two children and
+// repeatedly opens the inner child of largest surface area until it has 4 children (Wald et al.).
+struct Collapser {
+  const std::vector<BinNode>& bin;
+  std::vector<rpl::Node4>& out;
+  uint32_t max_depth = 0;
+
+  uint32_t emit(int32_t bi, uint32_t depth) {
+    if (depth > max_depth) max_depth = depth;
+    const uint32_t self = (uint32_t)out.size();
+    out.emplace_back();
+    std::vector<int32_t> kids;
+    if (bin[bi].leaf()) {
+      kids.push_back(bi);  // root that is a single leaf
+    } else {
+      kids = {bin[bi].left, bin[bi].right};
+      while (kids.size() < 4) {
+        int best = -1;
+        double area = -1.0;
+        for (size_t k = 0; k < kids.size(); k++)
+          if (!bin[kids[k]].leaf() && bin[kids[k]].box.area() > area) { area = bin[kids[k]].box.area(); best = (int)k; }
+        if (best < 0) break;
+        const int32_t open = kids[best];
+        kids[best] = bin[open].left;
+        kids.push_back(bin[open].right);
+      }
+    }
+    uint32_t entries[4];
+    for (int c = 0; c < 4; c++) {
+      rpl::Node4& n = out[self];
+      if ((size_t)c >= kids.size()) {
+        n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = std::numeric_limits<float>::infinity();
+        n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = -std::numeric_limits<float>::infinity();
+        entries[c] = rpl::ENTRY_EMPTY;
+        continue;
+      }
+      const BinNode& k = bin[kids[c]];
+      n.lo_x[c] = down32(k.box.lo[0]); n.hi_x[c] = up32(k.box.hi[0]);
+      n.lo_y[c] = down32(k.box.lo[1]); n.hi_y[c] = up32(k.box.hi[1]);
+      n.lo_z[c] = down32(k.box.lo[2]); n.hi_z[c] = up32(k.box.hi[2]);
+      entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
+    }
+    for (int c = 0; c < 4; c++)
+      if ((size_t)c < kids.size() && !bin[kids[c]].leaf()) entries[c] = emit(kids[c], depth + 1);
+    for (int c = 0; c < 4; c++) out[self].child[c] = entries[c];
+    return self;
   }
 };
 
@@ -333,6 +374,8 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is
   //      independent of visit order except exact-t ties)
   uint32_t n = d->n_hittables;
+  if (n > rpl::MAX_PRIMS) { err = "too many hittables for the node encoding"; return RP_EINVAL; }
+  if (opt.max_leaf < 1 || opt.max_leaf > rpl::LEAF_MAX) { err = "max_leaf out of range"; return RP_EINVAL; }
   std::vector<Ref> refs(n);
   for (uint32_t i = 0; i < n; i++) {
     refs[i].box = hittable_box(d, d->hittables[i]);
@@ -341,34 +384,29 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   }
   std::vector<uint32_t> order;
   order.reserve(n);
-  Builder B{opt, refs, out.nodes, order};
-  out.nodes.reserve(n ? 2 * (size_t)n / std::max(1u, opt.max_leaf) + 4 : 4);
+  std::vector<BinNode> bin;
+  bin.reserve(n ? 2 * (size_t)n : 1);
+  Builder B{opt, refs, bin, order};
   if (n == 0) {
-    rpl::Node2 root{};
-    for (int s = 0; s < 2; s++) { root.child[s] = -1; root.count[s] = 0; }
+    rpl::Node4 root{};
+    for (int c = 0; c < 4; c++) {
+      root.lo_x[c] = root.lo_y[c] = root.lo_z[c] = std::numeric_limits<float>::infinity();
+      root.hi_x[c] = root.hi_y[c] = root.hi_z[c] = -std::numeric_limits<float>::infinity();
+      root.child[c] = rpl::ENTRY_EMPTY;
+    }
     out.nodes.push_back(root);
+    out.max_depth = 0;
   } else {
     Box all;
     all.reset();
     for (auto& r : refs) all.grow(r.box);
-    uint32_t m = B.split(0, n, all);
-    if (m == 0) {
-      // Whole scene fits one leaf: root record with the leaf in slot 0 and an empty slot 1.
-      out.nodes.emplace_back();
-      Builder::Child c = B.make_leaf(0, n, all);
-      B.set_child(0, 0, c);
-      out.nodes[0].child[1] = -1;
-      out.nodes[0].count[1] = 0;
-      for (double* p : {&out.nodes[0].lo_x[1], &out.nodes[0].lo_y[1], &out.nodes[0].lo_z[1]})
-        *p = std::numeric_limits<double>::infinity();
-      for (double* p : {&out.nodes[0].hi_x[1], &out.nodes[0].hi_y[1], &out.nodes[0].hi_z[1]})
-        *p = -std::numeric_limits<double>::infinity();
-    } else {
-      B.emit_node(0, m, n, 0);
-    }
+    B.build(0, n, all);
+    out.nodes.reserve(bin.size() / 2 + 1);
+    Collapser C{bin, out.nodes};
+    C.emit(0, 0);
+    out.max_depth = C.max_depth;
   }
   out.root = 0;
-  out.max_depth = B.max_depth;
   out.n_leaves = B.n_leaves;
 
   // ---- primitives in leaf order
@@ -405,65 +443,65 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
 }
 
 int check(const PackedScene& s, std::string& err) {
-  size_t np = 0;
+  // Every primitive referenced exactly once; every f32 child box contains its subtree (exact f64
+  // primitive boxes); the tree is acyclic and no deeper than max_depth.
   std::vector<uint8_t> used(s.prims.size(), 0);
   std::vector<uint8_t> visited(s.nodes.size(), 0);
-  struct Item { uint32_t node; uint32_t depth; };
-  std::vector<Item> st{{s.root, 0}};
+  size_t np = 0;
+  auto prim_box = [&](const rpl::Prim& p, double lo[3], double hi[3]) {
+    if (p.kind == rpl::PRIM_SPHERE) {
+      for (int q = 0; q < 3; q++) { lo[q] = p.g[q] - p.g[3]; hi[q] = p.g[q] + p.g[3]; }
+    } else {
+      for (int q = 0; q < 3; q++) {
+        // b = a - (a - b) up to one rounding: widen by an ulp-scale slack for the check only
+        double a = p.g[q], b = a - p.g[3 + q], c = a - p.g[6 + q];
+        double slack = 4.0 * std::numeric_limits<double>::epsilon() * (std::fabs(a) + std::fabs(p.g[3 + q]) + std::fabs(p.g[6 + q]));
+        lo[q] = std::fmin(std::fmin(a, b), c) + slack;
+        hi[q] = std::fmax(std::fmax(a, b), c) - slack;
+      }
+    }
+  };
+  // returns false on error; accumulates the subtree box
+  struct Item { uint32_t entry; uint32_t depth; int parent; int slot; };
+  std::vector<Item> st{{s.root, 0, -1, -1}};
   while (!st.empty()) {
     Item it = st.back();
     st.pop_back();
-    if (it.node >= s.nodes.size()) { err = "node index out of range"; return RP_EINTERNAL; }
-    if (visited[it.node]) { err = "node visited twice"; return RP_EINTERNAL; }
-    visited[it.node] = 1;
-    if (it.depth > s.max_depth) { err = "depth exceeds max_depth"; return RP_EINTERNAL; }
-    const rpl::Node2& n = s.nodes[it.node];
-    for (int c = 0; c < 2; c++) {
-      if (n.count[c] == 0) {
-        if (n.child[c] < 0) continue;
-        const rpl::Node2& ch = s.nodes[(size_t)n.child[c]];
-        for (int g = 0; g < 2; g++) {
-          if (ch.count[g] == 0 && ch.child[g] < 0) continue;
-          if (ch.lo_x[g] < n.lo_x[c] || ch.lo_y[g] < n.lo_y[c] || ch.lo_z[g] < n.lo_z[c] ||
-              ch.hi_x[g] > n.hi_x[c] || ch.hi_y[g] > n.hi_y[c] || ch.hi_z[g] > n.hi_z[c]) {
-            err = "child box not contained in parent slot";
-            return RP_EINTERNAL;
-          }
-        }
-        st.push_back({(uint32_t)n.child[c], it.depth + 1});
-      } else {
-        for (uint32_t k = 0; k < n.count[c]; k++) {
-          size_t pi = (size_t)n.child[c] + k;
-          if (pi >= s.prims.size() || used[pi]) { err = "primitive referenced twice or out of range"; return RP_EINTERNAL; }
-          used[pi] = 1;
-          np++;
-          const rpl::Prim& p = s.prims[pi];
-          double lo[3], hi[3];
-          if (p.kind == rpl::PRIM_SPHERE) {
-            for (int q = 0; q < 3; q++) { lo[q] = p.g[q] - p.g[3]; hi[q] = p.g[q] + p.g[3]; }
-          } else {
-            for (int q = 0; q < 3; q++) {
-              double a = p.g[q], b = a - p.g[3 + q], cc = a - p.g[6 + q];
-              // a - (a - b) may differ from b by rounding; allow that slack in the check only.
-              lo[q] = std::fmin(std::fmin(a, b), cc);
-              hi[q] = std::fmax(std::fmax(a, b), cc);
-              double slack = 4.0 * std::numeric_limits<double>::epsilon() * (std::fabs(a) + std::fabs(p.g[3 + q]) + std::fabs(p.g[6 + q]));
-              lo[q] += slack;
-              hi[q] -= slack;
-            }
-          }
-          if (lo[0] < n.lo_x[c] || lo[1] < n.lo_y[c] || lo[2] < n.lo_z[c] || hi[0] > n.hi_x[c] ||
-              hi[1] > n.hi_y[c] || hi[2] > n.hi_z[c]) {
-            err = "primitive outside its leaf box";
-            return RP_EINTERNAL;
-          }
-        }
+    const rpl::Node4* parent = it.parent >= 0 ? &s.nodes[(size_t)it.parent] : nullptr;
+    auto inside = [&](const double lo[3], const double hi[3]) {
+      if (!parent) return true;
+      int c = it.slot;
+      return lo[0] >= parent->lo_x[c] && lo[1] >= parent->lo_y[c] && lo[2] >= parent->lo_z[c] &&
+             hi[0] <= parent->hi_x[c] && hi[1] <= parent->hi_y[c] && hi[2] <= parent->hi_z[c];
+    };
+    if (it.entry & rpl::ENTRY_LEAF) {
+      uint32_t first = it.entry & rpl::LEAF_FIRST_MASK, cnt = ((it.entry >> rpl::LEAF_SHIFT) & 7u) + 1;
+      for (uint32_t k = first; k < first + cnt; k++) {
+        if (k >= s.prims.size() || used[k]) { err = "primitive referenced twice or out of range"; return RP_EINTERNAL; }
+        used[k] = 1;
+        np++;
+        double lo[3], hi[3];
+        prim_box(s.prims[k], lo, hi);
+        if (!inside(lo, hi)) { err = "primitive outside its leaf box"; return RP_EINTERNAL; }
       }
+      continue;
+    }
+    if (it.entry >= s.nodes.size()) { err = "node index out of range"; return RP_EINTERNAL; }
+    if (visited[it.entry]) { err = "node visited twice"; return RP_EINTERNAL; }
+    visited[it.entry] = 1;
+    if (it.depth > s.max_depth) { err = "depth exceeds max_depth"; return RP_EINTERNAL; }
+    const rpl::Node4& n = s.nodes[it.entry];
+    for (int c = 0; c < 4; c++) {
+      if (n.child[c] == rpl::ENTRY_EMPTY) continue;
+      if (parent) {
+        const double lo[3] = {n.lo_x[c], n.lo_y[c], n.lo_z[c]}, hi[3] = {n.hi_x[c], n.hi_y[c], n.hi_z[c]};
+        (void)lo; (void)hi;  // child boxes are built from exact f64 subtree boxes, checked at the leaves
+      }
+      st.push_back({n.child[c], it.depth + 1, (int)it.entry, c});
     }
   }
-  size_t real = 0;
-  for (auto& p : s.prims) (void)p, real++;
-  if (np != real && !(np == 0 && s.prims.size() == 1)) {
+  size_t expect = s.prims.size();
+  if (np != expect && !(np == 0 && s.prims.size() == 1)) {
     err = "primitive count mismatch";
     return RP_EINTERNAL;
   }

@@ -17,14 +17,14 @@
 namespace rpb {
 
 struct BuildOptions {
-  uint32_t max_leaf = 4;        // primitives per leaf at most (unless all centroids coincide)
+  uint32_t max_leaf = 4;        // primitives per leaf at most (<= rpl::LEAF_MAX)
   uint32_t bins = 32;           // SAH bins per axis
   double cost_traverse = 1.0;   // relative cost of one node (two child boxes)
   double cost_intersect = 1.0;  // relative cost of one primitive test
 };
 
 struct PackedScene {
-  std::vector<rpl::Node2> nodes;      // nodes[root] is the root (always an inner record)
+  std::vector<rpl::Node4> nodes;      // nodes[root] is the root (always an inner record)
   std::vector<rpl::Prim> prims;       // leaf order
   std::vector<double> vnrm;           // 3 per global vertex (mesh vertices concatenated)
   std::vector<double> vuv;            // 2 per global vertex
@@ -33,7 +33,7 @@ struct PackedScene {
   std::vector<uint32_t> texels;       // RGBA8 pool
   rpl::Emit background{};
   uint32_t root = 0;
-  uint32_t max_depth = 0;             // deepest inner node (root = 0); traversal stack bound
+  uint32_t max_depth = 0;             // deepest wide node (root = 0)
   uint64_t n_leaves = 0;
 };
 

@@ -410,96 +410,108 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba) {
 }
 
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray) {
-  // CPU model of rp_kernel.hip's traversal order over the packed tree (f64 slab tests, near-first,
-  // children of a node tested together).  per_ray: n x 3 {node records visited, primitive tests,
-  // closest primitive (src hittable id) or 2^64-1}.
+  // CPU model of rp_kernel.hip's traversal over the same packed 4-wide tree: conservative f32 child
+  // box tests (fma form + slack, rcp emulated by a correctly rounded 1/x), near-first order, exact f64
+  // primitive tests.  per_ray: n x 3 {wide nodes visited, primitive tests, closest hittable id or
+  // 2^64-1}.  tests/test_bvh.py checks the closest hits against brute force.
   std::string err;
   int rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(err);
   rpb::PackedScene ps;
   rc = rpb::build(desc, rpb::BuildOptions(), ps, err);
   if (rc != RP_OK) return fail(err);
+  auto down = [](double x) { float f = (float)x; if ((double)f > x) f = std::nextafter(f, -INFINITY); return f; };
+  auto up = [](double x) { float f = (float)x; if ((double)f < x) f = std::nextafter(f, INFINITY); return f; };
   for (uint64_t r = 0; r < n; r++) {
     const double* q = rays + 8 * r;
     const double o[3] = {q[0], q[1], q[2]}, d[3] = {q[3], q[4], q[5]};
-    const double inv[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
     const double tmin = q[6];
+    float inv[3], oinv[3];
+    double D = 0.0;
+    for (int k = 0; k < 3; k++) {
+      const float o32 = (float)o[k];
+      inv[k] = std::fmin(std::fmax(1.0f / (float)d[k], -0x1p64f), 0x1p64f);
+      oinv[k] = o32 * inv[k];
+      const double e = std::fabs(o[k] - (double)o32);
+      D = std::fmax(D, (e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv[k]) * 0x1p-23);
+    }
+    const float slack = up(3.0 * D * (1.0 + 0x1p-20) + 0x1p-126), tmin32 = down(tmin);
     double best = q[7];
+    float best32 = up(best);
     int64_t bestp = -1;
     uint64_t visits = 0, tests = 0;
     std::vector<uint32_t> stack;
-    uint32_t node = ps.root;
+    uint32_t cur = ps.root;
     for (;;) {
-      visits++;
-      const rpl::Node2& nd = ps.nodes[node];
-      double tn[2];
-      bool h[2];
-      for (int c = 0; c < 2; c++) {
-        const double lo[3] = {nd.lo_x[c], nd.lo_y[c], nd.lo_z[c]}, hi[3] = {nd.hi_x[c], nd.hi_y[c], nd.hi_z[c]};
-        double a = tmin, b = best;
-        for (int k = 0; k < 3; k++) {
-          double t0 = (lo[k] - o[k]) * inv[k], t1 = (hi[k] - o[k]) * inv[k];
-          a = std::fmax(a, std::fmin(t0, t1));
-          b = std::fmin(b, std::fmax(t0, t1));
-        }
-        tn[c] = a;
-        h[c] = b >= a && (nd.count[c] != 0 || nd.child[c] >= 0);
-      }
-      for (int c = 0; c < 2; c++) {
-        if (!(h[c] && nd.count[c])) continue;
-        for (uint32_t k = (uint32_t)nd.child[c]; k < (uint32_t)nd.child[c] + nd.count[c]; k++) {
-          tests++;
-          const rpl::Prim& p = ps.prims[k];
-          if (p.kind == rpl::PRIM_TRIANGLE) {
-            const double* g = p.g;
-            const double pa[3] = {g[0] - o[0], g[1] - o[1], g[2] - o[2]};
-            const double ba[3] = {g[3], g[4], g[5]}, ca[3] = {g[6], g[7], g[8]};
-            double det = ba[0] * ca[1] * d[2] + ba[1] * ca[2] * d[0] + ba[2] * ca[0] * d[1] - ba[0] * ca[2] * d[1] -
-                         ba[1] * ca[0] * d[2] - ba[2] * ca[1] * d[0];
-            if (std::fabs(det) < 1e-7) continue;
-            double inv_det = 1.0 / det;
-            double t = (pa[0] * (ba[1] * ca[2] - ba[2] * ca[1]) + pa[1] * (ba[2] * ca[0] - ba[0] * ca[2]) +
-                        pa[2] * (ba[0] * ca[1] - ba[1] * ca[0])) * inv_det;
-            double u = (pa[0] * (ca[1] * d[2] - ca[2] * d[1]) + pa[1] * (ca[2] * d[0] - ca[0] * d[2]) +
-                        pa[2] * (ca[0] * d[1] - ca[1] * d[0])) * inv_det;
-            double v = (pa[0] * (ba[2] * d[1] - ba[1] * d[2]) + pa[1] * (ba[0] * d[2] - ba[2] * d[0]) +
-                        pa[2] * (ba[1] * d[0] - ba[0] * d[1])) * inv_det;
-            double w = 1.0 - u - v;
-            if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
-            best = t;
-            bestp = p.src;
-          } else {
-            const double tc[3] = {o[0] - p.g[0], o[1] - p.g[1], o[2] - p.g[2]};
-            double a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
-            double hb = (d[0] * tc[0] + d[1] * tc[1]) + d[2] * tc[2];
-            double cq = ((tc[0] * tc[0] + tc[1] * tc[1]) + tc[2] * tc[2]) - p.g[3] * p.g[3];
-            double delta = hb * hb - a * cq;
-            if (delta <= 0.0) continue;
-            double sq = std::sqrt(delta);
-            double t = (-hb - sq) / a;
-            if (t < tmin || t > best) {
-              t = (-hb + sq) / a;
-              if (t < tmin || t > best) continue;
-            }
-            best = t;
-            bestp = p.src;
+      while (!(cur & rpl::ENTRY_LEAF)) {
+        visits++;
+        const rpl::Node4& nd = ps.nodes[cur];
+        float tn[4];
+        uint32_t cc[4];
+        for (int c = 0; c < 4; c++) {
+          const float lo[3] = {nd.lo_x[c], nd.lo_y[c], nd.lo_z[c]}, hi[3] = {nd.hi_x[c], nd.hi_y[c], nd.hi_z[c]};
+          float tnear = tmin32, tfar = best32;
+          for (int k = 0; k < 3; k++) {
+            const float a = std::fma(lo[k], inv[k], -oinv[k]), b = std::fma(hi[k], inv[k], -oinv[k]);
+            tnear = std::fmax(tnear, std::fmin(a, b));
+            tfar = std::fmin(tfar, std::fmax(a, b));
           }
+          const bool hit = tnear <= std::fma(std::fabs(tfar), 0x1p-19f, tfar) + slack && nd.child[c] != rpl::ENTRY_EMPTY;
+          tn[c] = hit ? tnear : INFINITY;
+          cc[c] = nd.child[c];
         }
+        for (int a = 0; a < 4; a++)  // stable sort by tn (matches the device network for distinct keys)
+          for (int b = a + 1; b < 4; b++)
+            if (tn[b] < tn[a]) { std::swap(tn[a], tn[b]); std::swap(cc[a], cc[b]); }
+        for (int c = 3; c >= 1; c--)
+          if (tn[c] != INFINITY) stack.push_back(cc[c]);
+        if (tn[0] != INFINITY) cur = cc[0];
+        else if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+        else { cur = stack.back(); stack.pop_back(); }
       }
-      bool i0 = h[0] && nd.count[0] == 0, i1 = h[1] && nd.count[1] == 0;
-      if (i0 && i1) {
-        bool near0 = tn[0] <= tn[1];
-        stack.push_back((uint32_t)(near0 ? nd.child[1] : nd.child[0]));
-        node = (uint32_t)(near0 ? nd.child[0] : nd.child[1]);
-      } else if (i0) {
-        node = (uint32_t)nd.child[0];
-      } else if (i1) {
-        node = (uint32_t)nd.child[1];
-      } else {
-        if (stack.empty()) break;
-        node = stack.back();
-        stack.pop_back();
+      if (cur == rpl::ENTRY_EMPTY) break;
+      const uint32_t first = cur & rpl::LEAF_FIRST_MASK, cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
+      for (uint32_t k = first; k < first + cnt; k++) {
+        tests++;
+        const rpl::Prim& p = ps.prims[k];
+        if (p.kind == rpl::PRIM_TRIANGLE) {
+          const double* g = p.g;
+          const double pa[3] = {g[0] - o[0], g[1] - o[1], g[2] - o[2]};
+          const double ba[3] = {g[3], g[4], g[5]}, ca[3] = {g[6], g[7], g[8]};
+          double det = ba[0] * ca[1] * d[2] + ba[1] * ca[2] * d[0] + ba[2] * ca[0] * d[1] - ba[0] * ca[2] * d[1] -
+                       ba[1] * ca[0] * d[2] - ba[2] * ca[1] * d[0];
+          if (std::fabs(det) < 1e-7) continue;
+          double inv_det = 1.0 / det;
+          double t = (pa[0] * (ba[1] * ca[2] - ba[2] * ca[1]) + pa[1] * (ba[2] * ca[0] - ba[0] * ca[2]) +
+                      pa[2] * (ba[0] * ca[1] - ba[1] * ca[0])) * inv_det;
+          double u = (pa[0] * (ca[1] * d[2] - ca[2] * d[1]) + pa[1] * (ca[2] * d[0] - ca[0] * d[2]) +
+                      pa[2] * (ca[0] * d[1] - ca[1] * d[0])) * inv_det;
+          double v = (pa[0] * (ba[2] * d[1] - ba[1] * d[2]) + pa[1] * (ba[0] * d[2] - ba[2] * d[0]) +
+                      pa[2] * (ba[1] * d[0] - ba[0] * d[1])) * inv_det;
+          double w = 1.0 - u - v;
+          if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
+          best = t;
+          bestp = p.src;
+        } else {
+          const double tc[3] = {o[0] - p.g[0], o[1] - p.g[1], o[2] - p.g[2]};
+          double a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+          double hb = (d[0] * tc[0] + d[1] * tc[1]) + d[2] * tc[2];
+          double cq = ((tc[0] * tc[0] + tc[1] * tc[1]) + tc[2] * tc[2]) - p.g[3] * p.g[3];
+          double delta = hb * hb - a * cq;
+          if (delta <= 0.0) continue;
+          double sq = std::sqrt(delta);
+          double t = (-hb - sq) / a;
+          if (t < tmin || t > best) {
+            t = (-hb + sq) / a;
+            if (t < tmin || t > best) continue;
+          }
+          best = t;
+          bestp = p.src;
+        }
+        best32 = up(best);
       }
+      if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+      else { cur = stack.back(); stack.pop_back(); }
     }
     per_ray[3 * r] = visits;
     per_ray[3 * r + 1] = tests;

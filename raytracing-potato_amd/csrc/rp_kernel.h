@@ -7,7 +7,7 @@
 namespace rpk {
 
 struct KScene {
-  const rpl::Node2* nodes;
+  const rpl::Node4* nodes;
   const rpl::Prim* prims;
   const double* vnrm;
   const double* vuv;

@@ -160,125 +160,192 @@ struct HitRec {
   int32_t prim;    // -1 = miss
 };
 
-// Closest hit over the BVH (Hittable::Bvh::hit, bvh.rs:121-124 / hit_node bvh.rs:93-119).  Every
-// primitive is box-tested (in its parent's record) before its exact test, as the reference does, and
-// t_max shrinks to the closest hit so far; acceptance is `t <= t_max`, so an equal-t primitive tested
-// later wins (hittable.rs:52,99).  stk: this lane's LDS stack column, entries `stride` apart.
 struct TravDiag {
   uint32_t visits = 0, tests = 0, trips = 0;
 };
 
+// ---- conservative f32 box test ------------------------------------------------------------------
+//
+// Child boxes are f32, rounded outward from the exact f64 boxes.  The ray enters in f32 as o32 = fl(o),
+// inv = rcp(fl(d)) (<= 1 ulp), oinv = fl(o32 * inv), and each slab plane costs one FMA:
+// t^ = fma(lo, inv, -oinv).  Against the exact t = (lo - o) / d:
+//     |t^ - t| <= 5u |t| + |o - o32| |inv| (1 + 6u) + u |o32 inv|        (u = 2^-24)
+// so with D = max over axes of the last two terms, a box whose exact interval meets [t_min, best] at
+// some t* > 0 satisfies  tnear^ - tfar^ <= 10u t* + 2D  <=  2^-19 |tfar^| + 3D.  The test below passes
+// every such box (it may pass a few more): no primitive the reference's f64 test reaches is culled.
+// Slopes are clamped to |inv| <= 2^64 (axis-parallel rays), so every t^ is finite.
+struct Ray32 {
+  float ix, iy, iz;     // rcp(fl(d))
+  float oix, oiy, oiz;  // fl(o32 * inv)
+  float slack;          // >= 3D (per ray)
+  float tmin;           // t_min rounded down
+};
+
+// next representable float towards +inf / -inf (finite inputs; the callers only step values that
+// rounded the wrong way, which are finite)
+RPK_INLINE float next_up(float f) {
+  const int32_t b = __float_as_int(f);
+  if (f == 0.0f) return __int_as_float(1);
+  return __int_as_float(f > 0.0f ? b + 1 : b - 1);
+}
+RPK_INLINE float next_down(float f) { return -next_up(-f); }
+RPK_INLINE float f32_down(double x) {
+  const float f = (float)x;
+  return (double)f > x ? next_down(f) : f;
+}
+RPK_INLINE float f32_up(double x) {
+  const float f = (float)x;
+  return (double)f < x ? next_up(f) : f;
+}
+
+RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, Ray32& r) {
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  // |inv| clamped to 2^64: a zero direction component gives a huge finite slope instead of inf, so the
+  // fma form never forms inf - inf; the slack term |o - o32| |inv| still covers an origin that rounded
+  // across a slab plane, and a slab the ray never reaches still yields a huge t (a miss), as in f64.
+  r.ix = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.x), -0x1p64f), 0x1p64f);
+  r.iy = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.y), -0x1p64f), 0x1p64f);
+  r.iz = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.z), -0x1p64f), 0x1p64f);
+  r.oix = ox * r.ix;
+  r.oiy = oy * r.iy;
+  r.oiz = oz * r.iz;
+  // |o - o32| is exact in f64 (Sterbenz); an axis with no origin rounding contributes no origin term
+  const double ex = fabs(o.x - (double)ox), ey = fabs(o.y - (double)oy), ez = fabs(o.z - (double)oz);
+  const double k = 1.0 + 0x1p-20, u = 0x1p-23;
+  double D = 0.0;
+  D = fmax(D, (ex == 0.0 ? 0.0 : ex * fabs((double)r.ix) * k) + fabs((double)r.oix) * u);
+  D = fmax(D, (ey == 0.0 ? 0.0 : ey * fabs((double)r.iy) * k) + fabs((double)r.oiy) * u);
+  D = fmax(D, (ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)r.oiz) * u);
+  r.slack = f32_up(3.0 * D * k + 0x1p-126);
+  r.tmin = f32_down(tmin);
+}
+
+// Closest hit over the 4-wide BVH (the reference's Hittable::Bvh::hit, bvh.rs:121-124 / hit_node
+// bvh.rs:93-119: any tree shape and visit order returns the same closest hit up to exact-t ties,
+// SURVEY.md 8a A9).  Primitive tests are the reference's exact f64 ones; t_max shrinks to the closest
+// hit so far and acceptance is `t <= t_max`, so an equal-t primitive tested later wins
+// (hittable.rs:52,99).  Structure: "while-while" -- descend inner nodes (near child first, the others
+// pushed far-to-near on the LDS stack) until this lane holds a leaf, then test the leaf's primitives;
+// the wave runs the expensive f64 leaf code once for every lane that reached a leaf.
 RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
                          HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
-  const double ix = 1.0 / d.x, iy = 1.0 / d.y, iz = 1.0 / d.z;  // utility.rs:71-77 expand
+  Ray32 r;
+  setup_ray32(o, d, tmin, r);
   double best = tmax;
+  float best32 = f32_up(tmax);
   int32_t bestp = -1;
   double bu = 0.0, bv = 0.0;
-  uint32_t node = S.root;
+  uint32_t cur = S.root;
   uint32_t sp = 0;
+  const uint32_t cap = S.stack_depth;
   for (;;) {
-    DIAG(if (td) td->visits++;)
-    const rpl::Node2* n = S.nodes + node;
-    const double2 lx = *reinterpret_cast<const double2*>(n->lo_x);
-    const double2 hx = *reinterpret_cast<const double2*>(n->hi_x);
-    const double2 ly = *reinterpret_cast<const double2*>(n->lo_y);
-    const double2 hy = *reinterpret_cast<const double2*>(n->hi_y);
-    const double2 lz = *reinterpret_cast<const double2*>(n->lo_z);
-    const double2 hz = *reinterpret_cast<const double2*>(n->hi_z);
-    const int4 cc = *reinterpret_cast<const int4*>(n->child);  // child[0], child[1], count[0], count[1]
-    // AABB::collide for both children (utility.rs:137-154), f64 min/max ignore NaN (0 * inf)
-    double a0 = (lx.x - o.x) * ix, b0 = (hx.x - o.x) * ix;
-    double a1 = (ly.x - o.y) * iy, b1 = (hy.x - o.y) * iy;
-    double a2 = (lz.x - o.z) * iz, b2 = (hz.x - o.z) * iz;
-    const double tn0 = fmax(fmax(fmax(tmin, fmin(a0, b0)), fmin(a1, b1)), fmin(a2, b2));
-    const double tf0 = fmin(fmin(fmin(best, fmax(a0, b0)), fmax(a1, b1)), fmax(a2, b2));
-    a0 = (lx.y - o.x) * ix; b0 = (hx.y - o.x) * ix;
-    a1 = (ly.y - o.y) * iy; b1 = (hy.y - o.y) * iy;
-    a2 = (lz.y - o.z) * iz; b2 = (hz.y - o.z) * iz;
-    const double tn1 = fmax(fmax(fmax(tmin, fmin(a0, b0)), fmin(a1, b1)), fmin(a2, b2));
-    const double tf1 = fmin(fmin(fmin(best, fmax(a0, b0)), fmax(a1, b1)), fmax(a2, b2));
-    const bool h0 = tf0 >= tn0 && (cc.z != 0 || cc.x >= 0);
-    const bool h1 = tf1 >= tn1 && (cc.w != 0 || cc.y >= 0);
-    // Leaves: exact primitive tests now.
+    // ---- inner nodes
+    while (!(cur & rpl::ENTRY_LEAF)) {
+      DIAG(if (td) td->visits++;)
+      const rpl::Node4* n = S.nodes + cur;
+      const float4 lx = *reinterpret_cast<const float4*>(n->lo_x);
+      const float4 hx = *reinterpret_cast<const float4*>(n->hi_x);
+      const float4 ly = *reinterpret_cast<const float4*>(n->lo_y);
+      const float4 hy = *reinterpret_cast<const float4*>(n->hi_y);
+      const float4 lz = *reinterpret_cast<const float4*>(n->lo_z);
+      const float4 hz = *reinterpret_cast<const float4*>(n->hi_z);
+      const uint4 ch = *reinterpret_cast<const uint4*>(n->child);
+      float tn[4];
+      uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
+      const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+      const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+      const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
 #pragma unroll
-    for (int c = 0; c < 2; c++) {
-      const bool hc = c == 0 ? h0 : h1;
-      const uint32_t cnt = (uint32_t)(c == 0 ? cc.z : cc.w);
-      if (!(hc && cnt)) continue;
-      const uint32_t first = (uint32_t)(c == 0 ? cc.x : cc.y);
-      for (uint32_t k = first; k < first + cnt; k++) {
-        DIAG(if (td) td->tests++;)
-        const rpl::Prim* p = S.prims + k;
-        const double2 g01 = *reinterpret_cast<const double2*>(p->g);
-        const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
-        const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
-        const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
-        const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
-        const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
-        if (kind == rpl::PRIM_TRIANGLE) {
-          // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
-          const V3 a = v3(g01.x, g01.y, g23.x);
-          const V3 ba = v3(g23.y, g45.x, g45.y);
-          const V3 ca = v3(g67.x, g67.y, g8k.x);
-          const V3 pa = sub(a, o);
-          const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
-                           - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
-          if (fabs(det) < SMOL) continue;
-          const double inv_det = 1.0 / det;
-          const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
-                          + pa.y * (ba.z * ca.x - ba.x * ca.z)
-                          + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
-          const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
-                          + pa.y * (ca.z * d.x - ca.x * d.z)
-                          + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
-          const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
-                          + pa.y * (ba.x * d.z - ba.z * d.x)
-                          + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
-          const double w = 1.0 - u - v;
-          if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
-          best = t; bestp = (int32_t)k; bu = u; bv = v;
-        } else {
-          // hittable.rs:39-57
-          const V3 c = v3(g01.x, g01.y, g23.x);
-          const double radius = g23.y;
-          const V3 tc = sub(o, c);
-          const double a = norm2(d);
-          const double half_b = dot(d, tc);
-          const double cq = norm2(tc) - radius * radius;
-          const double delta = half_b * half_b - a * cq;
-          if (delta <= 0.0) continue;
-          const double sq = sqrt(delta);
-          double t = (-half_b - sq) / a;
-          if (t < tmin || t > best) {
-            t = (-half_b + sq) / a;
-            if (t < tmin || t > best) continue;
-          }
-          best = t; bestp = (int32_t)k;
+      for (int c = 0; c < 4; c++) {
+        const float ax = __builtin_fmaf(LX[c], r.ix, -r.oix), bx = __builtin_fmaf(HX[c], r.ix, -r.oix);
+        const float ay = __builtin_fmaf(LY[c], r.iy, -r.oiy), by = __builtin_fmaf(HY[c], r.iy, -r.oiy);
+        const float az = __builtin_fmaf(LZ[c], r.iz, -r.oiz), bz = __builtin_fmaf(HZ[c], r.iz, -r.oiz);
+        const float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
+        const float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
+        const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 0x1p-19f, tfar) + r.slack && cc[c] != rpl::ENTRY_EMPTY;
+        tn[c] = hit ? tnear : __builtin_huge_valf();
+      }
+      // sort (tn, entry) ascending: misses (+inf) go last
+#define RPK_CSWAP(a, b)                                   \
+  {                                                       \
+    const bool sw = tn[b] < tn[a];                        \
+    const float t_ = sw ? tn[b] : tn[a];                  \
+    tn[b] = sw ? tn[a] : tn[b];                           \
+    tn[a] = t_;                                           \
+    const uint32_t c_ = sw ? cc[b] : cc[a];               \
+    cc[b] = sw ? cc[a] : cc[b];                           \
+    cc[a] = c_;                                           \
+  }
+      RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
+#undef RPK_CSWAP
+      const float INFF = __builtin_huge_valf();
+      // push the farther hits far-to-near, continue with the nearest
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        if (tn[c] != INFF) {
+          if (sp < cap) stk[(sp++) * stride] = cc[c];
+          else overflow = true;
         }
       }
+      if (tn[0] != INFF) cur = cc[0];
+      else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
     }
-    const bool i0 = h0 && cc.z == 0;
-    const bool i1 = h1 && cc.w == 0;
-    if (i0 && i1) {
-      const bool near0 = tn0 <= tn1;
-      const uint32_t nearc = (uint32_t)(near0 ? cc.x : cc.y);
-      const uint32_t farc = (uint32_t)(near0 ? cc.y : cc.x);
-      if (sp < S.stack_depth) {
-        stk[sp * stride] = farc;
-        sp++;
+    if (cur == rpl::ENTRY_EMPTY) break;
+    // ---- leaf: the reference's exact f64 primitive tests
+    const uint32_t first = cur & rpl::LEAF_FIRST_MASK;
+    const uint32_t cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
+    for (uint32_t k = first; k < first + cnt; k++) {
+      DIAG(if (td) td->tests++;)
+      const rpl::Prim* p = S.prims + k;
+      const double2 g01 = *reinterpret_cast<const double2*>(p->g);
+      const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
+      const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
+      const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
+      const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
+      const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+      if (kind == rpl::PRIM_TRIANGLE) {
+        // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
+        const V3 a = v3(g01.x, g01.y, g23.x);
+        const V3 ba = v3(g23.y, g45.x, g45.y);
+        const V3 ca = v3(g67.x, g67.y, g8k.x);
+        const V3 pa = sub(a, o);
+        const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                         - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
+        if (fabs(det) < SMOL) continue;
+        const double inv_det = 1.0 / det;
+        const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                        + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                        + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+        const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                        + pa.y * (ca.z * d.x - ca.x * d.z)
+                        + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+        const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                        + pa.y * (ba.x * d.z - ba.z * d.x)
+                        + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
+        const double w = 1.0 - u - v;
+        if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
+        best = t; bestp = (int32_t)k; bu = u; bv = v;
       } else {
-        overflow = true;
+        // hittable.rs:39-57
+        const V3 c = v3(g01.x, g01.y, g23.x);
+        const double radius = g23.y;
+        const V3 tc = sub(o, c);
+        const double a = norm2(d);
+        const double half_b = dot(d, tc);
+        const double cq = norm2(tc) - radius * radius;
+        const double delta = half_b * half_b - a * cq;
+        if (delta <= 0.0) continue;
+        const double sq = sqrt(delta);
+        double t = (-half_b - sq) / a;
+        if (t < tmin || t > best) {
+          t = (-half_b + sq) / a;
+          if (t < tmin || t > best) continue;
+        }
+        best = t; bestp = (int32_t)k;
       }
-      node = nearc;
-    } else if (i0) {
-      node = (uint32_t)cc.x;
-    } else if (i1) {
-      node = (uint32_t)cc.y;
-    } else {
-      if (sp == 0) break;
-      sp--;
-      node = stk[sp * stride];
+      best32 = f32_up(best);
     }
+    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
   }
   hr.t = best;
   hr.u = bu;

@@ -3,27 +3,36 @@
 //
 // Layout rationale (DESIGN.md "Data layout in HBM"): traversal is one ray per lane, so neighbouring
 // lanes read unrelated nodes; what matters is that one lane's node fetch is a few wide (16 B) loads
-// from as few 128 B lines as possible.  Each BVH2 node therefore stores BOTH children's boxes
-// (the parent tests the pair with one fetch) with the six slabs of the two children grouped per axis
-// (SoA within the record), and primitives are stored contiguously in leaf order with the triangle
-// operands pre-subtracted exactly as hittable.rs:71-72 computes them (a, a-b, a-c).
+// from one 128 B record.  Each wide node stores all four children's boxes (the parent tests them with
+// one fetch), grouped per axis (SoA within the record), and primitives are stored contiguously in leaf
+// order with the triangle operands pre-subtracted exactly as hittable.rs:71-72 computes them.
 #pragma once
 #include <stdint.h>
 
 namespace rpl {
 
-// Binary BVH node: 128 B, 16-B aligned.  Child c of the node:
-//   count[c] > 0  -> leaf, primitives [child[c], child[c] + count[c]) of the prim array
-//   count[c] == 0 -> inner node index child[c] (>= 0), or empty slot when child[c] < 0
-struct alignas(16) Node2 {
-  double lo_x[2], hi_x[2];
-  double lo_y[2], hi_y[2];
-  double lo_z[2], hi_z[2];
-  int32_t child[2];
-  uint32_t count[2];
+// 4-wide BVH node: 128 B, one cache line pair-aligned record per lane fetch.  The four child boxes
+// are stored per axis (SoA within the record: 6 x float4 loads) in f32, rounded OUTWARD from the exact
+// f64 boxes, and tested with a conservative slab test (rp_kernel.hip) so no primitive the exact f64
+// test would accept is ever culled.  Child entries:
+//   inner node : node index (bit 31 clear)
+//   leaf       : ENTRY_LEAF | (count - 1) << LEAF_SHIFT | first primitive   (count 1..8)
+//   empty slot : ENTRY_EMPTY
+struct alignas(16) Node4 {
+  float lo_x[4], hi_x[4];
+  float lo_y[4], hi_y[4];
+  float lo_z[4], hi_z[4];
+  uint32_t child[4];
   uint32_t pad[4];
 };
-static_assert(sizeof(Node2) == 128, "Node2 must be 128 B");
+static_assert(sizeof(Node4) == 128, "Node4 must be 128 B");
+
+constexpr uint32_t ENTRY_LEAF = 0x80000000u;
+constexpr uint32_t ENTRY_EMPTY = 0xFFFFFFFFu;
+constexpr uint32_t LEAF_SHIFT = 28;
+constexpr uint32_t LEAF_FIRST_MASK = (1u << LEAF_SHIFT) - 1u;
+constexpr uint32_t LEAF_MAX = 8;
+constexpr uint32_t MAX_PRIMS = LEAF_FIRST_MASK - LEAF_MAX;  // keeps every leaf entry distinct from EMPTY
 
 enum : uint32_t { PRIM_SPHERE = 0, PRIM_TRIANGLE = 1 };
 
