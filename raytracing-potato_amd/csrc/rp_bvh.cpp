@@ -315,6 +315,17 @@ int validate(const rp_scene_desc* d, std::string& err) {
   return RP_OK;
 }
 
+// Does sampling texture t read hit.uv?  (DebugUVs and Image do; Checker if either branch does;
+// Solid/Noise/Perlin/Missing do not -- texture.rs:21-118).  validate() guarantees termination.
+static bool texture_reads_uv(const rp_scene_desc* d, uint32_t t, int depth = 0) {
+  if (t >= d->n_textures || depth > 64) return true;
+  const rp_texture& x = d->textures[t];
+  if (x.kind == RP_TEXTURE_DEBUG_UVS || x.kind == RP_TEXTURE_IMAGE) return true;
+  if (x.kind == RP_TEXTURE_CHECKER)
+    return texture_reads_uv(d, x.odd, depth + 1) || texture_reads_uv(d, x.even, depth + 1);
+  return false;
+}
+
 int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std::string& err) {
   out = PackedScene();
   // ---- shading tables
@@ -339,6 +350,9 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     m.absorb_tex = s.absorb.texture;
     m.emit_kind = s.emit.kind;
     m.emit_tex = s.emit.texture;
+    // uv is only computed on the device when something will read it (the value is the reference's)
+    m.needs_uv = (s.absorb.kind == RP_ABSORB_ALBEDO_MAP && texture_reads_uv(d, s.absorb.texture)) ||
+                 (s.emit.kind == RP_EMIT_SKY_SPHERE && texture_reads_uv(d, s.emit.texture));
     for (int k = 0; k < 3; k++) {
       m.absorb_color[k] = s.absorb.color[k];
       m.emit_color[k] = s.emit.color[k];
@@ -369,6 +383,7 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   if (out.texels.empty()) out.texels.push_back(0);
   out.background.kind = d->background.kind;
   out.background.tex = d->background.texture;
+  out.background.needs_uv = d->background.kind == RP_EMIT_SKY_SPHERE && texture_reads_uv(d, d->background.texture);
   for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
 
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is

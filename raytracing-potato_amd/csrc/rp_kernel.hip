@@ -57,6 +57,10 @@ RPK_INLINE uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n));
 
 // ChaCha12 block (rand_chacha 0.3: 64-bit block counter in words 12-13, zero nonce).
 RPK_INLINE void chacha12(const uint32_t k[8], uint32_t ctr, uint32_t o[16]) {
+#ifdef RPK_ABLATE_RNG  // timing ablation only (wrong stream): a cheap mix instead of 12 rounds
+  for (int i = 0; i < 16; i++) { uint32_t x = k[i & 7] ^ (ctr * 0x9E3779B9u + i * 0x85EBCA6Bu); x ^= x >> 15; x *= 0x2C1B3C6Du; o[i] = x ^ (x >> 13); }
+  return;
+#endif
   uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
   uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
   uint32_t x12 = ctr, x13 = 0, x14 = 0, x15 = 0;
@@ -88,32 +92,44 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
   }
 }
 
-// Main stream of one pixel.  All draws on the path are u64 (Standard f64), so consuming the keystream
-// one 16-word block at a time yields exactly rand_chacha's 4-block-buffered stream.  The current block
-// lives in LDS (8 u64 per lane, lane-major: a wave's ds_read_b64 is conflict-free whatever word each
-// lane is at), which keeps 16 VGPRs out of the traversal's register budget.
+// Main stream of one pixel.  Every draw on the path is a u64 (Standard f64), so the stream is the
+// keystream read two words at a time from word `pos`: exactly rand_chacha's 4-block-buffered stream.
+// The 16-word block holding `pos` lives in registers only inside one loop iteration (RngBlk): it is
+// generated once per iteration for every lane at the same point (uniform across the wave), and a lane
+// regenerates only when its draws actually cross into the next block.  (Refilling a per-lane buffer
+// inside the rejection loops made the wave pay a whole ChaCha12 block whenever ANY lane ran dry:
+// 24% of the kernel at C3.)
 struct Rng {
   uint32_t key[8];
-  uint32_t ctr;         // next block
-  uint32_t idx;         // next u64 in the block, 8 = empty
-  uint64_t* buf;        // LDS: buf[k * BLOCK] = k-th u64 of the current block
+  uint32_t pos;  // next keystream word (even)
+};
+struct RngBlk {
+  uint32_t w[16];
+  uint32_t blk;  // block index held in w
 };
 
-RPK_INLINE uint64_t next_u64(Rng& r) {
-  if (r.idx >= 8) {
-    uint32_t b[16];
-    chacha12(r.key, r.ctr, b);
+RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
+  b.blk = r.pos >> 4;
+  chacha12(r.key, b.blk, b.w);
+}
+
+RPK_INLINE uint64_t next_u64(Rng& r, RngBlk& b) {
+  if ((r.pos >> 4) != b.blk) rng_load(r, b);
+  const uint32_t i = r.pos & 15u;
+  uint32_t lo = b.w[0], hi = b.w[1];
 #pragma unroll
-    for (int k = 0; k < 8; k++) r.buf[k * BLOCK] = ((uint64_t)b[2 * k + 1] << 32) | b[2 * k];
-    r.ctr++;
-    r.idx = 0;
+  for (int k = 1; k < 8; k++) {
+    const bool m = i == 2u * k;
+    lo = m ? b.w[2 * k] : lo;
+    hi = m ? b.w[2 * k + 1] : hi;
   }
-  return r.buf[(r.idx++) * BLOCK];
+  r.pos += 2;
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
 RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
-RPK_INLINE double gen_f64(Rng& r) { return u64_to_f64(next_u64(r)); }
+RPK_INLINE double gen_f64(Rng& r, RngBlk& b) { return u64_to_f64(next_u64(r, b)); }
 
 // ------------------------------------------------------------------ math -------------------------
 
@@ -360,10 +376,15 @@ struct Surf {
   uint32_t material;
 };
 
-RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s) {
+// uv is computed only when the hit material reads it (rpl::Material::needs_uv): same values, and the
+// f64 atan2/asin of a sphere hit are skipped for untextured spheres (the ground).
+RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, bool force_uv = false) {
   const rpl::Prim* p = S.prims + hr.prim;
   s.p = add(o, smul(hr.t, d));  // Ray::at (utility.rs:67)
   s.material = p->material;
+  s.u = 0.0;
+  s.v = 0.0;
+  const bool need_uv = force_uv || S.mats[s.material].needs_uv != 0;
   if (p->kind == rpl::PRIM_TRIANGLE) {
     const double u = hr.u, v = hr.v, w = 1.0 - u - v;
     const uint32_t i0 = p->v[0], i1 = p->v[1], i2 = p->v[2];
@@ -371,13 +392,17 @@ RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s) 
     const V3 n1 = v3(S.vnrm[3 * i1], S.vnrm[3 * i1 + 1], S.vnrm[3 * i1 + 2]);
     const V3 n2 = v3(S.vnrm[3 * i2], S.vnrm[3 * i2 + 1], S.vnrm[3 * i2 + 2]);
     s.n = add(add(smul(w, n0), smul(u, n1)), smul(v, n2));
-    s.u = (w * S.vuv[2 * i0] + u * S.vuv[2 * i1]) + v * S.vuv[2 * i2];
-    s.v = (w * S.vuv[2 * i0 + 1] + u * S.vuv[2 * i1 + 1]) + v * S.vuv[2 * i2 + 1];
+    if (need_uv) {
+      s.u = (w * S.vuv[2 * i0] + u * S.vuv[2 * i1]) + v * S.vuv[2 * i2];
+      s.v = (w * S.vuv[2 * i0 + 1] + u * S.vuv[2 * i1 + 1]) + v * S.vuv[2 * i2 + 1];
+    }
   } else {
     const V3 c = v3(p->g[0], p->g[1], p->g[2]);
     s.n = normalize(sub(s.p, c));
-    s.u = 0.5 - atan2(s.n.z, s.n.x) / TAU_;
-    s.v = asin(s.n.y) / PI_ + 0.5;
+    if (need_uv) {
+      s.u = 0.5 - atan2(s.n.z, s.n.x) / TAU_;
+      s.v = asin(s.n.y) / PI_ + 0.5;
+    }
   }
 }
 
@@ -471,14 +496,14 @@ RPK_INLINE V3 absorb_eval(const KScene& S, const rpl::Material& m, const Surf& h
 }
 
 // material.rs:27-34, 115-179 Scatter::evaluate.  Returns true and the new direction when scattered.
-RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, V3& nd) {
+RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, RngBlk& rb, V3& nd) {
   switch (m.scatter_kind) {
     case 1: {  // Lambert (material.rs:115-130)
       if (dot(h.n, d) > 0.0) return false;
       double x, y, s;
       do {  // UnitSphere (randomness.rs:58-73)
-        x = 2.0 * gen_f64(rng) - 1.0;
-        y = 2.0 * gen_f64(rng) - 1.0;
+        x = 2.0 * gen_f64(rng, rb) - 1.0;
+        y = 2.0 * gen_f64(rng, rb) - 1.0;
         s = x * x + y * y;
       } while (!(s < 1.0));
       const double q = 2.0 * sqrt(1.0 - s);
@@ -489,9 +514,9 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
       if (dot(h.n, d) > 0.0) return false;
       double x, y, z;
       do {  // UnitBall (randomness.rs:39-53)
-        x = 2.0 * gen_f64(rng) - 1.0;
-        y = 2.0 * gen_f64(rng) - 1.0;
-        z = 2.0 * gen_f64(rng) - 1.0;
+        x = 2.0 * gen_f64(rng, rb) - 1.0;
+        y = 2.0 * gen_f64(rng, rb) - 1.0;
+        z = 2.0 * gen_f64(rng, rb) - 1.0;
       } while (!((x * x + y * y) + z * z < 1.0));
       const V3 r = normalize(add(reflect(d, h.n), smul(m.scatter_param, v3(x, y, z))));
       if (dot(h.n, r) < 0.0) return false;
@@ -508,7 +533,7 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
       const double x = 1.0 + dot(n, d);
       const double x2 = x * x;
       const double reflectance = r0 + (1.0 - r0) * (x * (x2 * x2));  // powi(5), LLVM binary expansion
-      if (gen_f64(rng) < reflectance) {              // Bernoulli (randomness.rs:78-82)
+      if (gen_f64(rng, rb) < reflectance) {              // Bernoulli (randomness.rs:78-82)
         nd = reflect(d, n);
       } else {
         const double cos_theta = dot(n, d);          // refract (utility.rs:111-119)
@@ -555,6 +580,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.texels = A->S.texels;
   S.background.kind = A->S.background.kind;
   S.background.tex = A->S.background.tex;
+  S.background.needs_uv = A->S.background.needs_uv;
   S.background.color[0] = A->S.background.color[0];
   S.background.color[1] = A->S.background.color[1];
   S.background.color[2] = A->S.background.color[2];
@@ -569,11 +595,64 @@ RPK_INLINE KArgsPtr kargs() {
   return p;
 }
 
+// Pull the next pixel of the shard from the device-wide queue (slot order: tiles, row-major inside a
+// tile; slots of edge tiles outside the frame are skipped).  Returns false when the queue is drained.
+RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
+  KArgsPtr A = kargs();
+  unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
+  const uint32_t tw = A->P.tw, th = A->P.th, tile_px = tw * th;
+  for (;;) {
+    slot = atomicAdd(queue, 1u);
+    if ((uint64_t)slot >= A->P.n_slots) return false;
+    const uint32_t k = slot / tile_px, local = slot - k * tile_px;
+    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
+    pi = tx * tw + local % tw;
+    pj = ty * th + local / tw;
+    if (pi < A->P.W && pj < A->P.H) return true;
+  }
+}
+
+// One camera sample (main.rs:75-76): make_uv_jitter draws 2s, 2s+1 of a CLONE of the pixel-start
+// stream (render.rs:74-82) = keystream words 4s..4s+3 = block s/4 at offset 4(s%4); Camera::shoot
+// (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
+RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
+  KArgsPtr A = kargs();
+  uint32_t jb[16];
+  chacha12(rng.key, s >> 2, jb);
+  const uint32_t off = (s & 3u) * 4u;
+  uint32_t w0 = jb[0], w1 = jb[1], w2 = jb[2], w3 = jb[3];
+#pragma unroll
+  for (int q = 1; q < 4; q++) {
+    const bool m = off == 4u * q;
+    w0 = m ? jb[4 * q] : w0;
+    w1 = m ? jb[4 * q + 1] : w1;
+    w2 = m ? jb[4 * q + 2] : w2;
+    w3 = m ? jb[4 * q + 3] : w3;
+  }
+  const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
+  const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
+  double dx, dy;
+  do {  // UnitDisk (randomness.rs:21-34)
+    dx = 2.0 * gen_f64(rng, rb) - 1.0;
+    dy = 2.0 * gen_f64(rng, rb) - 1.0;
+  } while (!(dx * dx + dy * dy < 1.0));
+  A = kargs();
+  // tan(fov/2) is computed on the host (render.rs:33 is a per-camera constant; same libm as the reference)
+  const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
+  const V3 lo = v3(lens * dx, lens * dy, 0.0);
+  const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
+  double m[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
+  d = matvec(m, dl);
+  o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
+}
+
 __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
-  __shared__ uint64_t rng_lds[8 * BLOCK];
-  DIAG(__shared__ uint32_t wave_max[BLOCK / 64]; __shared__ unsigned long long wmax[BLOCK / 64][8];
+  DIAG(__shared__ unsigned long long wmax[BLOCK / 64][8];
        if (threadIdx.x < BLOCK / 64 * 8) wmax[threadIdx.x / 8][threadIdx.x % 8] = 0;)
   if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
   __syncthreads();
@@ -581,108 +660,46 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
 
   uint32_t n_rays = 0, n_samples = 0, n_pixels = 0;
   bool overflow = false;
-
-  // lane state
-  uint32_t slot = 0, pi = 0, pj = 0, s = 0, depth = 0;
-  bool need_pixel = true, new_sample = true, first = true;
-  Rng rng;
-  rng.buf = rng_lds + threadIdx.x;
-  V3 o = v3(0, 0, 0), d = v3(0, 0, 1), T = v3(0, 0, 0), L = v3(0, 0, 0), sum = v3(0, 0, 0);
-  uint32_t hits = 0;
   DIAG(uint64_t ph[5] = {0, 0, 0, 0, 0}; uint64_t iters = 0, active = 0; TravDiag td; uint64_t t_prev = stamp();)
 
-  for (;;) {
-    DIAG(iters++;)
-    if (need_pixel) {
-      KArgsPtr A = kargs();
-      unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
-      const uint32_t tw = A->P.tw, th = A->P.th, tile_px = tw * th;
-      bool found = false;
-      while (!found) {
-        slot = atomicAdd(queue, 1u);
-        if ((uint64_t)slot >= A->P.n_slots) break;
-        const uint32_t k = slot / tile_px, local = slot - k * tile_px;
-        const uint32_t t = A->P.shard + k * A->P.nshards;
-        const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
-        pi = tx * tw + local % tw;
-        pj = ty * th + local / tw;
-        found = pi < A->P.W && pj < A->P.H;
-      }
-      if (!found) break;  // queue drained: this lane retires
-      seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);  // RNG contract
-      rng.ctr = 0;
-      rng.idx = 8;
-      s = 0;
-      sum = v3(0.0, 0.0, 0.0);
-      hits = 0;
-      need_pixel = false;
-      new_sample = true;
-    }
-    DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
-    if (new_sample) {
-      KArgsPtr A = kargs();
-      // make_uv_jitter (render.rs:74-82): draws 2s, 2s+1 of a CLONE of the pixel-start stream =
-      // words 4s..4s+3 = block s/4, offset 4*(s%4).
-      uint32_t jb[16];
-      chacha12(rng.key, s >> 2, jb);
-      const uint32_t off = (s & 3u) * 4u;
-      uint32_t w0 = jb[0], w1 = jb[1], w2 = jb[2], w3 = jb[3];
-#pragma unroll
-      for (int q = 1; q < 4; q++) {
-        const bool m = off == 4u * q;
-        w0 = m ? jb[4 * q] : w0;
-        w1 = m ? jb[4 * q + 1] : w1;
-        w2 = m ? jb[4 * q + 2] : w2;
-        w3 = m ? jb[4 * q + 3] : w3;
-      }
-      const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
-      const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
-      // Camera::shoot (render.rs:32-52); tan(fov/2) computed on the host (same libm as the reference)
-      double dx, dy;
-      do {  // UnitDisk (randomness.rs:21-34), drawn even when lens_radius == 0
-        dx = 2.0 * gen_f64(rng) - 1.0;
-        dy = 2.0 * gen_f64(rng) - 1.0;
-      } while (!(dx * dx + dy * dy < 1.0));
-      A = kargs();
-      const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
-      const V3 lo = v3(lens * dx, lens * dy, 0.0);
-      const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
-      double m[9];
-#pragma unroll
-      for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
-      d = matvec(m, dl);
-      o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
-      T = v3(1.0, 1.0, 1.0);
-      L = v3(0.0, 0.0, 0.0);
-      depth = A->P.max_bounce;
-      first = true;
-      new_sample = false;
-    }
+  // ---- lane state: one pixel's path at a time
+  uint32_t slot = 0, pi = 0, pj = 0, s = 0, depth = 0, hits = 0;
+  bool first = true;
+  Rng rng;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 1), T = v3(1, 1, 1), L = v3(0, 0, 0), sum = v3(0, 0, 0);
+  bool alive = fetch_pixel(slot, pi, pj);
+  if (alive) {
+    KArgsPtr A = kargs();
+    seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);  // RNG contract
+    rng.pos = 0;
+    RngBlk rb;
+    rng_load(rng, rb);
+    start_sample(rng, rb, 0, pi, pj, o, d);
+    depth = A->P.max_bounce;
+  }
+  DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
 
-    DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; active += 1; })
-    // ---- trace (every live lane) ----
+  while (alive) {
+    DIAG(iters++; active++;)
+    // ---- trace (every live lane)
     HitRec hr;
     {
       KArgsPtr A = kargs();
       const KScene S = load_scene(A);
 #ifdef RPK_DIAG
-      const uint32_t v_before = td.visits;
-#ifdef RPK_DIAG_NOTD
-      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
-#else
       traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow, &td);
-#endif
-      wave_max[threadIdx.x >> 6] = 0;
-      __builtin_amdgcn_wave_barrier();
-      atomicMax(&wave_max[threadIdx.x >> 6], td.visits - v_before);
-      __builtin_amdgcn_wave_barrier();
-      td.trips += wave_max[threadIdx.x >> 6];
 #else
       traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
 #endif
     }
     DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
     n_rays++;
+
+    // ---- this iteration's keystream block, generated by every lane at once
+    RngBlk rb;
+    rng_load(rng, rb);
+
+    // ---- shade
     bool end_sample = true;
     if (hr.prim >= 0) {
       KArgsPtr A = kargs();
@@ -691,7 +708,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       surface(S, hr, o, d, h);
       const rpl::Material& m = S.mats[h.material];
       V3 nd;
-      const bool scattered = scatter_eval(m, d, h, rng, nd);   // order: scatter, absorb, emit
+      const bool scattered = scatter_eval(m, d, h, rng, rb, nd);   // order: scatter, absorb, emit
       const V3 ab = absorb_eval(S, m, h);
       const V3 em = emit_eval(S, m.emit_kind, m.emit_tex, m.emit_color, d, h);
       if (first) hits++;
@@ -710,20 +727,24 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       Surf h;
       h.p = d;
       h.n = d;
-      h.u = 0.5 - atan2(d.z, d.x) / TAU_;
-      h.v = asin(d.y) / PI_ + 0.5;
+      h.u = 0.0;
+      h.v = 0.0;
+      if (S.background.needs_uv) {
+        h.u = 0.5 - atan2(d.z, d.x) / TAU_;
+        h.v = asin(d.y) / PI_ + 0.5;
+      }
       const V3 em = emit_eval(S, S.background.kind, S.background.tex, S.background.color, d, h);
       L = add(L, mulc(T, em));
     }
-    DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
     first = false;
+
+    // ---- end of a camera sample: accumulate (main.rs:80), maybe finish the pixel, start the next one
     if (end_sample) {
-      sum = add(sum, L);  // main.rs:80
+      KArgsPtr A = kargs();
+      sum = add(sum, L);
       s++;
       n_samples++;
-      new_sample = true;
-      KArgsPtr A = kargs();
-      if (s == A->P.spp) {   // main.rs:86-87
+      if (s == A->P.spp) {  // main.rs:86-87
         const double spp = (double)A->P.spp;
         double* out = A->out;
         out[3 * (uint64_t)slot + 0] = sum.x / spp;
@@ -731,9 +752,26 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
         out[3 * (uint64_t)slot + 2] = sum.z / spp;
         if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
         n_pixels++;
-        need_pixel = true;
+        alive = fetch_pixel(slot, pi, pj);
+        if (alive) {
+          A = kargs();
+          seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);
+          rng.pos = 0;
+          s = 0;
+          hits = 0;
+          sum = v3(0.0, 0.0, 0.0);
+        }
+      }
+      if (alive) {
+        start_sample(rng, rb, s, pi, pj, o, d);
+        A = kargs();
+        depth = A->P.max_bounce;
+        T = v3(1.0, 1.0, 1.0);
+        L = v3(0.0, 0.0, 0.0);
+        first = true;
       }
     }
+    DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
   }
 
 #ifdef RPK_DIAG
@@ -780,7 +818,7 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
   double* oh = out_hit + 9 * i;
   if (hr.prim >= 0) {
     Surf h;
-    surface(S, hr, o, d, h);
+    surface(S, hr, o, d, h, true);  // Hittable::hit returns the full Hit record
     oh[0] = hr.t; oh[1] = h.p.x; oh[2] = h.p.y; oh[3] = h.p.z;
     oh[4] = h.n.x; oh[5] = h.n.y; oh[6] = h.n.z; oh[7] = h.u; oh[8] = h.v;
     out_mat[i] = h.material;

@@ -51,7 +51,7 @@ static_assert(sizeof(Prim) == 96, "Prim must be 96 B");
 // Material: rp_material flattened (material.rs:87-91).
 struct alignas(16) Material {
   uint32_t scatter_kind, absorb_kind, emit_kind, absorb_tex;
-  uint32_t emit_tex, pad0, pad1, pad2;
+  uint32_t emit_tex, needs_uv, pad1, pad2;  // needs_uv: a texture this material samples reads hit.uv
   double scatter_param;
   double absorb_color[3];
   double emit_color[3];
@@ -71,7 +71,8 @@ struct alignas(16) Texture {
 static_assert(sizeof(Texture) == 72 || sizeof(Texture) == 80, "Texture size");
 
 struct Emit {
-  uint32_t kind, tex;
+  uint32_t kind, tex;  // tex only read for SkySphere
+  uint32_t needs_uv, pad;
   double color[3];
 };
 

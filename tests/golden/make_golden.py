@@ -1,0 +1,382 @@
+"""Independent restatement (pure Python + numpy elementwise f64) of the reference's hot path, used to
+generate the golden fixtures that pin the C oracle (tests/test_oracle_golden.py).  Test infrastructure.
+
+    python tests/golden/make_golden.py     ->  tests/golden/golden.npz
+
+Written from the Rust sources (/root/reference/src), not from oracle/rp_oracle.c: Python floats and
+numpy f64 elementwise ops are IEEE binary64 with no FMA contraction, math.tan/atan2/asin/sqrt call the
+same libm as the C oracle, so the two restatements must agree bit for bit.  Closest hits here are
+brute force over every primitive (hit_list semantics, hittable.rs:110-120, vectorised with numpy
+in the reference's exact expression order) -- a different algorithm from the oracle's BVH, equal
+except for exact-t ties and measure-zero box-corner cases.
+
+Contents: RNG streams (seed_from_u64 -> ChaCha12 u64 draws), distribution samples, 3,000 ray hits on
+the bunny_full scene, and three small images (bunny C1 scene, Lambert C2 scene, full-material C3
+scene) under the per-pixel RNG contract.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [REPO, os.path.join(REPO, "raytracing-potato_amd")]
+
+M32 = 0xFFFFFFFF
+M64 = (1 << 64) - 1
+
+
+# ------------------------------------------------------------------ rand 0.8 StdRng (randomness.rs:5)
+def _rotl(x, n):
+    return ((x << n) | (x >> (32 - n))) & M32
+
+
+def chacha_block(key, counter, rounds=12):
+    s = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + list(key) + [counter & M32, counter >> 32, 0, 0]
+    x = list(s)
+
+    def qr(a, b, c, d):
+        x[a] = (x[a] + x[b]) & M32; x[d] = _rotl(x[d] ^ x[a], 16)
+        x[c] = (x[c] + x[d]) & M32; x[b] = _rotl(x[b] ^ x[c], 12)
+        x[a] = (x[a] + x[b]) & M32; x[d] = _rotl(x[d] ^ x[a], 8)
+        x[c] = (x[c] + x[d]) & M32; x[b] = _rotl(x[b] ^ x[c], 7)
+
+    for _ in range(rounds // 2):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    return [(x[i] + s[i]) & M32 for i in range(16)]
+
+
+class StdRng:
+    def __init__(self, key):
+        self.key = key
+        self.words = []
+        self.block = 0
+        self.idx = 0
+
+    @classmethod
+    def seed_from_u64(cls, state):  # rand_core 0.6: PCG32 expansion
+        key = []
+        state &= M64
+        for _ in range(8):
+            state = (state * 6364136223846793005 + 11634580027462260723) & M64
+            xs = (((state >> 18) ^ state) >> 27) & M32
+            rot = state >> 59
+            key.append(((xs >> rot) | (xs << ((32 - rot) & 31))) & M32)
+        return cls(key)
+
+    def clone(self):
+        c = StdRng(self.key)
+        c.words, c.block, c.idx = list(self.words), self.block, self.idx
+        return c
+
+    def next_u64(self):  # every draw of the hot path is a u64 (two words)
+        if self.idx >= len(self.words):
+            self.words = chacha_block(self.key, self.block)
+            self.block += 1
+            self.idx = 0
+        lo, hi = self.words[self.idx], self.words[self.idx + 1]
+        self.idx += 2
+        return (hi << 32) | lo
+
+    def gen(self):  # Standard f64
+        return (self.next_u64() >> 11) * (1.0 / 9007199254740992.0)
+
+
+def unit_disk(r):  # randomness.rs:21-34
+    while True:
+        x = 2.0 * r.gen() - 1.0
+        y = 2.0 * r.gen() - 1.0
+        if x * x + y * y < 1.0:
+            return (x, y)
+
+
+def unit_ball(r):  # randomness.rs:39-53
+    while True:
+        x = 2.0 * r.gen() - 1.0
+        y = 2.0 * r.gen() - 1.0
+        z = 2.0 * r.gen() - 1.0
+        if (x * x + y * y) + z * z < 1.0:
+            return (x, y, z)
+
+
+def unit_sphere(r):  # randomness.rs:58-73
+    while True:
+        x = 2.0 * r.gen() - 1.0
+        y = 2.0 * r.gen() - 1.0
+        s = x * x + y * y
+        if s < 1.0:
+            n = 2.0 * math.sqrt(1.0 - s)
+            return (x * n, y * n, 1.0 - 2.0 * s)
+
+
+# ------------------------------------------------------------------ vector helpers (nalgebra order)
+def add(a, b): return (a[0] + b[0], a[1] + b[1], a[2] + b[2])
+def sub(a, b): return (a[0] - b[0], a[1] - b[1], a[2] - b[2])
+def mulc(a, b): return (a[0] * b[0], a[1] * b[1], a[2] * b[2])
+def smul(s, a): return (s * a[0], s * a[1], s * a[2])
+def dot(a, b): return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+def normalize(a):
+    n = math.sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2])
+    return (a[0] / n, a[1] / n, a[2] / n)
+def reflect(i, n): return sub(i, smul(2.0 * dot(i, n), n))
+def matvec(m, v):  # column-major, column axpy accumulation
+    return ((v[0] * m[0] + v[1] * m[3]) + v[2] * m[6], (v[0] * m[1] + v[1] * m[4]) + v[2] * m[7],
+            (v[0] * m[2] + v[1] * m[5]) + v[2] * m[8])
+
+
+# ------------------------------------------------------------------ scene (plain Python data)
+class PyScene:
+    def __init__(self, scene):
+        sd = scene.scene_data
+        self.mats = sd.material_table
+        self.texs = sd.texture_table
+        self.background = scene.background
+        cam = scene.camera
+        self.cam = (cam.aspect_ratio, cam.fov, cam.focal_dist, cam.lens_radius,
+                    tuple(cam.transformation.orientation), tuple(cam.transformation.position))
+        root = scene.root
+        tri = root[root["kind"] == 1]
+        sph = root[root["kind"] == 0]
+        self.order = np.nonzero(root["kind"] == 1)[0].tolist() + np.nonzero(root["kind"] == 0)[0].tolist()
+        m = sd.mesh_table[0] if len(tri) else None
+        self.mesh = m
+        if len(tri):
+            idx = m.indices.reshape(-1)
+            t0 = tri["triangle"].astype(np.int64)
+            self.ia, self.ib, self.ic = idx[t0], idx[t0 + 1], idx[t0 + 2]
+            self.A, self.B, self.C = m.positions[self.ia], m.positions[self.ib], m.positions[self.ic]
+        else:
+            self.A = np.zeros((0, 3))
+        self.sph = [(tuple(h["center"]), float(h["radius"]), int(h["material"])) for h in sph]
+        self.root_order_tri = np.nonzero(root["kind"] == 1)[0]
+        self.root_order_sph = np.nonzero(root["kind"] == 0)[0]
+
+    # hit_list over all leaves in root order (hittable.rs:110-120), triangles vectorised
+    def hit(self, o, d, tmin=1e-3, tmax=math.inf):
+        best_t, best = tmax, None
+        cand = []
+        if len(self.A):
+            A, B, C = self.A, self.B, self.C
+            ba, ca = A - B, A - C
+            pa = A - np.array(o)
+            dx, dy, dz = d
+            det = (ba[:, 0] * ca[:, 1] * dz + ba[:, 1] * ca[:, 2] * dx + ba[:, 2] * ca[:, 0] * dy
+                   - ba[:, 0] * ca[:, 2] * dy - ba[:, 1] * ca[:, 0] * dz - ba[:, 2] * ca[:, 1] * dx)
+            with np.errstate(divide="ignore", invalid="ignore"):
+                inv = 1.0 / det
+                t = (pa[:, 0] * (ba[:, 1] * ca[:, 2] - ba[:, 2] * ca[:, 1])
+                     + pa[:, 1] * (ba[:, 2] * ca[:, 0] - ba[:, 0] * ca[:, 2])
+                     + pa[:, 2] * (ba[:, 0] * ca[:, 1] - ba[:, 1] * ca[:, 0])) * inv
+                u = (pa[:, 0] * (ca[:, 1] * dz - ca[:, 2] * dy)
+                     + pa[:, 1] * (ca[:, 2] * dx - ca[:, 0] * dz)
+                     + pa[:, 2] * (ca[:, 0] * dy - ca[:, 1] * dx)) * inv
+                v = (pa[:, 0] * (ba[:, 2] * dy - ba[:, 1] * dz)
+                     + pa[:, 1] * (ba[:, 0] * dz - ba[:, 2] * dx)
+                     + pa[:, 2] * (ba[:, 1] * dx - ba[:, 0] * dy)) * inv
+                w = 1.0 - u - v
+                ok = ~(np.abs(det) < 1e-7) & ~(t < tmin) & (u >= 0.0) & (v >= 0.0) & (w >= 0.0)
+            for k in np.nonzero(ok)[0]:
+                cand.append((int(self.root_order_tri[k]), "t", int(k), float(t[k]), float(u[k]), float(v[k])))
+        for k, (c, r, mat) in enumerate(self.sph):
+            cand.append((int(self.root_order_sph[k]), "s", k, None, None, None))
+        cand.sort()
+        for pos, kind, k, t, u, v in cand:  # t_max shrinks in list order; later equal t wins
+            if kind == "t":
+                if t > best_t:
+                    continue
+                best_t, best = t, ("t", k, u, v)
+            else:
+                c, r, mat = self.sph[k]
+                tc = sub(o, c)
+                a = dot(d, d)
+                hb = dot(d, tc)
+                cq = dot(tc, tc) - r * r
+                delta = hb * hb - a * cq
+                if delta <= 0.0:
+                    continue
+                sq = math.sqrt(delta)
+                tt = (-hb - sq) / a
+                if tt < tmin or tt > best_t:
+                    tt = (-hb + sq) / a
+                    if tt < tmin or tt > best_t:
+                        continue
+                best_t, best = tt, ("s", k, None, None)
+        if best is None:
+            return None
+        p = add(o, smul(best_t, d))
+        if best[0] == "t":
+            k, u, v = best[1], best[2], best[3]
+            w = 1.0 - u - v
+            m = self.mesh
+            n0, n1, n2 = (tuple(m.normals[i]) for i in (self.ia[k], self.ib[k], self.ic[k]))
+            uv0, uv1, uv2 = (tuple(m.uvs[i]) for i in (self.ia[k], self.ib[k], self.ic[k]))
+            n = add(add(smul(w, n0), smul(u, n1)), smul(v, n2))
+            uv = ((w * uv0[0] + u * uv1[0]) + v * uv2[0], (w * uv0[1] + u * uv1[1]) + v * uv2[1])
+            mat = m.material
+        else:
+            c, r, mat = self.sph[best[1]]
+            n = normalize(sub(p, c))
+            uv = (0.5 - math.atan2(n[2], n[0]) / (2.0 * math.pi), math.asin(n[1]) / math.pi + 0.5)
+        return best_t, p, n, uv, mat
+
+    def texture(self, tid, h):  # texture.rs:21-49 (kinds used by the configs)
+        t = self.texs[tid]
+        if t.kind == 2:
+            return t.color
+        if t.kind == 3:
+            img = t.image
+            hgt, wid = img.shape[0], img.shape[1]
+            x = min(max(h[3][0] * wid, 0.0), wid - 1.0)
+            y = min(max(h[3][1] * hgt, 0.0), hgt - 1.0)
+            px = img[int(y), int(x)]
+            return (float(px[0]) / 255.0, float(px[1]) / 255.0, float(px[2]) / 255.0)
+        raise NotImplementedError(t.kind)
+
+    def emit(self, e, d, h):  # material.rs:49-60
+        if e.kind == 0:
+            return (0.0, 0.0, 0.0)
+        if e.kind == 1:
+            return h[2]
+        if e.kind == 2:
+            return e.color
+        if e.kind == 3:
+            t = 0.5 * (d[1] / math.sqrt(dot(d, d)) + 1.0)
+            return add(smul(1.0 - t, (1.0, 1.0, 1.0)), smul(t, (0.5, 0.7, 1.0)))
+        return self.texture(e.texture, h)
+
+    def absorb(self, a, h):  # material.rs:74-81
+        if a.kind == 0:
+            return (0.0, 0.0, 0.0)
+        if a.kind == 1:
+            return (1.0, 1.0, 1.0)
+        if a.kind == 2:
+            return a.color
+        return self.texture(a.texture, h)
+
+    def scatter(self, sc, d, h, rng):  # material.rs:27-34, 115-179
+        n, p = h[2], h[1]
+        if sc.kind == 0:
+            return None
+        if sc.kind == 1:
+            if dot(n, d) > 0.0:
+                return None
+            return (p, normalize(add(n, unit_sphere(rng))))
+        if sc.kind == 2:
+            if dot(n, d) > 0.0:
+                return None
+            r = normalize(add(reflect(d, n), smul(sc.param, unit_ball(rng))))
+            if dot(n, r) < 0.0:
+                return None
+            return (p, r)
+        if dot(n, d) > 0.0:
+            eta, nn = sc.param, (-n[0], -n[1], -n[2])
+        else:
+            eta, nn = 1.0 / sc.param, n
+        r0 = ((1.0 - eta) / (1.0 + eta)) ** 2  # powi(2) == x * x
+        x = 1.0 + dot(nn, d)
+        refl = r0 + (1.0 - r0) * (x * ((x * x) * (x * x)))
+        if rng.gen() < refl:
+            return (p, reflect(d, nn))
+        cos = dot(nn, d)
+        k = 1.0 - eta * eta * (1.0 - cos * cos)
+        if k < 0.0:
+            return (p, reflect(d, nn))
+        return (p, sub(smul(eta, d), smul(eta * cos + math.sqrt(k), nn)))
+
+    def trace(self, o, d, depth, rng, counters):  # render.rs:94-146 (recursive)
+        if depth == 0:
+            return (0.0, 0.0, 0.0), False
+        counters[0] += 1
+        h = self.hit(o, d)
+        if h is None:
+            bd = (d, d)
+            uv = (0.5 - math.atan2(d[2], d[0]) / (2.0 * math.pi), math.asin(d[1]) / math.pi + 0.5)
+            return self.emit(self.background, d, (math.inf, d, d, uv)), False
+        m = self.mats[h[4]]
+        sc = self.scatter(m.scatter, d, h, rng)
+        ab = self.absorb(m.absorb, h)
+        em = self.emit(m.emit, d, h)
+        if sc is None:
+            return add(em, (0.0, 0.0, 0.0)), True
+        c, _ = self.trace(sc[0], sc[1], depth - 1, rng, counters)
+        return add(em, mulc(ab, c)), True
+
+    def render(self, W, H, spp, seed, max_bounce=8):
+        aspect, fov, focal, lens, orient, pos = self.cam
+        out = np.zeros((H, W, 3))
+        counters = [0]
+        for j in range(H):
+            for i in range(W):
+                rng = StdRng.seed_from_u64(seed + j * W + i)
+                jit = rng.clone()  # render.rs:75
+                acc = (0.0, 0.0, 0.0)
+                for _ in range(spp):
+                    u = (i + jit.gen()) / W
+                    v = (j + jit.gen()) / H
+                    tanf = math.tan(0.5 * fov)
+                    dx, dy = unit_disk(rng)
+                    lo = (lens * dx, lens * dy, 0.0)
+                    dl = normalize(sub(((2.0 * u - 1.0) * tanf * focal * aspect, (2.0 * v - 1.0) * tanf * focal,
+                                        -focal), lo))
+                    d = matvec(orient, dl)
+                    o = add(matvec(orient, lo), pos)
+                    c, _ = self.trace(o, d, max_bounce, rng, counters)
+                    acc = add(acc, c)
+                out[j, i] = (acc[0] / spp, acc[1] / spp, acc[2] / spp)
+        return out, counters[0]
+
+
+def main():
+    from rtpotato import scenes
+    out = {}
+    seeds = np.array([0, 1, 0x5EED0001, 2**64 - 1], dtype=np.uint64)
+    out["rng_seeds"] = seeds
+    out["rng_u64"] = np.array([[StdRng.seed_from_u64(int(s)).next_u64() if k == 0 else 0 for k in range(1)]
+                               for s in seeds], dtype=np.uint64)
+    streams = []
+    for s in seeds:
+        r = StdRng.seed_from_u64(int(s))
+        streams.append([r.next_u64() for _ in range(40)])
+    out["rng_u64"] = np.array(streams, dtype=np.uint64)
+    r = StdRng.seed_from_u64(12345)
+    out["dist_disk"] = np.array([unit_disk(r) for _ in range(200)])
+    out["dist_ball"] = np.array([unit_ball(r) for _ in range(200)])
+    out["dist_sphere"] = np.array([unit_sphere(r) for _ in range(200)])
+    out["dist_next_u64"] = np.array([r.next_u64()], dtype=np.uint64)
+
+    # ray-level hits on the C3 scene
+    scene = scenes.bunny_full()
+    ps = PyScene(scene)
+    rng = np.random.default_rng(7)
+    n = 3000
+    o = rng.uniform(-2.5, 2.5, size=(n, 3))
+    o[:, 1] = rng.uniform(-0.5, 2.5, size=n)
+    d = rng.uniform(-0.8, 0.8, size=(n, 3)) + np.array([0.0, 0.7, 0.0]) - o
+    rays = np.concatenate([o, d, np.full((n, 1), 1e-3), np.full((n, 1), np.inf)], axis=1)
+    hits = np.zeros((n, 9))
+    mats = np.full(n, 0xFFFFFFFF, dtype=np.uint32)
+    for k in range(n):
+        h = ps.hit(tuple(rays[k, 0:3]), tuple(rays[k, 3:6]))
+        if h is None:
+            hits[k, 0] = np.inf
+        else:
+            hits[k] = [h[0], *h[1], *h[2], *h[3]]
+            mats[k] = h[4]
+    out["rays"], out["ray_hits"], out["ray_mats"] = rays, hits, mats
+
+    # small images under the RNG contract
+    for name, (W, H, spp) in {"bunny": (16, 9, 2), "bunny_lambert": (12, 8, 2), "bunny_full": (12, 8, 2)}.items():
+        sc = scenes.configure(scenes.CATALOGUE[name](), W, H)
+        img, rays_n = PyScene(sc).render(W, H, spp, scenes.DEFAULT_SEED)
+        out[f"img_{name}"] = img
+        out[f"img_{name}_rays"] = np.array([rays_n])
+        out[f"img_{name}_size"] = np.array([W, H, spp])
+        print(name, img.mean(axis=(0, 1)), rays_n, flush=True)
+    np.savez_compressed(os.path.join(HERE, "golden.npz"), **out)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,22 @@
+"""Timing-only ablation A/B (NOT parity builds): C3 frame time per library variant, interleaved rounds."""
+import os, sys, json, subprocess
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+libs = sys.argv[1:]
+res = {}
+for rnd in range(2):
+    for lib in libs:
+        code = f"""
+import os,sys
+sys.path[:0]=['{REPO}','{REPO}/raytracing-potato_amd']
+os.environ['RP_LIB']='{REPO}/raytracing-potato_amd/lib/{lib}'
+from dataclasses import replace
+from rtpotato import scenes
+from rtpotato.render import DeviceScene
+sc,p=scenes.config_scene('C3'); p=replace(p, spp=64)
+ds=DeviceScene(sc); ds.render(replace(p,spp=4))
+ts=[ds.render(p)[2]['seconds'] for _ in range(2)]
+print(min(ts))
+"""
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        res.setdefault(lib, []).append(float(out.stdout.strip().split()[-1]) if out.returncode == 0 else out.stderr[-300:])
+print(json.dumps(res))
