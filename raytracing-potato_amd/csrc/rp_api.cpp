@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -67,6 +68,7 @@ struct rp_scene {
   uint32_t* d_texels = nullptr;
   uint64_t* d_ws = nullptr;  // default counter block (8 x u64)
   uint64_t* d_diag = nullptr;  // diagnostic counters (rpk::DIAG_N)
+  uint32_t* d_slab = nullptr;  // keystream cache, one slab per resident render lane
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
   uint32_t max_depth = 0;
   int num_cu = 0;
@@ -97,6 +99,18 @@ int make_tiling(const rp_render_params* p, Tiling& t) {
   return RP_OK;
 }
 
+// Lanes of a wave keep stepping traversal while at least this many are still traversing; below it,
+// the finished lanes shade and take new rays (1 = wait for every lane, 64 = shade eagerly).
+// Override with RP_TRAV_THRESHOLD for tuning.
+uint32_t trav_threshold() {
+  static const uint32_t v = [] {
+    const char* e = std::getenv("RP_TRAV_THRESHOLD");
+    long x = e ? std::strtol(e, nullptr, 10) : 24;
+    return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
+  }();
+  return v;
+}
+
 }  // namespace
 
 extern "C" {
@@ -121,7 +135,7 @@ void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
-                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag})
+                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -181,6 +195,10 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   int bpc = 0;
   if (rpk::render_blocks_per_cu(s->ks.stack_depth, &bpc) != 0 || bpc < 1) bpc = 1;
   s->blocks_per_cu = bpc;
+  const uint64_t lanes = (uint64_t)s->num_cu * (uint64_t)bpc * rpk::RENDER_BLOCK;
+  if (hipMalloc(reinterpret_cast<void**>(&s->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess)
+    return bail(fail(RP_ENOMEM, "hipMalloc keystream cache"));
+  s->ks.rng_slab = s->d_slab;
   *out = s;
   return RP_OK;
 }
@@ -266,6 +284,7 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
   kp.tiles_x = t.tiles_x;
   kp.n_shard_tiles = t.n_shard_tiles;
   kp.n_slots = t.n_slots;
+  kp.trav_threshold = trav_threshold();
   uint64_t want = (t.n_slots + 255) / 256;
   uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
   int grid = (int)(want < resident ? want : resident);

@@ -18,7 +18,13 @@ struct KScene {
   uint32_t root;
   uint32_t stack_depth;  // LDS traversal stack entries per lane (>= max_depth + 2)
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
+  uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
 };
+
+// Bytes of keystream cache (ChaCha key, ring of main-stream blocks, jitter blocks) per resident lane of
+// the render kernel; the render grid never exceeds the lanes the slab was sized for.
+uint64_t rng_slab_bytes_per_lane();
+enum { RENDER_BLOCK = 256 };
 
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
@@ -34,6 +40,8 @@ struct KParams {
   uint32_t tw, th, shard, nshards;
   uint32_t tiles_x, n_shard_tiles;
   uint64_t n_slots;  // n_shard_tiles * tw * th
+  uint32_t trav_threshold;  // resume shading once fewer than this many lanes of a wave still traverse
+  uint32_t pad;
 };
 
 // Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.

@@ -38,7 +38,7 @@ RPK_INLINE uint64_t stamp() {
 #define DIAG(...)
 #endif
 
-static constexpr int BLOCK = 256;
+static constexpr int BLOCK = RENDER_BLOCK;
 static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
 static constexpr double SMOL = 1e-7;         // utility.rs:31
 static constexpr double PI_ = 3.14159265358979323846;
@@ -94,23 +94,130 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 
 // Main stream of one pixel.  Every draw on the path is a u64 (Standard f64), so the stream is the
 // keystream read two words at a time from word `pos`: exactly rand_chacha's 4-block-buffered stream.
-// The 16-word block holding `pos` lives in registers only inside one loop iteration (RngBlk): it is
-// generated once per iteration for every lane at the same point (uniform across the wave), and a lane
-// regenerates only when its draws actually cross into the next block.  (Refilling a per-lane buffer
-// inside the rejection loops made the wave pay a whole ChaCha12 block whenever ANY lane ran dry:
-// 24% of the kernel at C3.)
+//
+// Keystream blocks are produced ahead of use into a per-lane slab in global memory (L2/MALL resident,
+// ~0.7 KB per lane): a ring of RING main-stream blocks and the two camera-jitter blocks the next
+// samples need.  Production happens in ONE place per round of the render loop (rng_refill), for every
+// lane that has room, so a ChaCha12 block (~600 VALU) runs with nearly all 64 lanes doing useful work;
+// the draw sites only load 16-word blocks from the ring.  Generating at the draw sites instead made the
+// wave pay a whole block whenever ANY lane crossed a block boundary (several per round at C3).  A draw
+// that finds the ring empty still generates its block in place (rare: the refill pass keeps > RNG_CRIT
+// blocks ahead of every lane).
+//
+// Slab layout per lane (uint4 units): [0,2) key words, [2, 2+4*RING) ring (block b in slot b % RING),
+// [2+4*RING, +8) jitter blocks (block b in slot b & 1).  Per-lane cursors (LDS): end = one past the
+// newest ring block; jtag[2] = block held by each jitter slot.
+static constexpr uint32_t RING = 8;
+static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_N = SLAB_JIT + 8;
+static constexpr uint32_t RNG_CRIT = 2;    // a lane holding <= this many blocks forces a refill pass
+static constexpr uint32_t RNG_BATCH = 48;  // ... as do this many lanes with room
+
 struct Rng {
-  uint32_t key[8];
-  uint32_t pos;  // next keystream word (even)
+  uint4* slab;     // global: this lane's slab
+  uint32_t pos;    // next keystream word (even)
+  uint32_t* end;   // LDS cursor: one past the newest ring block
+  uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
 struct RngBlk {
   uint32_t w[16];
   uint32_t blk;  // block index held in w
 };
 
+RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
+  const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
+  k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+  k[4] = c.x; k[5] = c.y; k[6] = c.z; k[7] = c.w;
+}
+RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
+  r.slab[SLAB_KEY] = make_uint4(k[0], k[1], k[2], k[3]);
+  r.slab[SLAB_KEY + 1] = make_uint4(k[4], k[5], k[6], k[7]);
+}
+RPK_INLINE void store_block(uint4* dst, const uint32_t w[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = src[q];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+}
+RPK_INLINE uint4* ring_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_RING + 4 * (b % RING); }
+RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT + 4 * (b & 1u); }
+
+// Block pos/16 into registers: from the ring, or generated in place when the ring ran dry.
 RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
   b.blk = r.pos >> 4;
-  chacha12(r.key, b.blk, b.w);
+  if (b.blk < *r.end) {
+    load_block(ring_slot(r, b.blk), b.w);
+  } else {
+    uint32_t k[8];
+    load_key(r, k);
+    chacha12(k, b.blk, b.w);
+    store_block(ring_slot(r, b.blk), b.w);
+    *r.end = b.blk + 1;
+  }
+}
+
+// A new pixel: key from the RNG contract seed, block 0 (shared by the main stream and the jitter of
+// samples 0-3, render.rs:74-82) generated once into both caches and into registers.
+RPK_INLINE void rng_begin_pixel(Rng& r, RngBlk& b, uint64_t seed) {
+  uint32_t k[8];
+  seed_key(seed, k);
+  store_key(r, k);
+  chacha12(k, 0, b.w);
+  b.blk = 0;
+  store_block(ring_slot(r, 0), b.w);
+  store_block(jit_slot(r, 0), b.w);
+  r.pos = 0;
+  *r.end = 1;
+  r.jtag[0] = 0;
+  r.jtag[BLOCK] = 0xFFFFFFFFu;
+}
+
+// The refill pass (wave-uniform call site).  `s` is the lane's in-flight sample, whose jitter is
+// already consumed; samples s+1.. need jitter blocks (s+1)/4 and the one after.
+RPK_INLINE void rng_refill(Rng& r, bool alive, uint32_t s, uint32_t spp) {
+  const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
+  const uint32_t b1 = (s + 1) >> 2, b2 = b1 + 1;
+  const bool j1 = alive && 4 * b1 < spp && r.jtag[(b1 & 1u) * BLOCK] != b1;
+  const bool j2 = alive && 4 * b2 < spp && r.jtag[(b2 & 1u) * BLOCK] != b2;
+  const bool crit = alive && have <= RNG_CRIT;
+  const bool room = alive && (have < RING || j1 || j2);
+  if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
+  if (room) {
+    const bool main = crit || !(j1 || j2);
+    const uint32_t b = main ? end : (j1 ? b1 : b2);
+    uint32_t k[8], w[16];
+    load_key(r, k);
+    chacha12(k, b, w);
+    store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);
+    if (main) *r.end = end + 1;
+    else r.jtag[(b & 1u) * BLOCK] = b;
+  }
+}
+
+// Jitter words 4s..4s+3 of the pixel-start stream (block s/4).
+RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
+  const uint32_t b = s >> 2;
+  if (r.jtag[(b & 1u) * BLOCK] == b) return jit_slot(r, b)[s & 3u];
+  uint32_t k[8], w[16];
+  load_key(r, k);
+  chacha12(k, b, w);
+  store_block(jit_slot(r, b), w);
+  r.jtag[(b & 1u) * BLOCK] = b;
+  const uint32_t o = (s & 3u) * 4u;
+  uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
+#pragma unroll
+  for (int q = 1; q < 4; q++) {
+    const bool m = o == 4u * q;
+    v.x = m ? w[4 * q] : v.x;
+    v.y = m ? w[4 * q + 1] : v.y;
+    v.z = m ? w[4 * q + 2] : v.z;
+    v.w = m ? w[4 * q + 3] : v.w;
+  }
+  return v;
 }
 
 RPK_INLINE uint64_t next_u64(Rng& r, RngBlk& b) {
@@ -243,130 +350,159 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, Ray32& r) {
 // (hittable.rs:52,99).  Structure: "while-while" -- descend inner nodes (near child first, the others
 // pushed far-to-near on the LDS stack) until this lane holds a leaf, then test the leaf's primitives;
 // the wave runs the expensive f64 leaf code once for every lane that reached a leaf.
+//
+// The traversal state is explicit (TravState) so a lane can stop between steps and resume later: the
+// render kernel steps traversal until few lanes are still traversing, shades the finished ones and
+// gives them new rays, then resumes (see render_kernel).
+struct TravState {
+  double best, bu, bv;
+  int32_t bestp;
+  uint32_t cur, sp;
+};
+
+RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
+  t.best = tmax;
+  t.bu = 0.0;
+  t.bv = 0.0;
+  t.bestp = -1;
+  t.cur = S.root;
+  t.sp = 0;
+}
+
+// One step: descend to a leaf, test it, pop the next entry.  t.cur == ENTRY_EMPTY when finished.
+RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const Ray32& r, V3 o, V3 d,
+                          double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
+  uint32_t cur = ts.cur, sp = ts.sp;
+  double best = ts.best;
+  float best32 = f32_up(best);
+  const uint32_t cap = S.stack_depth;
+  // ---- inner nodes
+  while (!(cur & rpl::ENTRY_LEAF)) {
+    DIAG(if (td) td->visits++;)
+    const rpl::Node4* n = S.nodes + cur;
+    const float4 lx = *reinterpret_cast<const float4*>(n->lo_x);
+    const float4 hx = *reinterpret_cast<const float4*>(n->hi_x);
+    const float4 ly = *reinterpret_cast<const float4*>(n->lo_y);
+    const float4 hy = *reinterpret_cast<const float4*>(n->hi_y);
+    const float4 lz = *reinterpret_cast<const float4*>(n->lo_z);
+    const float4 hz = *reinterpret_cast<const float4*>(n->hi_z);
+    const uint4 ch = *reinterpret_cast<const uint4*>(n->child);
+    float tn[4];
+    uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const float ax = __builtin_fmaf(LX[c], r.ix, -r.oix), bx = __builtin_fmaf(HX[c], r.ix, -r.oix);
+      const float ay = __builtin_fmaf(LY[c], r.iy, -r.oiy), by = __builtin_fmaf(HY[c], r.iy, -r.oiy);
+      const float az = __builtin_fmaf(LZ[c], r.iz, -r.oiz), bz = __builtin_fmaf(HZ[c], r.iz, -r.oiz);
+      const float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
+      const float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
+      const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 0x1p-19f, tfar) + r.slack && cc[c] != rpl::ENTRY_EMPTY;
+      tn[c] = hit ? tnear : __builtin_huge_valf();
+    }
+    // sort (tn, entry) ascending: misses (+inf) go last
+#define RPK_CSWAP(a, b)                                   \
+{                                                       \
+  const bool sw = tn[b] < tn[a];                        \
+  const float t_ = sw ? tn[b] : tn[a];                  \
+  tn[b] = sw ? tn[a] : tn[b];                           \
+  tn[a] = t_;                                           \
+  const uint32_t c_ = sw ? cc[b] : cc[a];               \
+  cc[b] = sw ? cc[a] : cc[b];                           \
+  cc[a] = c_;                                           \
+}
+    RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
+#undef RPK_CSWAP
+    const float INFF = __builtin_huge_valf();
+    // push the farther hits far-to-near, continue with the nearest
+#pragma unroll
+    for (int c = 3; c >= 1; c--) {
+      if (tn[c] != INFF) {
+        if (sp < cap) stk[(sp++) * stride] = cc[c];
+        else overflow = true;
+      }
+    }
+    if (tn[0] != INFF) cur = cc[0];
+    else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+  }
+  if (cur == rpl::ENTRY_EMPTY) {
+    ts.cur = cur;
+    ts.sp = sp;
+    return;
+  }
+  // ---- leaf: the reference's exact f64 primitive tests
+  const uint32_t first = cur & rpl::LEAF_FIRST_MASK;
+  const uint32_t cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
+  for (uint32_t k = first; k < first + cnt; k++) {
+    DIAG(if (td) td->tests++;)
+    const rpl::Prim* p = S.prims + k;
+    const double2 g01 = *reinterpret_cast<const double2*>(p->g);
+    const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
+    const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
+    const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
+    const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
+    const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+    if (kind == rpl::PRIM_TRIANGLE) {
+      // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
+      const V3 a = v3(g01.x, g01.y, g23.x);
+      const V3 ba = v3(g23.y, g45.x, g45.y);
+      const V3 ca = v3(g67.x, g67.y, g8k.x);
+      const V3 pa = sub(a, o);
+      const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                       - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
+      if (fabs(det) < SMOL) continue;
+      const double inv_det = 1.0 / det;
+      const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                      + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                      + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+      const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                      + pa.y * (ca.z * d.x - ca.x * d.z)
+                      + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+      const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                      + pa.y * (ba.x * d.z - ba.z * d.x)
+                      + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
+      const double w = 1.0 - u - v;
+      if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
+      best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
+    } else {
+      // hittable.rs:39-57
+      const V3 c = v3(g01.x, g01.y, g23.x);
+      const double radius = g23.y;
+      const V3 tc = sub(o, c);
+      const double a = norm2(d);
+      const double half_b = dot(d, tc);
+      const double cq = norm2(tc) - radius * radius;
+      const double delta = half_b * half_b - a * cq;
+      if (delta <= 0.0) continue;
+      const double sq = sqrt(delta);
+      double t = (-half_b - sq) / a;
+      if (t < tmin || t > best) {
+        t = (-half_b + sq) / a;
+        if (t < tmin || t > best) continue;
+      }
+      best = t; ts.bestp = (int32_t)k;
+    }
+    best32 = f32_up(best);
+  }
+  cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+  ts.cur = cur;
+  ts.sp = sp;
+  ts.best = best;
+}
+
 RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
                          HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
   Ray32 r;
   setup_ray32(o, d, tmin, r);
-  double best = tmax;
-  float best32 = f32_up(tmax);
-  int32_t bestp = -1;
-  double bu = 0.0, bv = 0.0;
-  uint32_t cur = S.root;
-  uint32_t sp = 0;
-  const uint32_t cap = S.stack_depth;
-  for (;;) {
-    // ---- inner nodes
-    while (!(cur & rpl::ENTRY_LEAF)) {
-      DIAG(if (td) td->visits++;)
-      const rpl::Node4* n = S.nodes + cur;
-      const float4 lx = *reinterpret_cast<const float4*>(n->lo_x);
-      const float4 hx = *reinterpret_cast<const float4*>(n->hi_x);
-      const float4 ly = *reinterpret_cast<const float4*>(n->lo_y);
-      const float4 hy = *reinterpret_cast<const float4*>(n->hi_y);
-      const float4 lz = *reinterpret_cast<const float4*>(n->lo_z);
-      const float4 hz = *reinterpret_cast<const float4*>(n->hi_z);
-      const uint4 ch = *reinterpret_cast<const uint4*>(n->child);
-      float tn[4];
-      uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
-      const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-      const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-      const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const float ax = __builtin_fmaf(LX[c], r.ix, -r.oix), bx = __builtin_fmaf(HX[c], r.ix, -r.oix);
-        const float ay = __builtin_fmaf(LY[c], r.iy, -r.oiy), by = __builtin_fmaf(HY[c], r.iy, -r.oiy);
-        const float az = __builtin_fmaf(LZ[c], r.iz, -r.oiz), bz = __builtin_fmaf(HZ[c], r.iz, -r.oiz);
-        const float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
-        const float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
-        const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 0x1p-19f, tfar) + r.slack && cc[c] != rpl::ENTRY_EMPTY;
-        tn[c] = hit ? tnear : __builtin_huge_valf();
-      }
-      // sort (tn, entry) ascending: misses (+inf) go last
-#define RPK_CSWAP(a, b)                                   \
-  {                                                       \
-    const bool sw = tn[b] < tn[a];                        \
-    const float t_ = sw ? tn[b] : tn[a];                  \
-    tn[b] = sw ? tn[a] : tn[b];                           \
-    tn[a] = t_;                                           \
-    const uint32_t c_ = sw ? cc[b] : cc[a];               \
-    cc[b] = sw ? cc[a] : cc[b];                           \
-    cc[a] = c_;                                           \
-  }
-      RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
-#undef RPK_CSWAP
-      const float INFF = __builtin_huge_valf();
-      // push the farther hits far-to-near, continue with the nearest
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        if (tn[c] != INFF) {
-          if (sp < cap) stk[(sp++) * stride] = cc[c];
-          else overflow = true;
-        }
-      }
-      if (tn[0] != INFF) cur = cc[0];
-      else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
-    }
-    if (cur == rpl::ENTRY_EMPTY) break;
-    // ---- leaf: the reference's exact f64 primitive tests
-    const uint32_t first = cur & rpl::LEAF_FIRST_MASK;
-    const uint32_t cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
-    for (uint32_t k = first; k < first + cnt; k++) {
-      DIAG(if (td) td->tests++;)
-      const rpl::Prim* p = S.prims + k;
-      const double2 g01 = *reinterpret_cast<const double2*>(p->g);
-      const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
-      const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
-      const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
-      const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
-      const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
-      if (kind == rpl::PRIM_TRIANGLE) {
-        // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
-        const V3 a = v3(g01.x, g01.y, g23.x);
-        const V3 ba = v3(g23.y, g45.x, g45.y);
-        const V3 ca = v3(g67.x, g67.y, g8k.x);
-        const V3 pa = sub(a, o);
-        const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
-                         - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
-        if (fabs(det) < SMOL) continue;
-        const double inv_det = 1.0 / det;
-        const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
-                        + pa.y * (ba.z * ca.x - ba.x * ca.z)
-                        + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
-        const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
-                        + pa.y * (ca.z * d.x - ca.x * d.z)
-                        + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
-        const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
-                        + pa.y * (ba.x * d.z - ba.z * d.x)
-                        + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
-        const double w = 1.0 - u - v;
-        if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
-        best = t; bestp = (int32_t)k; bu = u; bv = v;
-      } else {
-        // hittable.rs:39-57
-        const V3 c = v3(g01.x, g01.y, g23.x);
-        const double radius = g23.y;
-        const V3 tc = sub(o, c);
-        const double a = norm2(d);
-        const double half_b = dot(d, tc);
-        const double cq = norm2(tc) - radius * radius;
-        const double delta = half_b * half_b - a * cq;
-        if (delta <= 0.0) continue;
-        const double sq = sqrt(delta);
-        double t = (-half_b - sq) / a;
-        if (t < tmin || t > best) {
-          t = (-half_b + sq) / a;
-          if (t < tmin || t > best) continue;
-        }
-        best = t; bestp = (int32_t)k;
-      }
-      best32 = f32_up(best);
-    }
-    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
-  }
-  hr.t = best;
-  hr.u = bu;
-  hr.v = bv;
-  hr.prim = bestp;
+  TravState t;
+  trav_init(S, tmax, t);
+  while (t.cur != rpl::ENTRY_EMPTY) trav_step(S, stk, stride, r, o, d, tmin, t, overflow, td);
+  hr.t = t.best;
+  hr.u = t.bu;
+  hr.v = t.bv;
+  hr.prim = t.bestp;
 }
 
 // Hit record of the closest primitive (hittable.rs:59-62, 103-107).
@@ -378,7 +514,7 @@ struct Surf {
 
 // uv is computed only when the hit material reads it (rpl::Material::needs_uv): same values, and the
 // f64 atan2/asin of a sphere hit are skipped for untextured spheres (the ground).
-RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, bool force_uv = false) {
+RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, bool force_uv = false) {
   const rpl::Prim* p = S.prims + hr.prim;
   s.p = add(o, smul(hr.t, d));  // Ray::at (utility.rs:67)
   s.material = p->material;
@@ -399,11 +535,9 @@ RPK_INLINE void surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, 
   } else {
     const V3 c = v3(p->g[0], p->g[1], p->g[2]);
     s.n = normalize(sub(s.p, c));
-    if (need_uv) {
-      s.u = 0.5 - atan2(s.n.z, s.n.x) / TAU_;
-      s.v = asin(s.n.y) / PI_ + 0.5;
-    }
+    return need_uv;  // the caller computes the sphere uv (shared site)
   }
+  return false;
 }
 
 // ------------------------------------------------------------------ shading ----------------------
@@ -471,26 +605,26 @@ RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
   }
 }
 
-// material.rs:49-60 Emit::evaluate
-RPK_INLINE V3 emit_eval(const KScene& S, uint32_t kind, uint32_t tex, const double* color, V3 d, const Surf& h) {
+// material.rs:49-60 Emit::evaluate (SkySphere's texture value sampled by the caller)
+RPK_INLINE V3 emit_eval(uint32_t kind, V3 color, V3 tex, V3 d, const Surf& h) {
   switch (kind) {
     case 1: return h.n;                                  // DebugNormals
-    case 2: return v3(color[0], color[1], color[2]);     // Color
+    case 2: return color;                                // Color
     case 3: {                                            // SkyGradient
       const double t = 0.5 * (d.y / sqrt(norm2(d)) + 1.0);
       return add(smul(1.0 - t, v3(1.0, 1.0, 1.0)), smul(t, v3(0.5, 0.7, 1.0)));
     }
-    case 4: return tex_sample(S, tex, h);                // SkySphere
+    case 4: return tex;                                  // SkySphere
     default: return v3(0.0, 0.0, 0.0);                   // None
   }
 }
 
-// material.rs:74-81 Absorb::evaluate
-RPK_INLINE V3 absorb_eval(const KScene& S, const rpl::Material& m, const Surf& h) {
+// material.rs:74-81 Absorb::evaluate (AlbedoMap's texture value sampled by the caller)
+RPK_INLINE V3 absorb_eval(const rpl::Material& m, V3 tex) {
   switch (m.absorb_kind) {
     case 1: return v3(1.0, 1.0, 1.0);
     case 2: return v3(m.absorb_color[0], m.absorb_color[1], m.absorb_color[2]);
-    case 3: return tex_sample(S, m.absorb_tex, h);
+    case 3: return tex;
     default: return v3(0.0, 0.0, 0.0);
   }
 }
@@ -586,6 +720,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.background.color[2] = A->S.background.color[2];
   S.root = A->S.root;
   S.stack_depth = A->S.stack_depth;
+  S.rng_slab = A->S.rng_slab;
   return S;
 }
 
@@ -618,18 +753,8 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
 // (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
 RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
   KArgsPtr A = kargs();
-  uint32_t jb[16];
-  chacha12(rng.key, s >> 2, jb);
-  const uint32_t off = (s & 3u) * 4u;
-  uint32_t w0 = jb[0], w1 = jb[1], w2 = jb[2], w3 = jb[3];
-#pragma unroll
-  for (int q = 1; q < 4; q++) {
-    const bool m = off == 4u * q;
-    w0 = m ? jb[4 * q] : w0;
-    w1 = m ? jb[4 * q + 1] : w1;
-    w2 = m ? jb[4 * q + 2] : w2;
-    w3 = m ? jb[4 * q + 3] : w3;
-  }
+  const uint4 jw = rng_jitter(rng, s);
+  const uint32_t w0 = jw.x, w1 = jw.y, w2 = jw.z, w3 = jw.w;
   const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
   const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
   double dx, dy;
@@ -662,113 +787,192 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   bool overflow = false;
   DIAG(uint64_t ph[5] = {0, 0, 0, 0, 0}; uint64_t iters = 0, active = 0; TravDiag td; uint64_t t_prev = stamp();)
 
-  // ---- lane state: one pixel's path at a time
-  uint32_t slot = 0, pi = 0, pj = 0, s = 0, depth = 0, hits = 0;
+  // ---- lane state: one pixel's path at a time.  Hot state (ray, throughput, radiance, traversal)
+  // in registers; cold per-pixel state (pixel sum, slot/pixel/sample counters, keystream cursors) in
+  // LDS, structure-of-arrays so every access is bank-conflict-free; keystream blocks in the slab.
+  __shared__ double c_sum[3 * BLOCK];
+  __shared__ double c_T[3 * BLOCK];
+  __shared__ uint32_t c_u[8 * BLOCK];
+  const uint32_t tid = threadIdx.x;
+  uint32_t& slot = c_u[tid];
+  uint32_t& pi = c_u[BLOCK + tid];
+  uint32_t& pj = c_u[2 * BLOCK + tid];
+  uint32_t& s = c_u[3 * BLOCK + tid];
+  uint32_t& hits = c_u[4 * BLOCK + tid];
+  double& sum_x = c_sum[tid];
+  double& sum_y = c_sum[BLOCK + tid];
+  double& sum_z = c_sum[2 * BLOCK + tid];
+  double& T_x = c_T[tid];  // path throughput (read and written once per shade)
+  double& T_y = c_T[BLOCK + tid];
+  double& T_z = c_T[2 * BLOCK + tid];
+  uint32_t depth = 0;
   bool first = true;
   Rng rng;
-  V3 o = v3(0, 0, 0), d = v3(0, 0, 1), T = v3(1, 1, 1), L = v3(0, 0, 0), sum = v3(0, 0, 0);
+  rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N;
+  rng.end = c_u + 5 * BLOCK + tid;
+  rng.jtag = c_u + 6 * BLOCK + tid;
+  rng.pos = 0;
+  V3 o = v3(0, 0, 0), d = v3(0, 0, 1);
+  T_x = T_y = T_z = 1.0;
+  s = 0;
+  hits = 0;
+  sum_x = sum_y = sum_z = 0.0;
+  TravState ts;
   bool alive = fetch_pixel(slot, pi, pj);
+  bool tdone = true;  // traversal of the current ray finished (or no ray)
   if (alive) {
     KArgsPtr A = kargs();
-    seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);  // RNG contract
-    rng.pos = 0;
     RngBlk rb;
-    rng_load(rng, rb);
+    rng_begin_pixel(rng, rb, A->P.seed + (uint64_t)pj * A->P.W + pi);  // RNG contract
     start_sample(rng, rb, 0, pi, pj, o, d);
     depth = A->P.max_bounce;
+    trav_init(load_scene(A), INF, ts);
+    tdone = false;
   }
   DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
 
-  while (alive) {
-    DIAG(iters++; active++;)
-    // ---- trace (every live lane)
-    HitRec hr;
+  // Every lane of the wave stays in this loop until the whole wave has retired, so the ballots below
+  // see all 64 lanes.  Each round: step the traversal of the lanes that are still traversing until
+  // fewer than trav_threshold of them remain (and some finished lane is waiting), then shade the
+  // finished lanes and give them their next ray; unfinished lanes resume where they stopped (their
+  // node, LDS stack and closest hit so far are kept).
+  for (;;) {
+    DIAG(iters++;)
+    rng_refill(rng, alive, s, kargs()->P.spp);
+    DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
     {
       KArgsPtr A = kargs();
       const KScene S = load_scene(A);
+      const uint32_t thr = A->P.trav_threshold;
+      Ray32 r;
+      setup_ray32(o, d, RAY_EPSILON, r);
+      for (;;) {
+        if (alive && !tdone) {
 #ifdef RPK_DIAG
-      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow, &td);
+          trav_step(S, stk, BLOCK, r, o, d, RAY_EPSILON, ts, overflow, &td);
 #else
-      traverse(S, stk, BLOCK, o, d, RAY_EPSILON, INF, hr, overflow);
+          trav_step(S, stk, BLOCK, r, o, d, RAY_EPSILON, ts, overflow);
 #endif
+          tdone = ts.cur == rpl::ENTRY_EMPTY;
+        }
+        const uint64_t act = __ballot(alive && !tdone);
+        const uint64_t waiting = __ballot(alive && tdone);
+        if (act == 0 || (waiting != 0 && (uint32_t)__popcll(act) < thr)) break;
+      }
     }
     DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
-    n_rays++;
+    if (__ballot(alive) == 0) break;
 
-    // ---- this iteration's keystream block, generated by every lane at once
-    RngBlk rb;
-    rng_load(rng, rb);
+    if (alive && tdone) {
+      DIAG(active++;)
+      n_rays++;
+      HitRec hr;
+      hr.t = ts.best;
+      hr.u = ts.bu;
+      hr.v = ts.bv;
+      hr.prim = ts.bestp;
 
-    // ---- shade
-    bool end_sample = true;
-    if (hr.prim >= 0) {
-      KArgsPtr A = kargs();
-      const KScene S = load_scene(A);
-      Surf h;
-      surface(S, hr, o, d, h);
-      const rpl::Material& m = S.mats[h.material];
-      V3 nd;
-      const bool scattered = scatter_eval(m, d, h, rng, rb, nd);   // order: scatter, absorb, emit
-      const V3 ab = absorb_eval(S, m, h);
-      const V3 em = emit_eval(S, m.emit_kind, m.emit_tex, m.emit_color, d, h);
-      if (first) hits++;
-      L = add(L, mulc(T, em));  // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142)
-      if (scattered) {
-        T = mulc(T, ab);
-        o = h.p;
-        d = nd;
-        depth--;
-        end_sample = depth == 0;  // trace_path_continue(depth 0) is black (render.rs:128-131)
+      // ---- this ray's keystream block
+      RngBlk rb;
+      rng_load(rng, rb);
+
+      // ---- shade.  Hits and misses share one spherical-uv site and one texture-sampling site, so a wave
+      // with both pays for each f64 atan2/asin and texture walk once.
+      bool end_sample = true;
+      {
+        KArgsPtr A = kargs();
+        const KScene S = load_scene(A);
+        const bool hit = hr.prim >= 0;
+        Surf h;
+        const rpl::Material* m = nullptr;
+        bool sph_uv;
+        if (hit) {
+          sph_uv = surface(S, hr, o, d, h);
+          m = &S.mats[h.material];
+        } else {
+          // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
+          h.p = d;
+          h.n = d;
+          h.u = 0.0;
+          h.v = 0.0;
+          h.material = 0;
+          sph_uv = S.background.needs_uv != 0;
+        }
+        if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
+          const V3 q = hit ? h.n : d;
+          h.u = 0.5 - atan2(q.z, q.x) / TAU_;
+          h.v = asin(q.y) / PI_ + 0.5;
+        }
+        // scatter first (the only RNG consumer; order scatter, absorb, emit as material.rs), then the
+        // textures this lane reads: absorb map (hit), sky sphere (hit emission or background)
+        V3 nd = v3(0.0, 0.0, 0.0);
+        const bool scattered = hit && scatter_eval(*m, d, h, rng, rb, nd);
+        const uint32_t emit_kind = hit ? m->emit_kind : S.background.kind;
+        const uint32_t emit_tex = hit ? m->emit_tex : S.background.tex;
+        V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
+        bool pend_a = hit && m->absorb_kind == 3, pend_e = emit_kind == 4;
+        while (__ballot(pend_a || pend_e)) {
+          if (pend_a || pend_e) {
+            const V3 t = tex_sample(S, pend_a ? m->absorb_tex : emit_tex, h);
+            if (pend_a) { tex_ab = t; pend_a = false; }
+            else { tex_em = t; pend_e = false; }
+          }
+        }
+        const double* ecol = hit ? m->emit_color : S.background.color;
+        const V3 em = emit_eval(emit_kind, v3(ecol[0], ecol[1], ecol[2]), tex_em, d, h);
+        // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142), accumulated forward: each
+        // bounce's T (*) emit goes straight into the pixel sum (main.rs:80 adds the sample's total; the
+        // association differs in the last ulp only)
+        sum_x = sum_x + T_x * em.x;
+        sum_y = sum_y + T_y * em.y;
+        sum_z = sum_z + T_z * em.z;
+        if (hit && first) hits++;
+        if (scattered) {
+          const V3 ab = absorb_eval(*m, tex_ab);
+          T_x = T_x * ab.x;
+          T_y = T_y * ab.y;
+          T_z = T_z * ab.z;
+          o = h.p;
+          d = nd;
+          depth--;
+          end_sample = depth == 0;  // trace_path_continue(depth 0) is black (render.rs:128-131)
+        }
       }
-    } else {
-      // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
-      KArgsPtr A = kargs();
-      const KScene S = load_scene(A);
-      Surf h;
-      h.p = d;
-      h.n = d;
-      h.u = 0.0;
-      h.v = 0.0;
-      if (S.background.needs_uv) {
-        h.u = 0.5 - atan2(d.z, d.x) / TAU_;
-        h.v = asin(d.y) / PI_ + 0.5;
-      }
-      const V3 em = emit_eval(S, S.background.kind, S.background.tex, S.background.color, d, h);
-      L = add(L, mulc(T, em));
-    }
-    first = false;
+      first = false;
 
-    // ---- end of a camera sample: accumulate (main.rs:80), maybe finish the pixel, start the next one
-    if (end_sample) {
-      KArgsPtr A = kargs();
-      sum = add(sum, L);
-      s++;
-      n_samples++;
-      if (s == A->P.spp) {  // main.rs:86-87
-        const double spp = (double)A->P.spp;
-        double* out = A->out;
-        out[3 * (uint64_t)slot + 0] = sum.x / spp;
-        out[3 * (uint64_t)slot + 1] = sum.y / spp;
-        out[3 * (uint64_t)slot + 2] = sum.z / spp;
-        if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
-        n_pixels++;
-        alive = fetch_pixel(slot, pi, pj);
+      // ---- end of a camera sample: accumulate (main.rs:80), maybe finish the pixel, start the next
+      if (end_sample) {
+        KArgsPtr A = kargs();
+        s++;
+        n_samples++;
+        if (s == A->P.spp) {  // main.rs:86-87
+          const double spp = (double)A->P.spp;
+          double* out = A->out;
+          out[3 * (uint64_t)slot + 0] = sum_x / spp;
+          out[3 * (uint64_t)slot + 1] = sum_y / spp;
+          out[3 * (uint64_t)slot + 2] = sum_z / spp;
+          if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+          n_pixels++;
+          alive = fetch_pixel(slot, pi, pj);
+          if (alive) {
+            A = kargs();
+            rng_begin_pixel(rng, rb, A->P.seed + (uint64_t)pj * A->P.W + pi);
+            s = 0;
+            hits = 0;
+            sum_x = sum_y = sum_z = 0.0;
+          }
+        }
         if (alive) {
+          start_sample(rng, rb, s, pi, pj, o, d);
           A = kargs();
-          seed_key(A->P.seed + (uint64_t)pj * A->P.W + pi, rng.key);
-          rng.pos = 0;
-          s = 0;
-          hits = 0;
-          sum = v3(0.0, 0.0, 0.0);
+          depth = A->P.max_bounce;
+          T_x = T_y = T_z = 1.0;
+          first = true;
         }
       }
       if (alive) {
-        start_sample(rng, rb, s, pi, pj, o, d);
-        A = kargs();
-        depth = A->P.max_bounce;
-        T = v3(1.0, 1.0, 1.0);
-        L = v3(0.0, 0.0, 0.0);
-        first = true;
+        trav_init(load_scene(kargs()), INF, ts);
+        tdone = false;
       }
     }
     DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
@@ -818,7 +1022,10 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
   double* oh = out_hit + 9 * i;
   if (hr.prim >= 0) {
     Surf h;
-    surface(S, hr, o, d, h, true);  // Hittable::hit returns the full Hit record
+    if (surface(S, hr, o, d, h, true)) {  // Hittable::hit returns the full Hit record
+      h.u = 0.5 - atan2(h.n.z, h.n.x) / TAU_;
+      h.v = asin(h.n.y) / PI_ + 0.5;
+    }
     oh[0] = hr.t; oh[1] = h.p.x; oh[2] = h.p.y; oh[3] = h.p.z;
     oh[4] = h.n.x; oh[5] = h.n.y; oh[6] = h.n.z; oh[7] = h.u; oh[8] = h.v;
     out_mat[i] = h.material;
@@ -843,6 +1050,8 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
+
+uint64_t rng_slab_bytes_per_lane() { return (uint64_t)SLAB_N * sizeof(uint4); }
 
 int render_blocks_per_cu(uint32_t stack_depth, int* blocks) {
   const size_t lds = (size_t)stack_depth * BLOCK * sizeof(uint32_t);

@@ -68,6 +68,15 @@ def test_odd_sizes_and_tiles(gpu):
         _check(gpu, sc, p)
 
 
+@pytest.mark.parametrize("name", ["three_balls", "bunny_full"])
+@pytest.mark.parametrize("spp", [1, 2, 3])
+def test_small_spp(gpu, name, spp):
+    """Fewer than 4 samples: a pixel's whole stream can end inside keystream block 0, so the next pixel
+    on the same lane must not reuse any cached block (three_balls samples a lens)."""
+    scene, params = _scene(name, 72, 40, spp)
+    _check(gpu, scene, params)
+
+
 def test_max_bounce_variants(gpu):
     from rtpotato.scene import RenderParams
     from rtpotato import scenes

@@ -1,10 +1,15 @@
-"""Timing-only ablation A/B (NOT parity builds): C3 frame time per library variant, interleaved rounds."""
+"""Timing-only A/B: C3 64-spp frame time per variant, interleaved rounds.  A variant is a library file
+under raytracing-potato_amd/lib, optionally with a traversal threshold: `librp.so@16` (RP_TRAV_THRESHOLD)."""
 import os, sys, json, subprocess
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 libs = sys.argv[1:]
 res = {}
 for rnd in range(2):
-    for lib in libs:
+    for spec in libs:
+        lib, _, thr = spec.partition("@")
+        env = dict(os.environ)
+        if thr:
+            env["RP_TRAV_THRESHOLD"] = thr
         code = f"""
 import os,sys
 sys.path[:0]=['{REPO}','{REPO}/raytracing-potato_amd']
@@ -17,6 +22,6 @@ ds=DeviceScene(sc); ds.render(replace(p,spp=4))
 ts=[ds.render(p)[2]['seconds'] for _ in range(2)]
 print(min(ts))
 """
-        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
-        res.setdefault(lib, []).append(float(out.stdout.strip().split()[-1]) if out.returncode == 0 else out.stderr[-300:])
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+        res.setdefault(spec, []).append(float(out.stdout.strip().split()[-1]) if out.returncode == 0 else out.stderr[-300:])
 print(json.dumps(res))

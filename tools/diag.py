@@ -35,7 +35,7 @@ def main():
     iters, active, trips, visits, tests = d[5], d[6], d[7], d[8], d[9]
     out = {
         "config": a.config, "spp": a.spp, "rays": st["rays"], "seconds": st["seconds"],
-        "phase_share": {k: round(v / tot, 4) for k, v in zip(["fetch", "new_sample", "traverse", "shade", "tail"], ph)},
+        "phase_share": {k: round(v / tot, 4) for k, v in zip(["fetch", "rng_refill", "traverse", "shade", "tail"], ph)},
         "wave_iterations": iters, "lanes_active_at_traverse": round(active / max(1, iters) / 64, 4),
         "visits_per_ray": round(visits / st["rays"], 3), "prim_tests_per_ray": round(tests / st["rays"], 3),
         "traversal_lane_util": round(visits / max(1, trips * 64), 4),
