@@ -183,8 +183,9 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->ks.texels = s->d_texels;
   s->ks.background = ps.background;
   s->ks.root = ps.root;
-  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root
-  s->ks.stack_depth = 3 * ps.max_depth + 4;
+  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
+  // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
+  s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
   s->n_nodes = ps.nodes.size();
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;

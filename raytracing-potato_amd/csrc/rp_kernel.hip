@@ -39,6 +39,7 @@ RPK_INLINE uint64_t stamp() {
 #endif
 
 static constexpr int BLOCK = RENDER_BLOCK;
+static constexpr uint32_t STACK_SLACK = 3;  // spare LDS stack entries for the branchless push (writes reach sp+2 <= cap+2)
 static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
 static constexpr double SMOL = 1e-7;         // utility.rs:31
 static constexpr double PI_ = 3.14159265358979323846;
@@ -375,7 +376,7 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
   uint32_t cur = ts.cur, sp = ts.sp;
   double best = ts.best;
   float best32 = f32_up(best);
-  const uint32_t cap = S.stack_depth;
+  const uint32_t cap = S.stack_depth - STACK_SLACK;
   // ---- inner nodes
   while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
@@ -415,16 +416,22 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
 }
     RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
 #undef RPK_CSWAP
+    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1
+    // farther ones far-to-near without branches: slots sp..sp+2 are written unconditionally (the stack
+    // has STACK_SLACK spare entries; slots past the new top are garbage) and sp advances by k.
     const float INFF = __builtin_huge_valf();
-    // push the farther hits far-to-near, continue with the nearest
-#pragma unroll
-    for (int c = 3; c >= 1; c--) {
-      if (tn[c] != INFF) {
-        if (sp < cap) stk[(sp++) * stride] = cc[c];
-        else overflow = true;
-      }
+    const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
+                           (uint32_t)(tn[3] != INFF);
+    const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
+    stk[sp * stride] = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]);
+    stk[(sp + 1u) * stride] = k == 3u ? cc[2] : cc[1];
+    stk[(sp + 2u) * stride] = cc[1];
+    sp += k;
+    if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
+      overflow = true;
+      sp = cap;
     }
-    if (tn[0] != INFF) cur = cc[0];
+    if (n_hit) cur = cc[0];
     else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
   }
   if (cur == rpl::ENTRY_EMPTY) {
@@ -542,32 +549,47 @@ RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, 
 
 // ------------------------------------------------------------------ shading ----------------------
 
-// texture.rs:21-118 (Checker recursion unrolled into a walk; validate() guarantees it terminates)
-RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
-  for (;;) {
+// x / 255.0 for a byte x, correctly rounded without a division: q0 = x * fl(1/255) is off by at most
+// one ulp and one FMA residual step corrects it (exhaustively checked for all 256 x, tests/test_host.py).
+RPK_INLINE double u8_unit(uint32_t x) {
+  const double xd = (double)x, R = 1.0 / 255.0;
+  const double q0 = xd * R;
+  return __builtin_fma(__builtin_fma(-q0, 255.0, xd), R, q0);
+}
+
+// texture.rs:51-60: walk Checker indirections down to the texture that produces the value
+// (validate() guarantees the walk terminates).
+RPK_INLINE uint32_t tex_resolve(const KScene& S, uint32_t tid, const Surf& h) {
+  while (S.texs[tid].kind == 4) {
     const rpl::Texture& t = S.texs[tid];
-    switch (t.kind) {
-      case 1:  // DebugUVs
-        return v3(h.u, h.v, 0.0);
-      case 2:  // Solid
-        return v3(t.color[0], t.color[1], t.color[2]);
-      case 3: {  // Image (texture.rs:40-49): clamp then saturating `as u32`
-        const double w = (double)t.width, hh = (double)t.height;
-        double x = h.u * w, y = h.v * hh;
-        if (x < 0.0) x = 0.0;
-        if (x > w - 1.0) x = w - 1.0;
-        if (y < 0.0) y = 0.0;
-        if (y > hh - 1.0) y = hh - 1.0;
-        const uint32_t i = sat_u32(x), j = sat_u32(y);
-        const uint32_t px = S.texels[t.texel_offset + (uint64_t)i + (uint64_t)j * t.width];
-        return v3((double)(px & 0xffu) / 255.0, (double)((px >> 8) & 0xffu) / 255.0,
-                  (double)((px >> 16) & 0xffu) / 255.0);
-      }
-      case 4: {  // Checker (texture.rs:51-60)
-        const double s = floor(h.p.x) + floor(h.p.y) + floor(h.p.z);
-        tid = fmod(s, 2.0) == 0.0 ? t.even : t.odd;
-        continue;
-      }
+    const double s = floor(h.p.x) + floor(h.p.y) + floor(h.p.z);
+    tid = fmod(s, 2.0) == 0.0 ? t.even : t.odd;
+  }
+  return tid;
+}
+
+// texture.rs:40-49 Image: clamp, then saturating `as u32` -> texel index
+RPK_INLINE uint64_t image_texel(const rpl::Texture& t, const Surf& h) {
+  const double w = (double)t.width, hh = (double)t.height;
+  double x = h.u * w, y = h.v * hh;
+  if (x < 0.0) x = 0.0;
+  if (x > w - 1.0) x = w - 1.0;
+  if (y < 0.0) y = 0.0;
+  if (y > hh - 1.0) y = hh - 1.0;
+  return t.texel_offset + (uint64_t)sat_u32(x) + (uint64_t)sat_u32(y) * t.width;
+}
+
+// texture.rs:21-118 value of a resolved (non-Checker) texture; `px` is the Image texel, fetched by the
+// caller ahead of use so its latency overlaps other shading work.
+RPK_INLINE V3 tex_value(const KScene& S, uint32_t tid, const Surf& h, uint32_t px) {
+  const rpl::Texture& t = S.texs[tid];
+  switch (t.kind) {
+    case 1:  // DebugUVs
+      return v3(h.u, h.v, 0.0);
+    case 2:  // Solid
+      return v3(t.color[0], t.color[1], t.color[2]);
+    case 3:  // Image
+      return v3(u8_unit(px & 0xffu), u8_unit((px >> 8) & 0xffu), u8_unit((px >> 16) & 0xffu));
       case 5: {  // Noise (texture.rs:62-68)
         double x = noise_real(sat_i64(floor(h.p.x)), sat_i64(floor(h.p.y)), sat_i64(floor(h.p.z)), t.seed);
         x = 0.5 * x + 0.5;
@@ -600,9 +622,15 @@ RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
         return v3(x, x, x);
       }
       default:  // Missing
-        return v3(0.0, 0.0, 0.0);
-    }
+      return v3(0.0, 0.0, 0.0);
   }
+}
+
+RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
+  tid = tex_resolve(S, tid, h);
+  const rpl::Texture& t = S.texs[tid];
+  const uint32_t px = t.kind == 3 ? S.texels[image_texel(t, h)] : 0u;
+  return tex_value(S, tid, h, px);
 }
 
 // material.rs:49-60 Emit::evaluate (SkySphere's texture value sampled by the caller)
@@ -898,26 +926,40 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
           h.material = 0;
           sph_uv = S.background.needs_uv != 0;
         }
+#ifdef RPK_ABLATE_UV  // timing ablation only (colours change, rays do not)
+        sph_uv = false;
+#endif
         if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
           const V3 q = hit ? h.n : d;
           h.u = 0.5 - atan2(q.z, q.x) / TAU_;
           h.v = asin(q.y) / PI_ + 0.5;
         }
-        // scatter first (the only RNG consumer; order scatter, absorb, emit as material.rs), then the
-        // textures this lane reads: absorb map (hit), sky sphere (hit emission or background)
-        V3 nd = v3(0.0, 0.0, 0.0);
-        const bool scattered = hit && scatter_eval(*m, d, h, rng, rb, nd);
+        // Textures: each lane reads at most one here -- the absorb map of a hit or the sky sphere of a miss
+        // (or of an emissive hit); its Checker walk and Image texel load are issued BEFORE the scatter so
+        // the load latency overlaps it.  A hit reading both takes the second in a rare extra pass.
         const uint32_t emit_kind = hit ? m->emit_kind : S.background.kind;
         const uint32_t emit_tex = hit ? m->emit_tex : S.background.tex;
-        V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
-        bool pend_a = hit && m->absorb_kind == 3, pend_e = emit_kind == 4;
-        while (__ballot(pend_a || pend_e)) {
-          if (pend_a || pend_e) {
-            const V3 t = tex_sample(S, pend_a ? m->absorb_tex : emit_tex, h);
-            if (pend_a) { tex_ab = t; pend_a = false; }
-            else { tex_em = t; pend_e = false; }
-          }
+        bool ta = hit && m->absorb_kind == 3, te = emit_kind == 4;
+#ifdef RPK_ABLATE_TEX  // timing ablation only (colours change, rays do not)
+        ta = te = false;
+#endif
+        const bool t1 = ta || te;
+        uint32_t tid1 = 0, px1 = 0;
+        if (t1) {
+          tid1 = tex_resolve(S, ta ? m->absorb_tex : emit_tex, h);
+          const rpl::Texture& t = S.texs[tid1];
+          if (t.kind == 3) px1 = S.texels[image_texel(t, h)];
         }
+        // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
+        V3 nd = v3(0.0, 0.0, 0.0);
+        const bool scattered = hit && scatter_eval(*m, d, h, rng, rb, nd);
+        V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
+        if (t1) {
+          const V3 tv = tex_value(S, tid1, h, px1);
+          if (ta) tex_ab = tv;
+          else tex_em = tv;
+        }
+        if (ta && te) tex_em = tex_sample(S, emit_tex, h);
         const double* ecol = hit ? m->emit_color : S.background.color;
         const V3 em = emit_eval(emit_kind, v3(ecol[0], ecol[1], ecol[2]), tex_em, d, h);
         // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142), accumulated forward: each

@@ -118,3 +118,18 @@ def test_sky_panorama_deterministic():
     golden = os.path.join(os.path.dirname(__file__), "golden", "sky_panorama.sha256")
     if os.path.exists(golden):
         assert open(golden).read().strip() == digest
+
+
+def test_u8_unit_division_free_is_exact():
+    """rp_kernel.hip u8_unit(): x/255.0 for every byte x as fl(x*fl(1/255)) plus one FMA residual
+    correction -- bit-identical to the correctly rounded division texture.rs:47 performs."""
+    import ctypes
+    import struct
+    libm = ctypes.CDLL("libm.so.6")
+    libm.fma.restype = ctypes.c_double
+    libm.fma.argtypes = [ctypes.c_double] * 3
+    R = 1.0 / 255.0
+    for x in range(256):
+        q0 = float(x) * R
+        q = libm.fma(libm.fma(-q0, 255.0, float(x)), R, q0)
+        assert struct.pack("<d", q) == struct.pack("<d", float(x) / 255.0), x
