@@ -359,6 +359,7 @@ struct TravState {
   double best, bu, bv;
   int32_t bestp;
   uint32_t cur, sp;
+  uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
 };
 
 RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
@@ -368,12 +369,14 @@ RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
   t.bestp = -1;
   t.cur = S.root;
   t.sp = 0;
+  t.leaf = 0;
 }
 
-// One step: descend to a leaf, test it, pop the next entry.  t.cur == ENTRY_EMPTY when finished.
+// One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY (the
+// parked leaf is always consumed inside a step).
 RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
-  uint32_t cur = ts.cur, sp = ts.sp;
+  uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
   double best = ts.best;
   float best32 = f32_up(best);
   const uint32_t cap = S.stack_depth - STACK_SLACK;
@@ -433,15 +436,25 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     }
     if (n_hit) cur = cc[0];
     else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+#ifndef RPK_NO_SPECULATIVE
+    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
+    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.
+    if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+      leaf = cur;
+      cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+    }
+    if (__ballot(leaf == 0u) == 0) break;
+#endif
   }
-  if (cur == rpl::ENTRY_EMPTY) {
-    ts.cur = cur;
-    ts.sp = sp;
-    return;
+  if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+    leaf = cur;
+    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
   }
-  // ---- leaf: the reference's exact f64 primitive tests
-  const uint32_t first = cur & rpl::LEAF_FIRST_MASK;
-  const uint32_t cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
+  // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
+  // entry while it is a leaf as well
+  while (leaf != 0u) {
+  const uint32_t first = leaf & rpl::LEAF_FIRST_MASK;
+  const uint32_t cnt = ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
   for (uint32_t k = first; k < first + cnt; k++) {
     DIAG(if (td) td->tests++;)
     const rpl::Prim* p = S.prims + k;
@@ -493,10 +506,17 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     }
     best32 = f32_up(best);
   }
-  cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+  if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+    leaf = cur;
+    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+  } else {
+    leaf = 0u;
+  }
+  }
   ts.cur = cur;
   ts.sp = sp;
   ts.best = best;
+  ts.leaf = leaf;
 }
 
 RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
