@@ -156,6 +156,9 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
 
   rpb::PackedScene ps;
   rpb::BuildOptions opt;
+  // tuning knobs for experiments (the defaults are the measured best): leaf size and SAH cost ratio
+  if (const char* e = std::getenv("RP_BVH_MAX_LEAF")) opt.max_leaf = (uint32_t)std::strtoul(e, nullptr, 10);
+  if (const char* e = std::getenv("RP_BVH_COST_TRAVERSE")) opt.cost_traverse = std::strtod(e, nullptr);
   rc = rpb::build(desc, opt, ps, err);
   if (rc != RP_OK) return fail(rc, err);
 

@@ -29,7 +29,15 @@ enum { RENDER_BLOCK = 256 };
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
 // lane primitive tests.
-enum { DIAG_N = 16 };
+enum { DIAG_N = 64 };
+// Region counters (RPK_DIAG builds), from DIAG_N index 16: per code region r, [16 + 2r] = wave
+// executions and [17 + 2r] = active lanes summed over them (lane utilisation = lanes / (64 x execs)).
+enum {
+  DREG_NODE, DREG_PRIM, DREG_STEP, DREG_SHADE, DREG_SURF, DREG_SPHUV, DREG_TEX, DREG_LAMBERT, DREG_METAL,
+  DREG_DIELEC, DREG_LOOP_LAMBERT, DREG_LOOP_METAL, DREG_END_SAMPLE, DREG_END_PIXEL, DREG_START_SAMPLE,
+  DREG_REFILL, DREG_RNG_FALLBACK, DREG_JIT_FALLBACK, DREG_BEGIN_PIXEL, DREG_RING_LOAD, DREG_ROUND, DREG_MISS,
+  DREG_N
+};
 
 struct KParams {
   double orient[9];

@@ -34,11 +34,25 @@ RPK_INLINE uint64_t stamp() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): s_memtime returns through the LGKM counter
   return t;
 }
+__shared__ unsigned long long g_dreg[2 * DREG_N];
+// count one execution of region r by this wave and its active lanes (leader lane only; EXEC is read
+// directly, no ballot)
+#define DREG(r)                                                                        \
+  {                                                                                    \
+    const uint64_t ex_ = __builtin_amdgcn_read_exec();                                 \
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex_)) {                       \
+      atomicAdd(&g_dreg[2 * (r)], 1ull);                                               \
+      atomicAdd(&g_dreg[2 * (r) + 1], (unsigned long long)__popcll(ex_));             \
+    }                                                                                  \
+  }
 #else
 #define DIAG(...)
+#define DREG(r)
 #endif
 
 static constexpr int BLOCK = RENDER_BLOCK;
+typedef float f2 __attribute__((ext_vector_type(2)));
+RPK_INLINE f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 static constexpr uint32_t STACK_SLACK = 3;  // spare LDS stack entries for the branchless push (writes reach sp+2 <= cap+2)
 static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
 static constexpr double SMOL = 1e-7;         // utility.rs:31
@@ -108,10 +122,21 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 // Slab layout per lane (uint4 units): [0,2) key words, [2, 2+4*RING) ring (block b in slot b % RING),
 // [2+4*RING, +8) jitter blocks (block b in slot b & 1).  Per-lane cursors (LDS): end = one past the
 // newest ring block; jtag[2] = block held by each jitter slot.
-static constexpr uint32_t RING = 8;
-static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_N = SLAB_JIT + 8;
+#ifndef RPK_RING
+#define RPK_RING 8
+#endif
+#ifndef RPK_RNG_BATCH
+#define RPK_RNG_BATCH 48
+#endif
+static constexpr uint32_t RING = RPK_RING;
+static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
+#ifdef RPK_W4
+static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
+#else
+static constexpr uint32_t SLAB_N = SLAB_COLD;
+#endif
 static constexpr uint32_t RNG_CRIT = 2;    // a lane holding <= this many blocks forces a refill pass
-static constexpr uint32_t RNG_BATCH = 48;  // ... as do this many lanes with room
+static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // ... as do this many lanes with room
 
 struct Rng {
   uint4* slab;     // global: this lane's slab
@@ -151,8 +176,10 @@ RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT 
 RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
   b.blk = r.pos >> 4;
   if (b.blk < *r.end) {
+    DREG(DREG_RING_LOAD)
     load_block(ring_slot(r, b.blk), b.w);
   } else {
+    DREG(DREG_RNG_FALLBACK)
     uint32_t k[8];
     load_key(r, k);
     chacha12(k, b.blk, b.w);
@@ -164,6 +191,7 @@ RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
 // A new pixel: key from the RNG contract seed, block 0 (shared by the main stream and the jitter of
 // samples 0-3, render.rs:74-82) generated once into both caches and into registers.
 RPK_INLINE void rng_begin_pixel(Rng& r, RngBlk& b, uint64_t seed) {
+  DREG(DREG_BEGIN_PIXEL)
   uint32_t k[8];
   seed_key(seed, k);
   store_key(r, k);
@@ -188,6 +216,7 @@ RPK_INLINE void rng_refill(Rng& r, bool alive, uint32_t s, uint32_t spp) {
   const bool room = alive && (have < RING || j1 || j2);
   if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
   if (room) {
+    DREG(DREG_REFILL)
     const bool main = crit || !(j1 || j2);
     const uint32_t b = main ? end : (j1 ? b1 : b2);
     uint32_t k[8], w[16];
@@ -203,6 +232,7 @@ RPK_INLINE void rng_refill(Rng& r, bool alive, uint32_t s, uint32_t spp) {
 RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
   const uint32_t b = s >> 2;
   if (r.jtag[(b & 1u) * BLOCK] == b) return jit_slot(r, b)[s & 3u];
+  DREG(DREG_JIT_FALLBACK)
   uint32_t k[8], w[16];
   load_key(r, k);
   chacha12(k, b, w);
@@ -372,6 +402,58 @@ RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
   t.leaf = 0;
 }
 
+// One exact f64 primitive test (the reference's Hittable::hit for a leaf, hittable.rs:39-101): on
+// acceptance `best` shrinks to t and the hit record is taken.
+RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, double& best, TravState& ts) {
+  const rpl::Prim* p = S.prims + k;
+  const double2 g01 = *reinterpret_cast<const double2*>(p->g);
+  const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
+  const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
+  const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
+  const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
+  const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+  if (kind == rpl::PRIM_TRIANGLE) {
+    // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
+    const V3 a = v3(g01.x, g01.y, g23.x);
+    const V3 ba = v3(g23.y, g45.x, g45.y);
+    const V3 ca = v3(g67.x, g67.y, g8k.x);
+    const V3 pa = sub(a, o);
+    const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                     - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
+    if (fabs(det) < SMOL) return;
+    const double inv_det = 1.0 / det;
+    const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                    + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                    + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+    const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                    + pa.y * (ca.z * d.x - ca.x * d.z)
+                    + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+    const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                    + pa.y * (ba.x * d.z - ba.z * d.x)
+                    + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
+    const double w = 1.0 - u - v;
+    if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) return;
+    best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
+  } else {
+    // hittable.rs:39-57
+    const V3 c = v3(g01.x, g01.y, g23.x);
+    const double radius = g23.y;
+    const V3 tc = sub(o, c);
+    const double a = norm2(d);
+    const double half_b = dot(d, tc);
+    const double cq = norm2(tc) - radius * radius;
+    const double delta = half_b * half_b - a * cq;
+    if (delta <= 0.0) return;
+    const double sq = sqrt(delta);
+    double t = (-half_b - sq) / a;
+    if (t < tmin || t > best) {
+      t = (-half_b + sq) / a;
+      if (t < tmin || t > best) return;
+    }
+    best = t; ts.bestp = (int32_t)k;
+  }
+}
+
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY (the
 // parked leaf is always consumed inside a step).
 RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const Ray32& r, V3 o, V3 d,
@@ -383,6 +465,7 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
   // ---- inner nodes
   while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
+    DREG(DREG_NODE)
     const rpl::Node4* n = S.nodes + cur;
     const float4 lx = *reinterpret_cast<const float4*>(n->lo_x);
     const float4 hx = *reinterpret_cast<const float4*>(n->hi_x);
@@ -393,18 +476,33 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     const uint4 ch = *reinterpret_cast<const uint4*>(n->child);
     float tn[4];
     uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
-    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    // slab planes of children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the
+    // same per-element rounding as fmaf
+    const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+    const f2 nox = {-r.oix, -r.oix}, noy = {-r.oiy, -r.oiy}, noz = {-r.oiz, -r.oiz};
+    const f2 AX[2] = {pk_fma(f2{lx.x, lx.y}, ix, nox), pk_fma(f2{lx.z, lx.w}, ix, nox)};
+    const f2 BX[2] = {pk_fma(f2{hx.x, hx.y}, ix, nox), pk_fma(f2{hx.z, hx.w}, ix, nox)};
+    const f2 AY[2] = {pk_fma(f2{ly.x, ly.y}, iy, noy), pk_fma(f2{ly.z, ly.w}, iy, noy)};
+    const f2 BY[2] = {pk_fma(f2{hy.x, hy.y}, iy, noy), pk_fma(f2{hy.z, hy.w}, iy, noy)};
+    const f2 AZ[2] = {pk_fma(f2{lz.x, lz.y}, iz, noz), pk_fma(f2{lz.z, lz.w}, iz, noz)};
+    const f2 BZ[2] = {pk_fma(f2{hz.x, hz.y}, iz, noz), pk_fma(f2{hz.z, hz.w}, iz, noz)};
+    f2 TN[2], TF[2];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const float ax = __builtin_fmaf(LX[c], r.ix, -r.oix), bx = __builtin_fmaf(HX[c], r.ix, -r.oix);
-      const float ay = __builtin_fmaf(LY[c], r.iy, -r.oiy), by = __builtin_fmaf(HY[c], r.iy, -r.oiy);
-      const float az = __builtin_fmaf(LZ[c], r.iz, -r.oiz), bz = __builtin_fmaf(HZ[c], r.iz, -r.oiz);
-      const float tnear = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
-      const float tfar = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
-      const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 0x1p-19f, tfar) + r.slack && cc[c] != rpl::ENTRY_EMPTY;
-      tn[c] = hit ? tnear : __builtin_huge_valf();
+    for (int q = 0; q < 2; q++) {
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const float ax = AX[q][e], bx = BX[q][e], ay = AY[q][e], by = BY[q][e], az = AZ[q][e], bz = BZ[q][e];
+        TN[q][e] = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
+        TF[q][e] = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
+      }
+      // tnear <= tfar + 2^-19 |tfar| + slack (section 4.2 of DESIGN.md), as packed FMA + add
+      const f2 lim = pk_fma(f2{fabsf(TF[q][0]), fabsf(TF[q][1])}, f2{0x1p-19f, 0x1p-19f}, TF[q]) +
+                     f2{r.slack, r.slack};
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const int c = 2 * q + e;
+        tn[c] = (TN[q][e] <= lim[e] && cc[c] != rpl::ENTRY_EMPTY) ? TN[q][e] : __builtin_huge_valf();
+      }
     }
     // sort (tn, entry) ascending: misses (+inf) go last
 #define RPK_CSWAP(a, b)                                   \
@@ -451,67 +549,24 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
-  // entry while it is a leaf as well
+  // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
+  // lanes with different leaf sizes advance together instead of the wave running every leaf's count.
+  uint32_t k = leaf & rpl::LEAF_FIRST_MASK;
+  uint32_t kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
   while (leaf != 0u) {
-  const uint32_t first = leaf & rpl::LEAF_FIRST_MASK;
-  const uint32_t cnt = ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
-  for (uint32_t k = first; k < first + cnt; k++) {
     DIAG(if (td) td->tests++;)
-    const rpl::Prim* p = S.prims + k;
-    const double2 g01 = *reinterpret_cast<const double2*>(p->g);
-    const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
-    const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
-    const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
-    const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
-    const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
-    if (kind == rpl::PRIM_TRIANGLE) {
-      // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
-      const V3 a = v3(g01.x, g01.y, g23.x);
-      const V3 ba = v3(g23.y, g45.x, g45.y);
-      const V3 ca = v3(g67.x, g67.y, g8k.x);
-      const V3 pa = sub(a, o);
-      const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
-                       - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
-      if (fabs(det) < SMOL) continue;
-      const double inv_det = 1.0 / det;
-      const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
-                      + pa.y * (ba.z * ca.x - ba.x * ca.z)
-                      + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
-      const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
-                      + pa.y * (ca.z * d.x - ca.x * d.z)
-                      + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
-      const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
-                      + pa.y * (ba.x * d.z - ba.z * d.x)
-                      + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
-      const double w = 1.0 - u - v;
-      if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
-      best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
-    } else {
-      // hittable.rs:39-57
-      const V3 c = v3(g01.x, g01.y, g23.x);
-      const double radius = g23.y;
-      const V3 tc = sub(o, c);
-      const double a = norm2(d);
-      const double half_b = dot(d, tc);
-      const double cq = norm2(tc) - radius * radius;
-      const double delta = half_b * half_b - a * cq;
-      if (delta <= 0.0) continue;
-      const double sq = sqrt(delta);
-      double t = (-half_b - sq) / a;
-      if (t < tmin || t > best) {
-        t = (-half_b + sq) / a;
-        if (t < tmin || t > best) continue;
+    DREG(DREG_PRIM)
+    prim_test(S, k, o, d, tmin, best, ts);
+    if (++k == kend) {
+      if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+        leaf = cur;
+        cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+        k = leaf & rpl::LEAF_FIRST_MASK;
+        kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+      } else {
+        leaf = 0u;
       }
-      best = t; ts.bestp = (int32_t)k;
     }
-    best32 = f32_up(best);
-  }
-  if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
-    leaf = cur;
-    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
-  } else {
-    leaf = 0u;
-  }
   }
   ts.cur = cur;
   ts.sp = sp;
@@ -681,9 +736,11 @@ RPK_INLINE V3 absorb_eval(const rpl::Material& m, V3 tex) {
 RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, RngBlk& rb, V3& nd) {
   switch (m.scatter_kind) {
     case 1: {  // Lambert (material.rs:115-130)
+      DREG(DREG_LAMBERT)
       if (dot(h.n, d) > 0.0) return false;
       double x, y, s;
       do {  // UnitSphere (randomness.rs:58-73)
+        DREG(DREG_LOOP_LAMBERT)
         x = 2.0 * gen_f64(rng, rb) - 1.0;
         y = 2.0 * gen_f64(rng, rb) - 1.0;
         s = x * x + y * y;
@@ -693,9 +750,11 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
       return true;
     }
     case 2: {  // Metal (material.rs:132-152)
+      DREG(DREG_METAL)
       if (dot(h.n, d) > 0.0) return false;
       double x, y, z;
       do {  // UnitBall (randomness.rs:39-53)
+        DREG(DREG_LOOP_METAL)
         x = 2.0 * gen_f64(rng, rb) - 1.0;
         y = 2.0 * gen_f64(rng, rb) - 1.0;
         z = 2.0 * gen_f64(rng, rb) - 1.0;
@@ -706,6 +765,7 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
       return true;
     }
     case 3: {  // Dielectric (material.rs:154-179)
+      DREG(DREG_DIELEC)
       double eta;
       V3 n;
       if (dot(h.n, d) > 0.0) { eta = m.scatter_param; n = v3(-h.n.x, -h.n.y, -h.n.z); }
@@ -800,6 +860,7 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
 // stream (render.rs:74-82) = keystream words 4s..4s+3 = block s/4 at offset 4(s%4); Camera::shoot
 // (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
 RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
+  DREG(DREG_START_SAMPLE)
   KArgsPtr A = kargs();
   const uint4 jw = rng_jitter(rng, s);
   const uint32_t w0 = jw.x, w1 = jw.y, w2 = jw.z, w3 = jw.w;
@@ -822,12 +883,18 @@ RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint
   o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
 }
 
-__global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
+#ifdef RPK_W4
+#define RPK_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#else
+#define RPK_RENDER_ATTR
+#endif
+__global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
   DIAG(__shared__ unsigned long long wmax[BLOCK / 64][8];
        if (threadIdx.x < BLOCK / 64 * 8) wmax[threadIdx.x / 8][threadIdx.x % 8] = 0;)
   if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
+  DIAG(if (threadIdx.x < 2 * DREG_N) g_dreg[threadIdx.x] = 0;)
   __syncthreads();
   uint32_t* stk = lds_stack + threadIdx.x;
 
@@ -838,8 +905,10 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   // ---- lane state: one pixel's path at a time.  Hot state (ray, throughput, radiance, traversal)
   // in registers; cold per-pixel state (pixel sum, slot/pixel/sample counters, keystream cursors) in
   // LDS, structure-of-arrays so every access is bank-conflict-free; keystream blocks in the slab.
+#ifndef RPK_W4
   __shared__ double c_sum[3 * BLOCK];
   __shared__ double c_T[3 * BLOCK];
+#endif
   __shared__ uint32_t c_u[8 * BLOCK];
   const uint32_t tid = threadIdx.x;
   uint32_t& slot = c_u[tid];
@@ -847,12 +916,23 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   uint32_t& pj = c_u[2 * BLOCK + tid];
   uint32_t& s = c_u[3 * BLOCK + tid];
   uint32_t& hits = c_u[4 * BLOCK + tid];
+#ifdef RPK_W4
+  double* cold = reinterpret_cast<double*>(reinterpret_cast<uint4*>(kargs()->S.rng_slab) +
+                                           ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N + SLAB_COLD);
+  double& sum_x = cold[0];
+  double& sum_y = cold[1];
+  double& sum_z = cold[2];
+  double& T_x = cold[3];
+  double& T_y = cold[4];
+  double& T_z = cold[5];
+#else
   double& sum_x = c_sum[tid];
   double& sum_y = c_sum[BLOCK + tid];
   double& sum_z = c_sum[2 * BLOCK + tid];
   double& T_x = c_T[tid];  // path throughput (read and written once per shade)
   double& T_y = c_T[BLOCK + tid];
   double& T_z = c_T[2 * BLOCK + tid];
+#endif
   uint32_t depth = 0;
   bool first = true;
   Rng rng;
@@ -886,6 +966,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
   // node, LDS stack and closest hit so far are kept).
   for (;;) {
     DIAG(iters++;)
+    DREG(DREG_ROUND)
     rng_refill(rng, alive, s, kargs()->P.spp);
     DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
     {
@@ -896,6 +977,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       setup_ray32(o, d, RAY_EPSILON, r);
       for (;;) {
         if (alive && !tdone) {
+          DREG(DREG_STEP)
 #ifdef RPK_DIAG
           trav_step(S, stk, BLOCK, r, o, d, RAY_EPSILON, ts, overflow, &td);
 #else
@@ -913,6 +995,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
 
     if (alive && tdone) {
       DIAG(active++;)
+      DREG(DREG_SHADE)
       n_rays++;
       HitRec hr;
       hr.t = ts.best;
@@ -935,9 +1018,11 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
         const rpl::Material* m = nullptr;
         bool sph_uv;
         if (hit) {
+          DREG(DREG_SURF)
           sph_uv = surface(S, hr, o, d, h);
           m = &S.mats[h.material];
         } else {
+          DREG(DREG_MISS)
           // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
           h.p = d;
           h.n = d;
@@ -950,6 +1035,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
         sph_uv = false;
 #endif
         if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
+          DREG(DREG_SPHUV)
           const V3 q = hit ? h.n : d;
           h.u = 0.5 - atan2(q.z, q.x) / TAU_;
           h.v = asin(q.y) / PI_ + 0.5;
@@ -975,6 +1061,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
         const bool scattered = hit && scatter_eval(*m, d, h, rng, rb, nd);
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
         if (t1) {
+          DREG(DREG_TEX)
           const V3 tv = tex_value(S, tid1, h, px1);
           if (ta) tex_ab = tv;
           else tex_em = tv;
@@ -1004,10 +1091,12 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
 
       // ---- end of a camera sample: accumulate (main.rs:80), maybe finish the pixel, start the next
       if (end_sample) {
+        DREG(DREG_END_SAMPLE)
         KArgsPtr A = kargs();
         s++;
         n_samples++;
         if (s == A->P.spp) {  // main.rs:86-87
+          DREG(DREG_END_PIXEL)
           const double spp = (double)A->P.spp;
           double* out = A->out;
           out[3 * (uint64_t)slot + 0] = sum_x / spp;
@@ -1058,6 +1147,7 @@ __global__ void __launch_bounds__(BLOCK) render_kernel(const KArgs args) {
       for (int q = 0; q < 6; q++) atomicAdd(&dg[q], wmax[w][q]);
       atomicAdd(&dg[7], wmax[w][6]);
     }
+    if (threadIdx.x < 2 * DREG_N) atomicAdd(&dg[16 + threadIdx.x], g_dreg[threadIdx.x]);
   }
 #endif
   atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);

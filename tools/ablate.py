@@ -1,15 +1,21 @@
 """Timing-only A/B: C3 64-spp frame time per variant, interleaved rounds.  A variant is a library file
-under raytracing-potato_amd/lib, optionally with a traversal threshold: `librp.so@16` (RP_TRAV_THRESHOLD)."""
+under raytracing-potato_amd/lib, optionally with a traversal threshold and env knobs:
+`librp.so@16` (RP_TRAV_THRESHOLD), `librp.so@40:RP_BVH_MAX_LEAF=2,RP_BVH_COST_TRAVERSE=1.5`."""
 import os, sys, json, subprocess
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 libs = sys.argv[1:]
 res = {}
 for rnd in range(2):
     for spec in libs:
-        lib, _, thr = spec.partition("@")
+        # spec: LIB[@THRESHOLD][:ENV=VALUE,...]
+        head, _, extra = spec.partition(":")
+        lib, _, thr = head.partition("@")
         env = dict(os.environ)
         if thr:
             env["RP_TRAV_THRESHOLD"] = thr
+        for kv in filter(None, extra.split(",")):
+            k, _, v = kv.partition("=")
+            env[k] = v
         code = f"""
 import os,sys
 sys.path[:0]=['{REPO}','{REPO}/raytracing-potato_amd']

@@ -25,10 +25,10 @@ def main():
     params = replace(params, spp=a.spp)
     ds = DeviceScene(scene)
     ds.render(replace(params, spp=1))  # warm
-    buf = (ctypes.c_uint64 * 16)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 16, 1))
+    buf = (ctypes.c_uint64 * 64)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 64, 1))
     _, _, st = ds.render(params)
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 16, 1))
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 64, 1))
     d = list(buf)
     ph = d[:5]
     tot = sum(ph)
@@ -43,7 +43,14 @@ def main():
         "wave_cycles_per_iteration": round(tot / max(1, iters), 1),
         "traverse_cycles_per_trip": round(ph[2] / max(1, trips), 1),
     }
-    print(json.dumps(out))
+    regions = ["node", "prim", "step", "shade", "surface", "sph_uv", "texture", "lambert", "metal", "dielectric",
+               "loop_lambert", "loop_metal", "end_sample", "end_pixel", "start_sample", "refill", "rng_fallback",
+               "jit_fallback", "begin_pixel", "ring_load", "round", "miss"]
+    out["regions"] = {
+        name: {"wave_execs_per_kray": round(1000 * d[16 + 2 * i] / st["rays"], 2),
+               "lane_util": round(d[17 + 2 * i] / max(1, 64 * d[16 + 2 * i]), 3)}
+        for i, name in enumerate(regions)}
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
