@@ -159,7 +159,7 @@ def main():
                        "rays_per_frame": int(total_rays_step), "rays_per_sample": total_rays_step / total_samples_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "rpk::render_kernel", "kernel_ms": round(kernel_s * 1e3, 3),
+                         "kernel": "rpk::render_kernel<false>", "kernel_ms": round(kernel_s * 1e3, 3),
                          "bytes_per_ray": round(bpr, 1),
                          "note": "bunny scene (~1.3 MB) is cache-resident: HBM fraction is low by construction; "
                                  "fp64_vector gives the VALU roofline"},

@@ -5,6 +5,7 @@
 // once, and launches the persistent render kernel (rp_kernel.hip) per frame / shard.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -69,6 +70,9 @@ struct rp_scene {
   uint64_t* d_ws = nullptr;  // default counter block (8 x u64)
   uint64_t* d_diag = nullptr;  // diagnostic counters (rpk::DIAG_N)
   uint32_t* d_slab = nullptr;  // keystream cache, one slab per resident render lane
+  uint32_t* d_tile_cost = nullptr;   // cost probe output, rpk::TILE_SORT_MAX entries
+  uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
+  uint64_t* d_probe_ctr = nullptr;   // counter block of the probe launch
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
   uint32_t max_depth = 0;
   int num_cu = 0;
@@ -111,6 +115,15 @@ uint32_t trav_threshold() {
   return v;
 }
 
+// Cost-ordered tile scheduling (rp_kernel.h); RP_TILE_ORDER=0 restores plain shard order (for A/B timing).
+bool tile_order_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("RP_TILE_ORDER");
+    return !(e && std::strtol(e, nullptr, 10) == 0);
+  }();
+  return v;
+}
+
 }  // namespace
 
 extern "C" {
@@ -135,7 +148,8 @@ void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
-                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab})
+                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab,
+                  (void*)s->d_tile_cost, (void*)s->d_tile_order, (void*)s->d_probe_ctr})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -173,6 +187,9 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
       (rc = upload(ps.texels, &s->d_texels)))
     return bail(rc);
   if (hipMalloc(reinterpret_cast<void**>(&s->d_ws), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s->d_probe_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s->d_tile_cost), sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&s->d_tile_order), sizeof(uint32_t) * rpk::TILE_SORT_MAX) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&s->d_diag), sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess ||
       hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
     return bail(fail(RP_ENOMEM, "hipMalloc workspace"));
@@ -289,11 +306,29 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
   kp.n_shard_tiles = t.n_shard_tiles;
   kp.n_slots = t.n_slots;
   kp.trav_threshold = trav_threshold();
-  uint64_t want = (t.n_slots + 255) / 256;
-  uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
-  int grid = (int)(want < resident ? want : resident);
-  if (grid < 1) grid = 1;
-  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid, stream);
+  const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
+  auto grid_for = [&](uint64_t slots) {
+    const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
+    return (int)std::max<uint64_t>(1, std::min(want, resident));
+  };
+  if (tile_order_enabled() && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
+    // probe sample 0 of PROBE_PX pixels per tile, then sort the tiles by cost (same stream, no host sync)
+    rpk::KParams pk = kp;
+    pk.probe = 1;
+    pk.spp = 1;
+    // every pixel's sample 0 once spp is large enough to amortise it (a 1/spp extra), else a lattice
+    pk.probe_px = p->spp >= rpk::PROBE_FULL_MIN_SPP ? t.tw * t.th : (uint32_t)rpk::PROBE_LATTICE;
+    pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
+    pk.tile_cost = s->d_tile_cost;
+    RP_HIP(hipMemsetAsync(s->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+    RP_HIP(hipMemsetAsync(s->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
+    int e = rpk::launch_render(s->ks, pk, d_rgb, nullptr, s->d_probe_ctr, grid_for(pk.n_slots), stream);
+    if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
+    e = rpk::launch_tile_sort(s->d_tile_cost, t.n_shard_tiles, pk.probe_px, s->d_tile_order, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
+    kp.tile_order = s->d_tile_order;
+  }
+  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid_for(t.n_slots), stream);
   if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
   return RP_OK;
 }

@@ -29,7 +29,11 @@ enum { RENDER_BLOCK = 256 };
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
 // lane primitive tests.
-enum { DIAG_N = 64 };
+enum { DIAG_N = 256 };
+// Timeline histograms (RPK_DIAG builds), 64 bins of DIAG_BIN_TICKS (100 MHz real-time clock) from the
+// block's start: [64 + b] lanes retiring in bin b, [128 + b] rays of the pixels fetched in bin b,
+// [192 + b] pixels fetched in bin b.
+enum { DIAG_HIST = 64, DIAG_BIN_TICKS = 1000000 };
 // Region counters (RPK_DIAG builds), from DIAG_N index 16: per code region r, [16 + 2r] = wave
 // executions and [17 + 2r] = active lanes summed over them (lane utilisation = lanes / (64 x execs)).
 enum {
@@ -49,8 +53,22 @@ struct KParams {
   uint32_t tiles_x, n_shard_tiles;
   uint64_t n_slots;  // n_shard_tiles * tw * th
   uint32_t trav_threshold;  // resume shading once fewer than this many lanes of a wave still traverse
+  uint32_t probe;           // 1 = cost probe: sample 0 of probe_px pixels per tile
+  uint32_t probe_px;        // probe: every pixel of the tile (tw * th) or a 4 x 4 lattice (16)
   uint32_t pad;
+  const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
+  uint32_t* tile_cost;         // probe: [k] rays summed over the tile's probed samples, [TILE_SORT_MAX + k]
+                               // the longest probed sample (zeroed by the caller)
 };
+
+// Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last
+// pixels after the queue drained) was ~23% of the C3 frame; handing out the expensive tiles first
+// (longest-processing-time-first) leaves cheap, uniform tiles for the end.  The order comes from a probe
+// launch of the same kernel (sample 0 of every pixel, or of a 4 x 4 lattice per tile at low spp: the exact
+// paths of the frame) and a one-block sort.  Tiles holding the longest paths go first: a pixel's samples
+// run sequentially on one lane, so one expensive pixel fetched late becomes a latency-bound tail by itself.
+// Results do not depend on the order (per-pixel seeding).
+enum { PROBE_LATTICE = 16, PROBE_FULL_MIN_SPP = 32, TILE_SORT_MAX = 16384 };
 
 // Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_QUEUE = 4, CTR_N = 8 };
@@ -60,6 +78,10 @@ enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
 // the same stream.  Returns a hipError_t as int.
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
                   int grid, void* stream);
+
+// Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (longest sample, mean rays per probed
+// pixel), ties by tile index, into order[] (shard tile indices).  One block.
+int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32_t* order, void* stream);
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t stack_depth, int* blocks);

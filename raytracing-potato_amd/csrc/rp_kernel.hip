@@ -840,14 +840,29 @@ RPK_INLINE KArgsPtr kargs() {
 
 // Pull the next pixel of the shard from the device-wide queue (slot order: tiles, row-major inside a
 // tile; slots of edge tiles outside the frame are skipped).  Returns false when the queue is drained.
+template <bool PROBE>
 RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
   KArgsPtr A = kargs();
   unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
-  const uint32_t tw = A->P.tw, th = A->P.th, tile_px = tw * th;
-  for (;;) {
+  const uint32_t tw = A->P.tw, th = A->P.th;
+  if (PROBE && A->P.probe_px == PROBE_LATTICE) {  // cost probe: a 4x4 lattice per tile, clamped into the frame
     slot = atomicAdd(queue, 1u);
     if ((uint64_t)slot >= A->P.n_slots) return false;
-    const uint32_t k = slot / tile_px, local = slot - k * tile_px;
+    const uint32_t k = slot / PROBE_LATTICE, sub = slot % PROBE_LATTICE;
+    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
+    pi = min(tx * tw + min((sub & 3u) * tw / 4u + tw / 8u, tw - 1u), A->P.W - 1u);
+    pj = min(ty * th + min((sub >> 2) * th / 4u + th / 8u, th - 1u), A->P.H - 1u);
+    return true;
+  }
+  const uint32_t tile_px = tw * th;
+  for (;;) {
+    const uint32_t q = atomicAdd(queue, 1u);
+    if ((uint64_t)q >= A->P.n_slots) return false;
+    uint32_t k = q / tile_px;
+    const uint32_t local = q - k * tile_px;
+    if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
+    slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
     const uint32_t t = A->P.shard + k * A->P.nshards;
     const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
     pi = tx * tw + local % tw;
@@ -888,6 +903,9 @@ RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint
 #else
 #define RPK_RENDER_ATTR
 #endif
+// PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
+// and timings of the frame kernel never mix with it.
+template <bool PROBE>
 __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
@@ -895,12 +913,17 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
        if (threadIdx.x < BLOCK / 64 * 8) wmax[threadIdx.x / 8][threadIdx.x % 8] = 0;)
   if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
   DIAG(if (threadIdx.x < 2 * DREG_N) g_dreg[threadIdx.x] = 0;)
+  // frame timeline (100 MHz real-time clock, comparable across XCDs): first block start, first failed
+  // pixel fetch (queue drained), last wave exit -- minima stored bit-inverted so atomicMax serves both
+  DIAG(if (!PROBE && threadIdx.x == 0) atomicMax(&kargs()->diag[10], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
   __syncthreads();
   uint32_t* stk = lds_stack + threadIdx.x;
 
   uint32_t n_rays = 0, n_samples = 0, n_pixels = 0;
   bool overflow = false;
   DIAG(uint64_t ph[5] = {0, 0, 0, 0, 0}; uint64_t iters = 0, active = 0; TravDiag td; uint64_t t_prev = stamp();)
+  DIAG(const uint64_t t_blk = __builtin_amdgcn_s_memrealtime(); uint64_t t_pix = t_blk, t_retire = t_blk; uint32_t rays_pix = 0;
+       auto tbin = [&](uint64_t t) { return (uint32_t)min<uint64_t>((t - t_blk) / DIAG_BIN_TICKS, DIAG_HIST - 1); };)
 
   // ---- lane state: one pixel's path at a time.  Hot state (ray, throughput, radiance, traversal)
   // in registers; cold per-pixel state (pixel sum, slot/pixel/sample counters, keystream cursors) in
@@ -946,7 +969,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   hits = 0;
   sum_x = sum_y = sum_z = 0.0;
   TravState ts;
-  bool alive = fetch_pixel(slot, pi, pj);
+  bool alive = fetch_pixel<PROBE>(slot, pi, pj);
   bool tdone = true;  // traversal of the current ray finished (or no ray)
   if (alive) {
     KArgsPtr A = kargs();
@@ -1009,7 +1032,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 
       // ---- shade.  Hits and misses share one spherical-uv site and one texture-sampling site, so a wave
       // with both pays for each f64 atan2/asin and texture walk once.
-      bool end_sample = true;
+      bool end_sample = true, scattered_any = false;
       {
         KArgsPtr A = kargs();
         const KScene S = load_scene(A);
@@ -1076,6 +1099,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         sum_y = sum_y + T_y * em.y;
         sum_z = sum_z + T_z * em.z;
         if (hit && first) hits++;
+        scattered_any = scattered;
         if (scattered) {
           const V3 ab = absorb_eval(*m, tex_ab);
           T_x = T_x * ab.x;
@@ -1097,14 +1121,30 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         n_samples++;
         if (s == A->P.spp) {  // main.rs:86-87
           DREG(DREG_END_PIXEL)
-          const double spp = (double)A->P.spp;
-          double* out = A->out;
-          out[3 * (uint64_t)slot + 0] = sum_x / spp;
-          out[3 * (uint64_t)slot + 1] = sum_y / spp;
-          out[3 * (uint64_t)slot + 2] = sum_z / spp;
-          if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+          if (PROBE) {
+            // spp is 1 here: the sample traced max_bounce - depth scattered rays plus its last one
+            const uint32_t k = slot / A->P.probe_px, r = A->P.max_bounce - depth + (scattered_any ? 0u : 1u);
+            atomicAdd(&A->P.tile_cost[k], r);
+            atomicMax(&A->P.tile_cost[TILE_SORT_MAX + k], r);
+          } else {
+            const double spp = (double)A->P.spp;
+            double* out = A->out;
+            out[3 * (uint64_t)slot + 0] = sum_x / spp;
+            out[3 * (uint64_t)slot + 1] = sum_y / spp;
+            out[3 * (uint64_t)slot + 2] = sum_z / spp;
+            if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+          }
           n_pixels++;
-          alive = fetch_pixel(slot, pi, pj);
+          DIAG(if (!PROBE) {
+            const uint32_t b = tbin(t_pix);
+            atomicAdd(&A->diag[128 + b], (unsigned long long)(n_rays - rays_pix));
+            atomicAdd(&A->diag[192 + b], 1ull);
+            t_pix = __builtin_amdgcn_s_memrealtime();
+            rays_pix = n_rays;
+          })
+          alive = fetch_pixel<PROBE>(slot, pi, pj);
+          DIAG(if (!alive) t_retire = __builtin_amdgcn_s_memrealtime();)
+          DIAG(if (!PROBE && !alive) atomicMax(&A->diag[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
           if (alive) {
             A = kargs();
             rng_begin_pixel(rng, rb, A->P.seed + (uint64_t)pj * A->P.W + pi);
@@ -1148,6 +1188,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       atomicAdd(&dg[7], wmax[w][6]);
     }
     if (threadIdx.x < 2 * DREG_N) atomicAdd(&dg[16 + threadIdx.x], g_dreg[threadIdx.x]);
+    if (!PROBE && (threadIdx.x & 63) == 0) atomicMax(&dg[12], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (!PROBE) atomicAdd(&dg[64 + tbin(t_retire)], 1ull);
   }
 #endif
   atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);
@@ -1199,7 +1241,51 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.out_fg = out_fg;
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
-  hipLaunchKernelGGL(render_kernel, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  if (p.probe) hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(render_kernel<false>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// Bitonic sort of the probed tiles in LDS, one block: key = inverted (longest sample: 4 bits, mean rays per
+// probed pixel x 16: 14 bits) << 14 | k, so an ascending sort orders by descending cost, ties by shard
+// tile index.  Padding keys sort last.
+static constexpr int SORT_BLOCK = 1024;
+static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
+__global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n,
+                                                               uint32_t probe_px, uint32_t np2,
+                                                               uint32_t* __restrict__ order) {
+  __shared__ uint32_t key[TILE_SORT_MAX];
+  for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
+    uint32_t kk = 0xFFFFFFFFu;
+    if (i < n) {
+      const uint32_t longest = min(cost[TILE_SORT_MAX + i], 15u);
+      const uint32_t mean16 = (uint32_t)min<uint64_t>((uint64_t)cost[i] * 16u / probe_px, 16383u);
+      kk = ((((15u - longest) << 14) | (16383u - mean16)) << 14) | i;
+    }
+    key[i] = kk;
+  }
+  __syncthreads();
+  for (uint32_t size = 2; size <= np2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
+        const uint32_t j = i ^ stride;
+        if (j > i) {
+          const uint32_t a = key[i], b = key[j];
+          const bool up = (i & size) == 0;
+          if ((a > b) == up) { key[i] = b; key[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < n; i += SORT_BLOCK) order[i] = key[i] & 0x3FFFu;
+}
+
+int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32_t* order, void* stream) {
+  if (n == 0 || n > TILE_SORT_MAX) return (int)hipErrorInvalidValue;
+  uint32_t np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(SORT_BLOCK), 0, (hipStream_t)stream, cost, n, probe_px, np2, order);
   return (int)hipGetLastError();
 }
 
@@ -1207,7 +1293,7 @@ uint64_t rng_slab_bytes_per_lane() { return (uint64_t)SLAB_N * sizeof(uint4); }
 
 int render_blocks_per_cu(uint32_t stack_depth, int* blocks) {
   const size_t lds = (size_t)stack_depth * BLOCK * sizeof(uint32_t);
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel, BLOCK, lds);
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false>, BLOCK, lds);
 }
 
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,

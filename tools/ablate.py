@@ -23,7 +23,7 @@ os.environ['RP_LIB']='{REPO}/raytracing-potato_amd/lib/{lib}'
 from dataclasses import replace
 from rtpotato import scenes
 from rtpotato.render import DeviceScene
-sc,p=scenes.config_scene('C3'); p=replace(p, spp=64)
+sc,p=scenes.config_scene("C3"); p=replace(p, spp=int(os.environ.get("ABLATE_SPP","64")))
 ds=DeviceScene(sc); ds.render(replace(p,spp=4))
 ts=[ds.render(p)[2]['seconds'] for _ in range(2)]
 print(min(ts))

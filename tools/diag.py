@@ -25,10 +25,10 @@ def main():
     params = replace(params, spp=a.spp)
     ds = DeviceScene(scene)
     ds.render(replace(params, spp=1))  # warm
-    buf = (ctypes.c_uint64 * 64)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 64, 1))
+    buf = (ctypes.c_uint64 * 256)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 256, 1))
     _, _, st = ds.render(params)
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 64, 1))
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 256, 1))
     d = list(buf)
     ph = d[:5]
     tot = sum(ph)
@@ -43,6 +43,10 @@ def main():
         "wave_cycles_per_iteration": round(tot / max(1, iters), 1),
         "traverse_cycles_per_trip": round(ph[2] / max(1, trips), 1),
     }
+    t0, tq, t1 = (~d[10]) & (2**64 - 1), (~d[11]) & (2**64 - 1), d[12]
+    if t1 > t0:  # 100 MHz real-time clock
+        out["timeline_ms"] = {"queue_drained": round((tq - t0) / 1e5, 3), "last_exit": round((t1 - t0) / 1e5, 3),
+                              "tail_frac": round((t1 - tq) / (t1 - t0), 4)}
     regions = ["node", "prim", "step", "shade", "surface", "sph_uv", "texture", "lambert", "metal", "dielectric",
                "loop_lambert", "loop_metal", "end_sample", "end_pixel", "start_sample", "refill", "rng_fallback",
                "jit_fallback", "begin_pixel", "ring_load", "round", "miss"]
@@ -50,6 +54,10 @@ def main():
         name: {"wave_execs_per_kray": round(1000 * d[16 + 2 * i] / st["rays"], 2),
                "lane_util": round(d[17 + 2 * i] / max(1, 64 * d[16 + 2 * i]), 3)}
         for i, name in enumerate(regions)}
+    # timeline histograms (10 ms bins from each block's start): lanes retiring, pixels fetched and their rays
+    last = max([b for b in range(64) if d[64 + b] or d[192 + b]] or [0])
+    out["timeline_10ms"] = [{"t_ms": 10 * b, "retired_lanes": d[64 + b], "pixels": d[192 + b],
+                             "rays_per_pixel": round(d[128 + b] / max(1, d[192 + b]), 1)} for b in range(last + 1)]
     print(json.dumps(out, indent=1))
 
 
