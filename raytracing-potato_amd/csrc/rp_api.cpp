@@ -62,6 +62,7 @@ struct rp_scene {
   rpk::KScene ks{};
   rpl::Node4* d_nodes = nullptr;
   rpl::Prim* d_prims = nullptr;
+  rpl::PrimRef* d_prim_refs = nullptr;
   double* d_vnrm = nullptr;
   double* d_vuv = nullptr;
   rpl::Material* d_mats = nullptr;
@@ -147,7 +148,7 @@ int rp_device_count(int* count) {
 void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
-  for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
+  for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_prim_refs, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
                   (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab,
                   (void*)s->d_tile_cost, (void*)s->d_tile_order, (void*)s->d_probe_ctr})
     if (p) (void)hipFree(p);
@@ -182,6 +183,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->num_cu = prop.multiProcessorCount;
   auto bail = [&](int code) { rp_scene_destroy(s); return code; };
   if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
+      (rc = upload(ps.prim_refs, &s->d_prim_refs)) ||
       (rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
       (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
@@ -196,6 +198,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->ks.diag = s->d_diag;
   s->ks.nodes = s->d_nodes;
   s->ks.prims = s->d_prims;
+  s->ks.prim_refs = s->d_prim_refs;
   s->ks.vnrm = s->d_vnrm;
   s->ks.vuv = s->d_vuv;
   s->ks.mats = s->d_mats;
@@ -210,7 +213,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
   s->max_depth = ps.max_depth;
-  s->device_bytes = sizeof(rpl::Node4) * ps.nodes.size() + sizeof(rpl::Prim) * ps.prims.size() +
+  s->device_bytes = sizeof(rpl::Node4) * ps.nodes.size() + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * ps.prims.size() +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
   int bpc = 0;

@@ -390,6 +390,8 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   //      independent of visit order except exact-t ties)
   uint32_t n = d->n_hittables;
   if (n > rpl::MAX_PRIMS) { err = "too many hittables for the node encoding"; return RP_EINVAL; }
+  // the kernels address primitives and wide nodes by 32-bit byte offsets (<= n nodes of 128 B)
+  if ((uint64_t)n * sizeof(rpl::Prim) > 0xFFFFFFFFull) { err = "too many hittables for 32-bit device offsets"; return RP_EINVAL; }
   if (opt.max_leaf < 1 || opt.max_leaf > rpl::LEAF_MAX) { err = "max_leaf out of range"; return RP_EINVAL; }
   std::vector<Ref> refs(n);
   for (uint32_t i = 0; i < n; i++) {
@@ -427,10 +429,13 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   // ---- primitives in leaf order
   out.prims.resize(order.size() ? order.size() : 1);
   std::memset(out.prims.data(), 0, sizeof(rpl::Prim) * out.prims.size());
+  out.prim_refs.resize(out.prims.size());
+  std::memset(out.prim_refs.data(), 0, sizeof(rpl::PrimRef) * out.prim_refs.size());
   for (size_t k = 0; k < order.size(); k++) {
     const rp_hittable& h = d->hittables[order[k]];
     rpl::Prim& p = out.prims[k];
-    p.src = order[k];
+    rpl::PrimRef& pr = out.prim_refs[k];
+    pr.src = order[k];
     if (h.kind == RP_HITTABLE_SPHERE) {
       p.kind = rpl::PRIM_SPHERE;
       p.material = h.material;
@@ -449,9 +454,9 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
         p.g[3 + k2] = a[k2] - b[k2];  // ba, hittable.rs:71 (same IEEE subtraction as on the device)
         p.g[6 + k2] = a[k2] - c[k2];  // ca, hittable.rs:72
       }
-      p.v[0] = (uint32_t)(vbase[h.mesh] + i0);
-      p.v[1] = (uint32_t)(vbase[h.mesh] + i1);
-      p.v[2] = (uint32_t)(vbase[h.mesh] + i2);
+      pr.v[0] = (uint32_t)(vbase[h.mesh] + i0);
+      pr.v[1] = (uint32_t)(vbase[h.mesh] + i1);
+      pr.v[2] = (uint32_t)(vbase[h.mesh] + i2);
     }
   }
   return RP_OK;

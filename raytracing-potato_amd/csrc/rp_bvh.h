@@ -26,6 +26,7 @@ struct BuildOptions {
 struct PackedScene {
   std::vector<rpl::Node4> nodes;      // nodes[root] is the root (always an inner record)
   std::vector<rpl::Prim> prims;       // leaf order
+  std::vector<rpl::PrimRef> prim_refs;  // leaf order: vertex ids, source hittable
   std::vector<double> vnrm;           // 3 per global vertex (mesh vertices concatenated)
   std::vector<double> vuv;            // 2 per global vertex
   std::vector<rpl::Material> materials;

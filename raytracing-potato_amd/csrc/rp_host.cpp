@@ -491,7 +491,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
           double w = 1.0 - u - v;
           if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
           best = t;
-          bestp = p.src;
+          bestp = ps.prim_refs[k].src;
         } else {
           const double tc[3] = {o[0] - p.g[0], o[1] - p.g[1], o[2] - p.g[2]};
           double a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
@@ -506,7 +506,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
             if (t < tmin || t > best) continue;
           }
           best = t;
-          bestp = p.src;
+          bestp = ps.prim_refs[k].src;
         }
         best32 = up(best);
       }

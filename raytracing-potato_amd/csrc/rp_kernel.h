@@ -9,6 +9,7 @@ namespace rpk {
 struct KScene {
   const rpl::Node4* nodes;
   const rpl::Prim* prims;
+  const rpl::PrimRef* prim_refs;
   const double* vnrm;
   const double* vuv;
   const rpl::Material* mats;

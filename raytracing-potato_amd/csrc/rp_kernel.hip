@@ -129,6 +129,12 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 #define RPK_RNG_BATCH 48
 #endif
 static constexpr uint32_t RING = RPK_RING;
+// Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs; the pixel sum and path throughput live in
+// the lane's slab instead of LDS, and a few cold values spill to scratch) -- measured 3.7% faster on C3
+// than 3 waves/SIMD with that state in LDS (-DRPK_W3).
+#ifndef RPK_W3
+#define RPK_W4
+#endif
 static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
 #ifdef RPK_W4
 static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
@@ -333,6 +339,8 @@ struct Ray32 {
   float oix, oiy, oiz;  // fl(o32 * inv)
   float slack;          // >= 3D (per ray)
   float tmin;           // t_min rounded down
+  uint32_t nx, ny, nz;  // byte offset of the near plane of each axis within Node4 (lo_* or hi_*: by the
+                        // sign of the slope), the far plane is the other one
 };
 
 // next representable float towards +inf / -inf (finite inputs; the callers only step values that
@@ -372,6 +380,10 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, Ray32& r) {
   D = fmax(D, (ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)r.oiz) * u);
   r.slack = f32_up(3.0 * D * k + 0x1p-126);
   r.tmin = f32_down(tmin);
+  // Node4: lo_x at 0, hi_x at 16, lo_y at 32, hi_y at 48, lo_z at 64, hi_z at 80
+  r.nx = r.ix < 0.0f ? 16u : 0u;
+  r.ny = r.iy < 0.0f ? 48u : 32u;
+  r.nz = r.iz < 0.0f ? 80u : 64u;
 }
 
 // Closest hit over the 4-wide BVH (the reference's Hittable::Bvh::hit, bvh.rs:121-124 / hit_node
@@ -405,12 +417,11 @@ RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
 // One exact f64 primitive test (the reference's Hittable::hit for a leaf, hittable.rs:39-101): on
 // acceptance `best` shrinks to t and the hit record is taken.
 RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, double& best, TravState& ts) {
-  const rpl::Prim* p = S.prims + k;
-  const double2 g01 = *reinterpret_cast<const double2*>(p->g);
-  const double2 g23 = *reinterpret_cast<const double2*>(p->g + 2);
-  const double2 g45 = *reinterpret_cast<const double2*>(p->g + 4);
-  const double2 g67 = *reinterpret_cast<const double2*>(p->g + 6);
-  const double2 g8k = *reinterpret_cast<const double2*>(p->g + 8);  // g[8], {kind, material}
+  // 32-bit byte offset from the wave-uniform base (scalar-base + vector-offset loads)
+  const double2* q = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(S.prims) +
+                                                      k * (uint32_t)sizeof(rpl::Prim));
+  const double2 g01 = q[0], g23 = q[1], g45 = q[2], g67 = q[3];
+  const double2 g8k = q[4];  // g[8], {kind, material}
   const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
   if (kind == rpl::PRIM_TRIANGLE) {
     // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
@@ -466,34 +477,39 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
   while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
     DREG(DREG_NODE)
-    const rpl::Node4* n = S.nodes + cur;
-    const float4 lx = *reinterpret_cast<const float4*>(n->lo_x);
-    const float4 hx = *reinterpret_cast<const float4*>(n->hi_x);
-    const float4 ly = *reinterpret_cast<const float4*>(n->lo_y);
-    const float4 hy = *reinterpret_cast<const float4*>(n->hi_y);
-    const float4 lz = *reinterpret_cast<const float4*>(n->lo_z);
-    const float4 hz = *reinterpret_cast<const float4*>(n->hi_z);
-    const uint4 ch = *reinterpret_cast<const uint4*>(n->child);
+    // Near/far planes chosen per ray by the slope signs (octant), so each child costs one max3 + max
+    // for t_near and one min3 + min for t_far.  For a valid box this is the same pair of values the
+    // min/max slab form picks (fma is monotone in the plane coordinate); an empty slot (lo = +inf,
+    // hi = -inf) gives t_near = +inf, t_far = -inf and a NaN limit, so it can never pass.
+    // 32-bit byte offsets from the (wave-uniform) node base: scalar-base + vector-offset addressing
+    const char* nb = reinterpret_cast<const char*>(S.nodes);
+    const uint32_t no = cur << 7;
+    const float4 nx = *reinterpret_cast<const float4*>(nb + (no + r.nx));
+    const float4 fx = *reinterpret_cast<const float4*>(nb + (no + (r.nx ^ 16u)));
+    const float4 ny = *reinterpret_cast<const float4*>(nb + (no + r.ny));
+    const float4 fy = *reinterpret_cast<const float4*>(nb + (no + (r.ny ^ 16u)));
+    const float4 nz = *reinterpret_cast<const float4*>(nb + (no + r.nz));
+    const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.nz ^ 16u)));
+    const uint4 ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
     float tn[4];
     uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
     // slab planes of children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the
     // same per-element rounding as fmaf
     const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
     const f2 nox = {-r.oix, -r.oix}, noy = {-r.oiy, -r.oiy}, noz = {-r.oiz, -r.oiz};
-    const f2 AX[2] = {pk_fma(f2{lx.x, lx.y}, ix, nox), pk_fma(f2{lx.z, lx.w}, ix, nox)};
-    const f2 BX[2] = {pk_fma(f2{hx.x, hx.y}, ix, nox), pk_fma(f2{hx.z, hx.w}, ix, nox)};
-    const f2 AY[2] = {pk_fma(f2{ly.x, ly.y}, iy, noy), pk_fma(f2{ly.z, ly.w}, iy, noy)};
-    const f2 BY[2] = {pk_fma(f2{hy.x, hy.y}, iy, noy), pk_fma(f2{hy.z, hy.w}, iy, noy)};
-    const f2 AZ[2] = {pk_fma(f2{lz.x, lz.y}, iz, noz), pk_fma(f2{lz.z, lz.w}, iz, noz)};
-    const f2 BZ[2] = {pk_fma(f2{hz.x, hz.y}, iz, noz), pk_fma(f2{hz.z, hz.w}, iz, noz)};
+    const f2 NX[2] = {pk_fma(f2{nx.x, nx.y}, ix, nox), pk_fma(f2{nx.z, nx.w}, ix, nox)};
+    const f2 FX[2] = {pk_fma(f2{fx.x, fx.y}, ix, nox), pk_fma(f2{fx.z, fx.w}, ix, nox)};
+    const f2 NY[2] = {pk_fma(f2{ny.x, ny.y}, iy, noy), pk_fma(f2{ny.z, ny.w}, iy, noy)};
+    const f2 FY[2] = {pk_fma(f2{fy.x, fy.y}, iy, noy), pk_fma(f2{fy.z, fy.w}, iy, noy)};
+    const f2 NZ[2] = {pk_fma(f2{nz.x, nz.y}, iz, noz), pk_fma(f2{nz.z, nz.w}, iz, noz)};
+    const f2 FZ[2] = {pk_fma(f2{fz.x, fz.y}, iz, noz), pk_fma(f2{fz.z, fz.w}, iz, noz)};
     f2 TN[2], TF[2];
 #pragma unroll
     for (int q = 0; q < 2; q++) {
 #pragma unroll
       for (int e = 0; e < 2; e++) {
-        const float ax = AX[q][e], bx = BX[q][e], ay = AY[q][e], by = BY[q][e], az = AZ[q][e], bz = BZ[q][e];
-        TN[q][e] = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), r.tmin));
-        TF[q][e] = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), best32));
+        TN[q][e] = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
+        TF[q][e] = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
       }
       // tnear <= tfar + 2^-19 |tfar| + slack (section 4.2 of DESIGN.md), as packed FMA + add
       const f2 lim = pk_fma(f2{fabsf(TF[q][0]), fabsf(TF[q][1])}, f2{0x1p-19f, 0x1p-19f}, TF[q]) +
@@ -501,7 +517,7 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
 #pragma unroll
       for (int e = 0; e < 2; e++) {
         const int c = 2 * q + e;
-        tn[c] = (TN[q][e] <= lim[e] && cc[c] != rpl::ENTRY_EMPTY) ? TN[q][e] : __builtin_huge_valf();
+        tn[c] = TN[q][e] <= lim[e] ? TN[q][e] : __builtin_huge_valf();
       }
     }
     // sort (tn, entry) ascending: misses (+inf) go last
@@ -605,7 +621,8 @@ RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, 
   const bool need_uv = force_uv || S.mats[s.material].needs_uv != 0;
   if (p->kind == rpl::PRIM_TRIANGLE) {
     const double u = hr.u, v = hr.v, w = 1.0 - u - v;
-    const uint32_t i0 = p->v[0], i1 = p->v[1], i2 = p->v[2];
+    const rpl::PrimRef& pr = S.prim_refs[hr.prim];
+    const uint32_t i0 = pr.v[0], i1 = pr.v[1], i2 = pr.v[2];
     const V3 n0 = v3(S.vnrm[3 * i0], S.vnrm[3 * i0 + 1], S.vnrm[3 * i0 + 2]);
     const V3 n1 = v3(S.vnrm[3 * i1], S.vnrm[3 * i1 + 1], S.vnrm[3 * i1 + 2]);
     const V3 n2 = v3(S.vnrm[3 * i2], S.vnrm[3 * i2 + 1], S.vnrm[3 * i2 + 2]);
@@ -815,6 +832,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   KScene S;
   S.nodes = A->S.nodes;
   S.prims = A->S.prims;
+  S.prim_refs = A->S.prim_refs;
   S.vnrm = A->S.vnrm;
   S.vuv = A->S.vuv;
   S.mats = A->S.mats;

@@ -36,17 +36,24 @@ constexpr uint32_t MAX_PRIMS = LEAF_FIRST_MASK - LEAF_MAX;  // keeps every leaf 
 
 enum : uint32_t { PRIM_SPHERE = 0, PRIM_TRIANGLE = 1 };
 
-// Primitive in leaf order: 96 B.
-//   triangle: g = {a.xyz, (a-b).xyz, (a-c).xyz}, v = global vertex ids (normals/uvs for shading)
+// Primitive in leaf order: 80 B, everything the intersection test reads (five 16 B loads per lane).
+//   triangle: g = {a.xyz, (a-b).xyz, (a-c).xyz}
 //   sphere:   g = {center.xyz, radius, 0...}
+// Adding data here costs more than it saves: each extra 16 B is one more divergent load per test (a
+// variant carrying the determinant's products, 176 B, ran 10% slower although it saved 12 f64 ops).
 struct alignas(16) Prim {
   double g[9];
   uint32_t kind;
   uint32_t material;
+};
+static_assert(sizeof(Prim) == 80, "Prim must be 80 B");
+
+// Per primitive, read only for the closest hit: global vertex ids (normals/uvs) and the source hittable.
+struct alignas(16) PrimRef {
   uint32_t v[3];
   uint32_t src;  // index of the source hittable (diagnostics / tie analysis)
 };
-static_assert(sizeof(Prim) == 96, "Prim must be 96 B");
+static_assert(sizeof(PrimRef) == 16, "PrimRef must be 16 B");
 
 // Material: rp_material flattened (material.rs:87-91).
 struct alignas(16) Material {
