@@ -18,10 +18,16 @@
  *     thread-local message for the last failure on the calling thread.  Nothing aborts or panics.
  *   - Ownership: the caller owns every buffer it passes.  rp_scene_create deep-copies the scene into
  *     device memory (HBM); the scene is immutable afterwards.
- *   - Determinism (the RNG contract): pixel (i, j) is rendered with its own
- *     StdRng::seed_from_u64(params.seed + j*width + i) (rand 0.8 StdRng = ChaCha12) and the unchanged
- *     per-pixel body of main.rs:70-87.  Output depends only on (scene, camera, seed, width, height, spp,
- *     max_bounce) -- never on tiling, sharding, device count or scheduling.
+ *   - Determinism (the RNG contract): the samples of pixel (i, j) are drawn in batches of
+ *     RP_SAMPLES_PER_STREAM; batch b (samples 64b .. 64b+63) is rendered with its own
+ *     StdRng::seed_from_u64(params.seed + b*width*height + j*width + i) (rand 0.8 StdRng = ChaCha12) and
+ *     the unchanged per-pixel body of main.rs:70-85 over its samples (make_uv_jitter from a clone of the
+ *     batch stream's start).  The pixel value is (S_0 + S_1 + ...) / spp, batch sums added in batch
+ *     order (main.rs:80,86).  For spp <= 64 this is one stream per pixel, seed + j*width + i.  Output
+ *     depends only on (scene, camera, seed, width, height, spp, max_bounce) -- never on tiling, sharding,
+ *     device count or scheduling.  (The reference draws every pixel of a worker's tiles from one
+ *     from_entropy() stream, main.rs:52, so its output is not reproducible; a pixel's samples are
+ *     sequential in a stream, so batching them is what lets one pixel's work spread over lanes/GPUs.)
  *   - Arithmetic is IEEE binary64 throughout, as the reference (utility.rs:14 `type Real = f64`).
  *   - Image layout: row-major, pixel (i, j) at index j*width + i, row j = 0 is the BOTTOM row
  *     (image.rs:31-33, main.rs:119, tga::save writes bottom-left origin).  RGB are linear f64 averages
@@ -37,7 +43,10 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 1
+#define RP_ABI_VERSION 2
+
+/* Samples per RNG stream (see "Determinism" above). */
+#define RP_SAMPLES_PER_STREAM 64
 
 typedef enum rp_status {
   RP_OK = 0,
@@ -195,7 +204,9 @@ int rp_render(rp_scene* scene, const rp_camera* camera, const rp_render_params* 
  * device.  d_shard_rgb: shard_pixel_count*3 doubles in device memory, compact shard order.
  * d_shard_fg (nullable): shard_pixel_count floats.  d_counters (nullable): 4 uint64 in device memory
  * that receive {rays, samples, pixels, status}; they are zeroed on the stream before the launch.
- * No host synchronisation, allocation or copy happens inside: safe to capture in a hipGraph. */
+ * No host synchronisation or copy happens inside.  A frame with spp > RP_SAMPLES_PER_STREAM uses a
+ * scene-owned workspace (3 doubles + 1 uint32 per pixel and batch) allocated by the first call that
+ * needs it: render once before capturing such calls into a hipGraph. */
 int rp_render_device(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
                      double* d_shard_rgb, float* d_shard_fg, uint64_t* d_counters, void* stream);
 

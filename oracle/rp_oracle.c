@@ -776,7 +776,8 @@ static ray_t shoot(const rp_camera* cam, double u, double v, or_rng* rng) {
   return r;
 }
 
-/* main.rs:70-87 per-pixel body, with the caller's rng; returns the average colour and foreground */
+/* main.rs:70-85 per-pixel body over `spp` samples with the caller's rng: the colour sum (main.rs:80)
+ * and the number of samples whose first ray hit (main.rs:81); the caller divides (main.rs:86-87). */
 static void render_pixel(const or_scene* s, const rp_camera* cam, uint32_t i, uint32_t j, uint32_t W, uint32_t H,
                          uint32_t spp, uint32_t max_bounce, or_rng* rng, ctr_t* C, double out[3], double* fg) {
   or_rng jit = *rng;  /* render.rs:75 make_uv_jitter clones the rng */
@@ -792,8 +793,8 @@ static void render_pixel(const or_scene* s, const rp_camera* cam, uint32_t i, ui
     fc = add(fc, c);
     if (hit) foreground += 1.0;
   }
-  out[0] = fc.x / (double)spp; out[1] = fc.y / (double)spp; out[2] = fc.z / (double)spp;
-  *fg = foreground / (double)spp;
+  out[0] = fc.x; out[1] = fc.y; out[2] = fc.z;
+  *fg = foreground;
 }
 
 /* ---- per-pixel-seeded render (RNG contract) ---- */
@@ -826,13 +827,25 @@ static void* render_worker(void* arg) {
     for (uint32_t tj = 0; tj < h; tj++)
       for (uint32_t ti = 0; ti < w; ti++) {
         uint32_t i = ox + ti, j = oy + tj;
-        or_rng rng;
-        or_rng_seed_from_u64(&rng, J->p->seed + (uint64_t)j * J->p->width + i);
-        double c[3], fg;
-        render_pixel(J->s, J->cam, i, j, J->p->width, J->p->height, J->p->spp, J->p->max_bounce, &rng, &C, c, &fg);
+        /* RNG contract: batch b (samples 64b .. 64b+63) of pixel (i, j) has its own stream
+         * seed_from_u64(seed + b*W*H + j*W + i) and runs the unchanged per-pixel body over its samples;
+         * the batch sums are added in batch order, then divided by spp (main.rs:86-87). */
+        const uint64_t WH = (uint64_t)J->p->width * J->p->height;
+        double c[3] = {0.0, 0.0, 0.0}, fg = 0.0;
+        for (uint32_t b = 0; b * OR_SAMPLES_PER_STREAM < J->p->spp; b++) {
+          uint32_t n = J->p->spp - b * OR_SAMPLES_PER_STREAM;
+          if (n > OR_SAMPLES_PER_STREAM) n = OR_SAMPLES_PER_STREAM;
+          or_rng rng;
+          or_rng_seed_from_u64(&rng, J->p->seed + b * WH + (uint64_t)j * J->p->width + i);
+          double cb[3], fb;
+          render_pixel(J->s, J->cam, i, j, J->p->width, J->p->height, n, J->p->max_bounce, &rng, &C, cb, &fb);
+          c[0] = c[0] + cb[0]; c[1] = c[1] + cb[1]; c[2] = c[2] + cb[2];
+          fg += fb;
+        }
+        const double spp = (double)J->p->spp;
         size_t px = (size_t)j * J->p->width + i;
-        J->out[3 * px] = c[0]; J->out[3 * px + 1] = c[1]; J->out[3 * px + 2] = c[2];
-        if (J->fg) J->fg[px] = (float)fg;
+        J->out[3 * px] = c[0] / spp; J->out[3 * px + 1] = c[1] / spp; J->out[3 * px + 2] = c[2] / spp;
+        if (J->fg) J->fg[px] = (float)(fg / spp);
       }
   }
   pthread_mutex_lock(&J->mu);
@@ -900,7 +913,9 @@ static void* base_worker(void* arg) {
       for (uint32_t ti = 0; ti < tile.w; ti++) {
         double c[3], fg;
         render_pixel(B->s, B->cam, ti + tile.oi, tj + tile.oj, B->W, B->H, B->spp, B->max_bounce, &rng, &C, c, &fg);
-        cb[3 * (ti + tj * tile.w)] = c[0]; cb[3 * (ti + tj * tile.w) + 1] = c[1]; cb[3 * (ti + tj * tile.w) + 2] = c[2];
+        const double spp = (double)B->spp;  /* main.rs:86 */
+        cb[3 * (ti + tj * tile.w)] = c[0] / spp; cb[3 * (ti + tj * tile.w) + 1] = c[1] / spp;
+        cb[3 * (ti + tj * tile.w) + 2] = c[2] / spp;
       }
     if (B->out)
       for (uint32_t tj = 0; tj < tile.h; tj++)

@@ -67,8 +67,12 @@ int or_scene_info(const or_scene* s, uint32_t* n_nodes, uint32_t* depth);
 int or_intersect(or_scene* s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_material,
                  uint64_t* counters);
 
-/* Per-pixel-seeded render (the RNG contract), same output convention as rp_render (full frame, only the
- * shard's pixels written).  threads >= 1; the result does not depend on it. */
+/* Samples per RNG stream of the RNG contract (include/rp.h RP_SAMPLES_PER_STREAM). */
+#define OR_SAMPLES_PER_STREAM RP_SAMPLES_PER_STREAM
+
+/* Per-pixel-seeded render (the RNG contract: one stream per pixel and batch of OR_SAMPLES_PER_STREAM
+ * samples), same output convention as rp_render (full frame, only the shard's pixels written).
+ * threads >= 1; the result does not depend on it. */
 int or_render(or_scene* s, const rp_camera* cam, const rp_render_params* p, double* out_rgb,
               float* out_fg, uint64_t* counters, int threads);
 

@@ -72,6 +72,9 @@ struct rp_scene {
   uint64_t* d_diag = nullptr;  // diagnostic counters (rpk::DIAG_N)
   uint32_t* d_slab = nullptr;  // keystream cache, one slab per resident render lane
   uint32_t* d_tile_cost = nullptr;   // cost probe output, rpk::TILE_SORT_MAX entries
+  double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames (grown on demand)
+  uint32_t* d_partial_hits = nullptr;
+  uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
   uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
   uint64_t* d_probe_ctr = nullptr;   // counter block of the probe launch
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
@@ -90,6 +93,7 @@ struct Tiling {
 int make_tiling(const rp_render_params* p, Tiling& t) {
   if (!p) return fail(RP_EINVAL, "params is NULL");
   if (p->width == 0 || p->height == 0) return fail(RP_EINVAL, "width and height must be >= 1");
+  if (p->width > 65535 || p->height > 65535) return fail(RP_EINVAL, "width and height must be <= 65535");
   t.tw = p->tile_w ? p->tile_w : 32;
   t.th = p->tile_h ? p->tile_h : 32;
   t.shards = p->num_shards ? p->num_shards : 1;
@@ -150,7 +154,8 @@ void rp_scene_destroy(rp_scene* s) {
   DeviceGuard g(s->device);
   for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_prim_refs, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
                   (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab,
-                  (void*)s->d_tile_cost, (void*)s->d_tile_order, (void*)s->d_probe_ctr})
+                  (void*)s->d_tile_cost, (void*)s->d_tile_order, (void*)s->d_probe_ctr, (void*)s->d_partial,
+                  (void*)s->d_partial_hits})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -309,6 +314,28 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
   kp.n_shard_tiles = t.n_shard_tiles;
   kp.n_slots = t.n_slots;
   kp.trav_threshold = trav_threshold();
+  // RP_SPP_BATCH overrides the contract's batch size for timing studies only (it changes every
+  // multi-batch image: never set it for parity runs)
+  kp.spp_batch = rpk::SPP_BATCH;
+  if (const char* e = std::getenv("RP_SPP_BATCH")) kp.spp_batch = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
+  kp.nbatch = (p->spp + kp.spp_batch - 1) / kp.spp_batch;
+  kp.n_queue = t.n_slots * kp.nbatch;
+  if (kp.n_queue >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units)");
+  if (kp.nbatch > 1) {
+    if (kp.n_queue > s->partial_units) {  // scene-owned workspace, grown on the first call that needs it
+      if (s->d_partial) (void)hipFree(s->d_partial);
+      if (s->d_partial_hits) (void)hipFree(s->d_partial_hits);
+      s->d_partial = nullptr;
+      s->d_partial_hits = nullptr;
+      s->partial_units = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&s->d_partial), sizeof(double) * 3 * kp.n_queue) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&s->d_partial_hits), sizeof(uint32_t) * kp.n_queue) != hipSuccess)
+        return fail(RP_ENOMEM, "hipMalloc sample-batch workspace");
+      s->partial_units = kp.n_queue;
+    }
+    kp.partial = s->d_partial;
+    kp.partial_hits = s->d_partial_hits;
+  }
   const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
   auto grid_for = [&](uint64_t slots) {
     const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
@@ -322,6 +349,9 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
     // every pixel's sample 0 once spp is large enough to amortise it (a 1/spp extra), else a lattice
     pk.probe_px = p->spp >= rpk::PROBE_FULL_MIN_SPP ? t.tw * t.th : (uint32_t)rpk::PROBE_LATTICE;
     pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
+    pk.nbatch = 1;
+    pk.spp_batch = 1;
+    pk.n_queue = pk.n_slots;
     pk.tile_cost = s->d_tile_cost;
     RP_HIP(hipMemsetAsync(s->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
     RP_HIP(hipMemsetAsync(s->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
@@ -331,8 +361,12 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = s->d_tile_order;
   }
-  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid_for(t.n_slots), stream);
+  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid_for(kp.n_queue), stream);
   if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+  if (kp.nbatch > 1) {
+    e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
+  }
   return RP_OK;
 }
 

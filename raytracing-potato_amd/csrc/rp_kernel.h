@@ -56,7 +56,11 @@ struct KParams {
   uint32_t trav_threshold;  // resume shading once fewer than this many lanes of a wave still traverse
   uint32_t probe;           // 1 = cost probe: sample 0 of probe_px pixels per tile
   uint32_t probe_px;        // probe: every pixel of the tile (tw * th) or a 4 x 4 lattice (16)
-  uint32_t pad;
+  uint32_t nbatch;          // sample batches (RNG streams) per pixel: ceil(spp / spp_batch); 1 in a probe
+  uint32_t spp_batch;       // samples per batch: SPP_BATCH (the contract); other values for timing studies only
+  uint64_t n_queue;         // queue entries: n_slots * nbatch units (render), probed pixels (probe)
+  double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
+  uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
   uint32_t* tile_cost;         // probe: [k] rays summed over the tile's probed samples, [TILE_SORT_MAX + k]
                                // the longest probed sample (zeroed by the caller)
@@ -71,6 +75,11 @@ struct KParams {
 // Results do not depend on the order (per-pixel seeding).
 enum { PROBE_LATTICE = 16, PROBE_FULL_MIN_SPP = 32, TILE_SORT_MAX = 16384 };
 
+// RNG streams per (pixel, batch of SPP_BATCH samples) -- include/rp.h RP_SAMPLES_PER_STREAM.  The queue
+// hands out units (pixel, batch), so one pixel's samples run on several lanes at once; a unit of a
+// multi-batch frame leaves its sample sum in `partial` and reduce_batches adds them in batch order.
+enum { SPP_BATCH = 64 };
+
 // Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_QUEUE = 4, CTR_N = 8 };
 enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
@@ -83,6 +92,9 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
 // Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (longest sample, mean rays per probed
 // pixel), ties by tile index, into order[] (shard tile indices).  One block.
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32_t* order, void* stream);
+
+// Final pass of a multi-batch frame: per shard slot, the batch sums added in batch order, / spp.
+int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void* stream);
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t stack_depth, int* blocks);

@@ -856,16 +856,18 @@ RPK_INLINE KArgsPtr kargs() {
   return p;
 }
 
-// Pull the next pixel of the shard from the device-wide queue (slot order: tiles, row-major inside a
-// tile; slots of edge tiles outside the frame are skipped).  Returns false when the queue is drained.
+// Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
+// tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
+// row-major; slots of edge tiles outside the frame are skipped.  Returns false when the queue is drained.
 template <bool PROBE>
-RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
+RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t& batch) {
   KArgsPtr A = kargs();
   unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
   const uint32_t tw = A->P.tw, th = A->P.th;
   if (PROBE && A->P.probe_px == PROBE_LATTICE) {  // cost probe: a 4x4 lattice per tile, clamped into the frame
     slot = atomicAdd(queue, 1u);
-    if ((uint64_t)slot >= A->P.n_slots) return false;
+    if ((uint64_t)slot >= A->P.n_queue) return false;
+    batch = 0;
     const uint32_t k = slot / PROBE_LATTICE, sub = slot % PROBE_LATTICE;
     const uint32_t t = A->P.shard + k * A->P.nshards;
     const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
@@ -873,12 +875,14 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
     pj = min(ty * th + min((sub >> 2) * th / 4u + th / 8u, th - 1u), A->P.H - 1u);
     return true;
   }
-  const uint32_t tile_px = tw * th;
+  const uint32_t tile_px = tw * th, tile_units = tile_px * A->P.nbatch;
   for (;;) {
     const uint32_t q = atomicAdd(queue, 1u);
-    if ((uint64_t)q >= A->P.n_slots) return false;
-    uint32_t k = q / tile_px;
-    const uint32_t local = q - k * tile_px;
+    if ((uint64_t)q >= A->P.n_queue) return false;
+    uint32_t k = q / tile_units;
+    const uint32_t rem = q - k * tile_units;
+    batch = rem / tile_px;
+    const uint32_t local = rem - batch * tile_px;
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
     slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
     const uint32_t t = A->P.shard + k * A->P.nshards;
@@ -887,6 +891,16 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj) {
     pj = ty * th + local / tw;
     if (pi < A->P.W && pj < A->P.H) return true;
   }
+}
+
+// RNG contract (include/rp.h): batch b of pixel (i, j) is its own StdRng stream,
+// seed_from_u64(seed + b * W * H + j * W + i); batch 0 is the per-pixel stream of the original contract.
+RPK_INLINE uint64_t unit_seed(KArgsPtr A, uint32_t pi, uint32_t pj, uint32_t batch) {
+  return A->P.seed + (uint64_t)batch * A->P.W * A->P.H + (uint64_t)pj * A->P.W + pi;
+}
+// Samples in this unit's batch.
+RPK_INLINE uint32_t unit_spp(KArgsPtr A, uint32_t batch) {
+  return min(A->P.spp_batch, A->P.spp - batch * A->P.spp_batch);
 }
 
 // One camera sample (main.rs:75-76): make_uv_jitter draws 2s, 2s+1 of a CLONE of the pixel-start
@@ -950,13 +964,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   __shared__ double c_sum[3 * BLOCK];
   __shared__ double c_T[3 * BLOCK];
 #endif
+  // (8 words per lane: one more would push the block past 40 KB of LDS and cost a block per CU)
   __shared__ uint32_t c_u[8 * BLOCK];
   const uint32_t tid = threadIdx.x;
   uint32_t& slot = c_u[tid];
-  uint32_t& pi = c_u[BLOCK + tid];
-  uint32_t& pj = c_u[2 * BLOCK + tid];
+  uint32_t& pipj = c_u[BLOCK + tid];  // pixel i | j << 16 (make_tiling caps width and height at 65535)
   uint32_t& s = c_u[3 * BLOCK + tid];
   uint32_t& hits = c_u[4 * BLOCK + tid];
+  uint32_t& batch = c_u[2 * BLOCK + tid];
 #ifdef RPK_W4
   double* cold = reinterpret_cast<double*>(reinterpret_cast<uint4*>(kargs()->S.rng_slab) +
                                            ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N + SLAB_COLD);
@@ -987,12 +1002,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   hits = 0;
   sum_x = sum_y = sum_z = 0.0;
   TravState ts;
-  bool alive = fetch_pixel<PROBE>(slot, pi, pj);
+  uint32_t pi = 0, pj = 0;
+  bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
+  pipj = pi | (pj << 16);
   bool tdone = true;  // traversal of the current ray finished (or no ray)
   if (alive) {
     KArgsPtr A = kargs();
     RngBlk rb;
-    rng_begin_pixel(rng, rb, A->P.seed + (uint64_t)pj * A->P.W + pi);  // RNG contract
+    rng_begin_pixel(rng, rb, unit_seed(A, pi, pj, batch));  // RNG contract
     start_sample(rng, rb, 0, pi, pj, o, d);
     depth = A->P.max_bounce;
     trav_init(load_scene(A), INF, ts);
@@ -1008,7 +1025,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   for (;;) {
     DIAG(iters++;)
     DREG(DREG_ROUND)
-    rng_refill(rng, alive, s, kargs()->P.spp);
+    rng_refill(rng, alive, s, unit_spp(kargs(), batch));
     DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
     {
       KArgsPtr A = kargs();
@@ -1137,22 +1154,29 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         KArgsPtr A = kargs();
         s++;
         n_samples++;
-        if (s == A->P.spp) {  // main.rs:86-87
+        if (s == unit_spp(A, batch)) {  // main.rs:86-87 (for this unit's batch of samples)
           DREG(DREG_END_PIXEL)
           if (PROBE) {
             // spp is 1 here: the sample traced max_bounce - depth scattered rays plus its last one
             const uint32_t k = slot / A->P.probe_px, r = A->P.max_bounce - depth + (scattered_any ? 0u : 1u);
             atomicAdd(&A->P.tile_cost[k], r);
             atomicMax(&A->P.tile_cost[TILE_SORT_MAX + k], r);
-          } else {
+          } else if (A->P.nbatch == 1) {
             const double spp = (double)A->P.spp;
             double* out = A->out;
             out[3 * (uint64_t)slot + 0] = sum_x / spp;
             out[3 * (uint64_t)slot + 1] = sum_y / spp;
             out[3 * (uint64_t)slot + 2] = sum_z / spp;
             if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+          } else {  // one batch of several: its sum, reduced in batch order by reduce_batches
+            const uint64_t u = (uint64_t)slot * A->P.nbatch + batch;
+            double* part = A->P.partial;
+            part[3 * u + 0] = sum_x;
+            part[3 * u + 1] = sum_y;
+            part[3 * u + 2] = sum_z;
+            A->P.partial_hits[u] = hits;
           }
-          n_pixels++;
+          n_pixels += batch == 0 ? 1u : 0u;
           DIAG(if (!PROBE) {
             const uint32_t b = tbin(t_pix);
             atomicAdd(&A->diag[128 + b], (unsigned long long)(n_rays - rays_pix));
@@ -1160,19 +1184,21 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             t_pix = __builtin_amdgcn_s_memrealtime();
             rays_pix = n_rays;
           })
-          alive = fetch_pixel<PROBE>(slot, pi, pj);
+          uint32_t pi = 0, pj = 0;
+          alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
+          pipj = pi | (pj << 16);
           DIAG(if (!alive) t_retire = __builtin_amdgcn_s_memrealtime();)
           DIAG(if (!PROBE && !alive) atomicMax(&A->diag[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
           if (alive) {
             A = kargs();
-            rng_begin_pixel(rng, rb, A->P.seed + (uint64_t)pj * A->P.W + pi);
+            rng_begin_pixel(rng, rb, unit_seed(A, pi, pj, batch));
             s = 0;
             hits = 0;
             sum_x = sum_y = sum_z = 0.0;
           }
         }
         if (alive) {
-          start_sample(rng, rb, s, pi, pj, o, d);
+          start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
           A = kargs();
           depth = A->P.max_bounce;
           T_x = T_y = T_z = 1.0;
@@ -1261,6 +1287,39 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
   if (p.probe) hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
   else hipLaunchKernelGGL(render_kernel<false>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+// Multi-batch frames: pixel value = (S_0 + S_1 + ... + S_{nb-1}) / spp, added in batch order (the oracle's
+// order), foreground likewise.  One thread per shard slot; slots of edge tiles outside the frame skipped.
+__global__ void __launch_bounds__(256) reduce_batches_kernel(const KParams P, double* __restrict__ out,
+                                                            float* __restrict__ out_fg) {
+  const uint64_t slot = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (slot >= P.n_slots) return;
+  const uint32_t tile_px = P.tw * P.th, k = (uint32_t)(slot / tile_px), local = (uint32_t)(slot % tile_px);
+  const uint32_t t = P.shard + k * P.nshards;
+  if ((t % P.tiles_x) * P.tw + local % P.tw >= P.W || (t / P.tiles_x) * P.th + local / P.tw >= P.H) return;
+  const double* part = P.partial + 3 * slot * P.nbatch;
+  const uint32_t* ph = P.partial_hits + slot * P.nbatch;
+  double x = 0.0, y = 0.0, z = 0.0;
+  uint32_t h = 0;
+  for (uint32_t b = 0; b < P.nbatch; b++) {
+    x = x + part[3 * b];
+    y = y + part[3 * b + 1];
+    z = z + part[3 * b + 2];
+    h += ph[b];
+  }
+  const double spp = (double)P.spp;
+  out[3 * slot + 0] = x / spp;
+  out[3 * slot + 1] = y / spp;
+  out[3 * slot + 2] = z / spp;
+  if (out_fg) out_fg[slot] = (float)((double)h / spp);
+}
+
+int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void* stream) {
+  if (p.n_slots == 0) return 0;
+  hipLaunchKernelGGL(reduce_batches_kernel, dim3((unsigned)((p.n_slots + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, p, out_rgb, out_fg);
   return (int)hipGetLastError();
 }
 

@@ -77,6 +77,31 @@ def test_small_spp(gpu, name, spp):
     _check(gpu, scene, params)
 
 
+@pytest.mark.parametrize("spp", [65, 130])
+def test_multi_batch_streams(gpu, spp):
+    """spp > RP_SAMPLES_PER_STREAM: one RNG stream per (pixel, batch of 64), batches on different lanes,
+    sums reduced in batch order -- a partial last batch (65 = 64 + 1, 130 = 64 + 64 + 2)."""
+    scene, params = _scene("bunny_full", 40, 24, spp)
+    _check(gpu, scene, params)
+
+
+def test_multi_batch_shards_bitwise(gpu):
+    """Batched frames shard like single-stream ones: shards reassemble into the full frame bit for bit."""
+    from rtpotato.scene import RenderParams
+    from rtpotato import scenes
+    sc = scenes.configure(scenes.bunny_full(), 50, 30)
+    full, _, st_full = gpu.render(sc, RenderParams(50, 30, 70, 8, 3, 16, 16))
+    acc = np.zeros_like(full)
+    with gpu.DeviceScene(sc) as ds:
+        for s in range(2):
+            p = RenderParams(50, 30, 70, 8, 3, 16, 16, s, 2)
+            part, _, _ = ds.render(p)
+            m = shard_mask(p)
+            acc[m] = part[m]
+    assert np.array_equal(acc, full)
+    assert st_full["pixels"] == 50 * 30
+
+
 def test_max_bounce_variants(gpu):
     from rtpotato.scene import RenderParams
     from rtpotato import scenes
