@@ -347,7 +347,11 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
     pk.probe = 1;
     pk.spp = 1;
     // every pixel's sample 0 once spp is large enough to amortise it (a 1/spp extra), else a lattice
-    pk.probe_px = p->spp >= rpk::PROBE_FULL_MIN_SPP ? t.tw * t.th : (uint32_t)rpk::PROBE_LATTICE;
+    // an n x n lattice of pixels per tile (RP_PROBE_N overrides n for tuning; 0 = every pixel)
+    pk.probe_n = rpk::PROBE_LATTICE_N;
+    if (const char* e = std::getenv("RP_PROBE_N")) pk.probe_n = (uint32_t)std::strtoul(e, nullptr, 10);
+    pk.probe_n = std::min(pk.probe_n, std::min(t.tw, t.th));
+    pk.probe_px = pk.probe_n ? pk.probe_n * pk.probe_n : t.tw * t.th;
     pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
     pk.nbatch = 1;
     pk.spp_batch = 1;

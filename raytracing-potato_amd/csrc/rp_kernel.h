@@ -55,7 +55,8 @@ struct KParams {
   uint64_t n_slots;  // n_shard_tiles * tw * th
   uint32_t trav_threshold;  // resume shading once fewer than this many lanes of a wave still traverse
   uint32_t probe;           // 1 = cost probe: sample 0 of probe_px pixels per tile
-  uint32_t probe_px;        // probe: every pixel of the tile (tw * th) or a 4 x 4 lattice (16)
+  uint32_t probe_px;        // probe: pixels probed per tile: every pixel (tw * th) or an n x n lattice (n^2)
+  uint32_t probe_n;         // probe: lattice side n, 0 = every pixel
   uint32_t nbatch;          // sample batches (RNG streams) per pixel: ceil(spp / spp_batch); 1 in a probe
   uint32_t spp_batch;       // samples per batch: SPP_BATCH (the contract); other values for timing studies only
   uint64_t n_queue;         // queue entries: n_slots * nbatch units (render), probed pixels (probe)
@@ -69,11 +70,11 @@ struct KParams {
 // Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last
 // pixels after the queue drained) was ~23% of the C3 frame; handing out the expensive tiles first
 // (longest-processing-time-first) leaves cheap, uniform tiles for the end.  The order comes from a probe
-// launch of the same kernel (sample 0 of every pixel, or of a 4 x 4 lattice per tile at low spp: the exact
+// launch of the same kernel (sample 0 of a 16 x 16 lattice of pixels per tile: the exact
 // paths of the frame) and a one-block sort.  Tiles holding the longest paths go first: a pixel's samples
 // run sequentially on one lane, so one expensive pixel fetched late becomes a latency-bound tail by itself.
 // Results do not depend on the order (per-pixel seeding).
-enum { PROBE_LATTICE = 16, PROBE_FULL_MIN_SPP = 32, TILE_SORT_MAX = 16384 };
+enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
 
 // RNG streams per (pixel, batch of SPP_BATCH samples) -- include/rp.h RP_SAMPLES_PER_STREAM.  The queue
 // hands out units (pixel, batch), so one pixel's samples run on several lanes at once; a unit of a

@@ -864,15 +864,16 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
   KArgsPtr A = kargs();
   unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
   const uint32_t tw = A->P.tw, th = A->P.th;
-  if (PROBE && A->P.probe_px == PROBE_LATTICE) {  // cost probe: a 4x4 lattice per tile, clamped into the frame
+  if (PROBE && A->P.probe_n) {  // cost probe: an n x n lattice per tile (cell centres), clamped into the frame
     slot = atomicAdd(queue, 1u);
     if ((uint64_t)slot >= A->P.n_queue) return false;
     batch = 0;
-    const uint32_t k = slot / PROBE_LATTICE, sub = slot % PROBE_LATTICE;
+    const uint32_t n = A->P.probe_n;
+    const uint32_t k = slot / A->P.probe_px, sub = slot % A->P.probe_px;
     const uint32_t t = A->P.shard + k * A->P.nshards;
     const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
-    pi = min(tx * tw + min((sub & 3u) * tw / 4u + tw / 8u, tw - 1u), A->P.W - 1u);
-    pj = min(ty * th + min((sub >> 2) * th / 4u + th / 8u, th - 1u), A->P.H - 1u);
+    pi = min(tx * tw + min((sub % n) * tw / n + tw / (2u * n), tw - 1u), A->P.W - 1u);
+    pj = min(ty * th + min((sub / n) * th / n + th / (2u * n), th - 1u), A->P.H - 1u);
     return true;
   }
   const uint32_t tile_px = tw * th, tile_units = tile_px * A->P.nbatch;
