@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import glob
 import json
 import os
 import sys
@@ -45,6 +46,15 @@ def algorithmic_per_ray(config: str):
     ev = json.load(open(os.path.join(REPO, "tests", "golden", "event_counts.json")))
     per = ev[config]["per_ray"]
     return (sum(BYTES[k] * per[k] for k in BYTES), sum(FLOPS[k] * per[k] for k in FLOPS), ev[config])
+
+
+def pmc_traffic(config: str):
+    """HBM-side bytes per launch of the frame kernel from the committed rocprofv3 PMC record
+    (tools/pmc_traffic.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"{config.lower()}_pmc_traffic.json")), reverse=True):
+        rec = json.load(open(f))
+        return rec["traffic_bytes"], os.path.relpath(f, REPO), rec.get("git")
+    return None, None, None
 
 
 def cpu_baseline(config: str, spp: int, workers: int):
@@ -146,6 +156,7 @@ def main():
     if rank == 0:
         bpr, fpr, ev = algorithmic_per_ray(args.config if args.config in ("C1", "C2", "C3") else "C3")
         achieved_gbs = bpr * rays_step / kernel_s / 1e9
+        traffic, traffic_src, traffic_git = pmc_traffic(args.config) if args.spp == 0 else (None, None, None)
         achieved_tf = fpr * rays_step / kernel_s / 1e12
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
@@ -158,7 +169,8 @@ def main():
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather" if world > 1 else "1 GPU",
                        "rays_per_frame": int(total_rays_step), "rays_per_sample": total_rays_step / total_samples_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src and f"{traffic_src} (rocprofv3 PMC, build {traffic_git})",
                          "kernel": "rpk::render_kernel<false>", "kernel_ms": round(kernel_s * 1e3, 3),
                          "bytes_per_ray": round(bpr, 1),
                          "note": "bunny scene (~1.3 MB) is cache-resident: HBM fraction is low by construction; "
