@@ -1062,10 +1062,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       hr.v = ts.bv;
       hr.prim = ts.bestp;
 
-      // ---- this ray's keystream block
-      RngBlk rb;
-      rng_load(rng, rb);
-
       // ---- shade.  Hits and misses share one spherical-uv site and one texture-sampling site, so a wave
       // with both pays for each f64 atan2/asin and texture walk once.
       bool end_sample = true, scattered_any = false;
@@ -1117,7 +1113,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         }
         // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
         V3 nd = v3(0.0, 0.0, 0.0);
-        const bool scattered = hit && scatter_eval(*m, d, h, rng, rb, nd);
+        // this ray's keystream block, in registers only around the scatter (the live set of the shading
+        // code is what decides the kernel's register budget)
+        bool scattered = false;
+        if (hit) {
+          RngBlk rb;
+          rng_load(rng, rb);
+          scattered = scatter_eval(*m, d, h, rng, rb, nd);
+        }
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
         if (t1) {
           DREG(DREG_TEX)
@@ -1192,13 +1195,16 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           DIAG(if (!PROBE && !alive) atomicMax(&A->diag[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
           if (alive) {
             A = kargs();
-            rng_begin_pixel(rng, rb, unit_seed(A, pi, pj, batch));
+            RngBlk rb0;
+            rng_begin_pixel(rng, rb0, unit_seed(A, pi, pj, batch));
             s = 0;
             hits = 0;
             sum_x = sum_y = sum_z = 0.0;
           }
         }
         if (alive) {
+          RngBlk rb;
+          rng_load(rng, rb);
           start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
           A = kargs();
           depth = A->P.max_bounce;
