@@ -19,11 +19,11 @@
  *   - Ownership: the caller owns every buffer it passes.  rp_scene_create deep-copies the scene into
  *     device memory (HBM); the scene is immutable afterwards.
  *   - Determinism (the RNG contract): the samples of pixel (i, j) are drawn in batches of
- *     RP_SAMPLES_PER_STREAM; batch b (samples 64b .. 64b+63) is rendered with its own
+ *     RP_SAMPLES_PER_STREAM; batch b (samples 32b .. 32b+31) is rendered with its own
  *     StdRng::seed_from_u64(params.seed + b*width*height + j*width + i) (rand 0.8 StdRng = ChaCha12) and
  *     the unchanged per-pixel body of main.rs:70-85 over its samples (make_uv_jitter from a clone of the
  *     batch stream's start).  The pixel value is (S_0 + S_1 + ...) / spp, batch sums added in batch
- *     order (main.rs:80,86).  For spp <= 64 this is one stream per pixel, seed + j*width + i.  Output
+ *     order (main.rs:80,86).  For spp <= 32 this is one stream per pixel, seed + j*width + i.  Output
  *     depends only on (scene, camera, seed, width, height, spp, max_bounce) -- never on tiling, sharding,
  *     device count or scheduling.  (The reference draws every pixel of a worker's tiles from one
  *     from_entropy() stream, main.rs:52, so its output is not reproducible; a pixel's samples are
@@ -46,7 +46,7 @@ extern "C" {
 #define RP_ABI_VERSION 2
 
 /* Samples per RNG stream (see "Determinism" above). */
-#define RP_SAMPLES_PER_STREAM 64
+#define RP_SAMPLES_PER_STREAM 32
 
 typedef enum rp_status {
   RP_OK = 0,

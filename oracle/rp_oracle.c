@@ -827,7 +827,7 @@ static void* render_worker(void* arg) {
     for (uint32_t tj = 0; tj < h; tj++)
       for (uint32_t ti = 0; ti < w; ti++) {
         uint32_t i = ox + ti, j = oy + tj;
-        /* RNG contract: batch b (samples 64b .. 64b+63) of pixel (i, j) has its own stream
+        /* RNG contract: batch b (samples 32b .. 32b+31) of pixel (i, j) has its own stream
          * seed_from_u64(seed + b*W*H + j*W + i) and runs the unchanged per-pixel body over its samples;
          * the batch sums are added in batch order, then divided by spp (main.rs:86-87). */
         const uint64_t WH = (uint64_t)J->p->width * J->p->height;

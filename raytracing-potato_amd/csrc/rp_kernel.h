@@ -30,10 +30,10 @@ enum { RENDER_BLOCK = 256 };
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
 // lane primitive tests.
-enum { DIAG_N = 256 };
+enum { DIAG_N = 320 };
 // Timeline histograms (RPK_DIAG builds), 64 bins of DIAG_BIN_TICKS (100 MHz real-time clock) from the
 // block's start: [64 + b] lanes retiring in bin b, [128 + b] rays of the pixels fetched in bin b,
-// [192 + b] pixels fetched in bin b.
+// [192 + b] pixels fetched in bin b, [256 + b] the most rays of one unit fetched in bin b.
 enum { DIAG_HIST = 64, DIAG_BIN_TICKS = 1000000 };
 // Region counters (RPK_DIAG builds), from DIAG_N index 16: per code region r, [16 + 2r] = wave
 // executions and [17 + 2r] = active lanes summed over them (lane utilisation = lanes / (64 x execs)).
@@ -79,7 +79,10 @@ enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
 // RNG streams per (pixel, batch of SPP_BATCH samples) -- include/rp.h RP_SAMPLES_PER_STREAM.  The queue
 // hands out units (pixel, batch), so one pixel's samples run on several lanes at once; a unit of a
 // multi-batch frame leaves its sample sum in `partial` and reduce_batches adds them in batch order.
-enum { SPP_BATCH = 64 };
+// 32 samples: a C3 pixel's 256 samples become 8 units (an 8-GPU shard: ~2 M units for 262 k lanes); 64 ran
+// 0.8% faster on one GPU but left an 8-GPU shard with a 30% latency-bound tail (projection, 70% vs 84%
+// efficiency).
+enum { SPP_BATCH = 32 };
 
 // Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_QUEUE = 4, CTR_N = 8 };

@@ -1185,6 +1185,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             const uint32_t b = tbin(t_pix);
             atomicAdd(&A->diag[128 + b], (unsigned long long)(n_rays - rays_pix));
             atomicAdd(&A->diag[192 + b], 1ull);
+            atomicMax(&A->diag[256 + b], (unsigned long long)(n_rays - rays_pix));
             t_pix = __builtin_amdgcn_s_memrealtime();
             rays_pix = n_rays;
           })

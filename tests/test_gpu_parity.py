@@ -79,8 +79,8 @@ def test_small_spp(gpu, name, spp):
 
 @pytest.mark.parametrize("spp", [65, 130])
 def test_multi_batch_streams(gpu, spp):
-    """spp > RP_SAMPLES_PER_STREAM: one RNG stream per (pixel, batch of 64), batches on different lanes,
-    sums reduced in batch order -- a partial last batch (65 = 64 + 1, 130 = 64 + 64 + 2)."""
+    """spp > RP_SAMPLES_PER_STREAM: one RNG stream per (pixel, batch of 32), batches on different lanes,
+    sums reduced in batch order -- a partial last batch (65 = 2 x 32 + 1, 130 = 4 x 32 + 2)."""
     scene, params = _scene("bunny_full", 40, 24, spp)
     _check(gpu, scene, params)
 
@@ -202,6 +202,32 @@ def test_intersect_rays(gpu):
     assert np.array_equal(hits[ok & hit, 0], ref[ok & hit, 0])
     np.testing.assert_array_equal(hits[ok & hit, 1:7], ref[ok & hit, 1:7])
     assert np.max(np.abs(hits[ok & hit, 7:] - ref[ok & hit, 7:])) < 1e-12  # uv: OCML vs glibc atan2/asin
+
+
+def test_random_mesh_deep_tree(gpu):
+    """Config C5's scene type (random small triangles, Lambert, SkyGradient) at 200k triangles: a deep tree
+    of many thin leaves, the HBM-bound traversal case, against the oracle's reference median-split tree."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.random_mesh(200_000), 64, 64)
+    with gpu.DeviceScene(sc) as ds:
+        assert ds.info()["max_depth"] >= 8
+    _check(gpu, sc, RenderParams(64, 64, 4, 8, scenes.DEFAULT_SEED))
+
+
+@pytest.mark.slow
+def test_c2_full_size_sampled_parity(gpu):
+    """Config C2 (Lambert bunny, SkyGradient, 1920x1080x64) at full size; the oracle re-renders every 64th
+    tile (shard 9 of 64)."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    scene, params = scenes.config_scene("C2")
+    rgb, _, st = gpu.render(scene, params)
+    sub = RenderParams(params.width, params.height, params.spp, params.max_bounce, params.seed, 32, 32, 9, 64)
+    ref, _, ctr = oracle_render(scene, sub, threads=16)
+    c = compare(rgb, ref, shard_mask(sub))
+    assert c["linf"] < TOL_LINF and c["exact_frac"] > 0.999, c
+    assert st["pixels"] == params.width * params.height
 
 
 @pytest.mark.slow

@@ -1,15 +1,17 @@
 """The RNG contract's sample batching (include/rp.h "Determinism"), on the CPU oracle.
 
-Batch b of pixel (i, j) is its own stream seed_from_u64(seed + b*W*H + j*W + i) over samples 64b..64b+63,
-so batch 1 of a frame with seed S is batch 0 of the same pixel in a frame with seed S + W*H: a 70-spp
-frame must equal the spp-weighted mean of a 64-spp frame (seed S) and a 6-spp frame (seed S + W*H).
-Frames with spp <= 64 are the single per-pixel stream, which the golden fixtures pin.
+Batch b of pixel (i, j) is its own stream seed_from_u64(seed + b*W*H + j*W + i) over samples Sb..Sb+S-1 (S = RP_SAMPLES_PER_STREAM = 32),
+so batch 1 of a frame with seed X is batch 0 of the same pixel in a frame with seed X + W*H: an (S+6)-spp
+frame must equal the spp-weighted mean of an S-spp frame (seed X) and a 6-spp frame (seed X + W*H).
+Frames with spp <= S are the single per-pixel stream, which the golden fixtures pin.
 """
 from dataclasses import replace
 
 import numpy as np
 
 from parity import oracle_render
+
+SAMPLES_PER_STREAM = 32  # include/rp.h RP_SAMPLES_PER_STREAM
 
 
 def test_batches_compose_from_single_stream_frames():
@@ -18,23 +20,24 @@ def test_batches_compose_from_single_stream_frames():
     w, h = 20, 12
     scene = scenes.configure(scenes.bunny_full(), w, h)
     seed = 777
-    full, fg_full, c_full = oracle_render(scene, RenderParams(w, h, 70, 8, seed), threads=8, foreground=True)
-    a, fg_a, c_a = oracle_render(scene, RenderParams(w, h, 64, 8, seed), threads=8, foreground=True)
+    S = SAMPLES_PER_STREAM
+    full, fg_full, c_full = oracle_render(scene, RenderParams(w, h, S + 6, 8, seed), threads=8, foreground=True)
+    a, fg_a, c_a = oracle_render(scene, RenderParams(w, h, S, 8, seed), threads=8, foreground=True)
     b, fg_b, c_b = oracle_render(scene, RenderParams(w, h, 6, 8, seed + w * h), threads=8, foreground=True)
-    np.testing.assert_allclose(full, (a * 64 + b * 6) / 70, rtol=1e-12, atol=1e-14)
-    np.testing.assert_allclose(fg_full, (fg_a.astype(np.float64) * 64 + fg_b * 6) / 70, rtol=1e-6)
+    np.testing.assert_allclose(full, (a * S + b * 6) / (S + 6), rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(fg_full, (fg_a.astype(np.float64) * S + fg_b * 6) / (S + 6), rtol=1e-6)
     assert c_full["rays"] == c_a["rays"] + c_b["rays"]
-    assert c_full["samples"] == 70 * w * h
+    assert c_full["samples"] == (S + 6) * w * h
 
 
 def test_single_batch_frames_are_the_per_pixel_stream():
-    """spp <= 64: one stream per pixel, seed + j*W + i -- a pixel's value does not depend on spp's batch
+    """spp <= S: one stream per pixel, seed + j*W + i -- a pixel's value does not depend on spp's batch
     count and a sub-rectangle shard agrees with the full frame (per-pixel seeding)."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
     w, h = 16, 10
     scene = scenes.configure(scenes.bunny_full(), w, h)
-    p = RenderParams(w, h, 64, 8, 5)
+    p = RenderParams(w, h, SAMPLES_PER_STREAM, 8, 5)
     full, _, _ = oracle_render(scene, p, threads=4)
     shard, _, _ = oracle_render(scene, replace(p, tile_w=8, tile_h=8, shard=1, num_shards=2), threads=4)
     m = np.any(shard != 0, axis=2)

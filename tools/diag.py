@@ -16,19 +16,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=32)
+    ap.add_argument("--shards", type=int, default=1, help="render shard 0 of N (per-rank work of an N-GPU run)")
     a = ap.parse_args()
     os.environ.setdefault("RP_LIB", os.path.join(REPO, "raytracing-potato_amd", "lib", "librp_diag.so"))
     from dataclasses import replace
     from rtpotato import _ffi as F, scenes
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
-    params = replace(params, spp=a.spp)
+    params = replace(params, spp=a.spp, shard=0, num_shards=a.shards)
     ds = DeviceScene(scene)
     ds.render(replace(params, spp=1))  # warm
-    buf = (ctypes.c_uint64 * 256)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 256, 1))
+    buf = (ctypes.c_uint64 * 320)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 320, 1))
     _, _, st = ds.render(params)
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 256, 1))
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 320, 1))
     d = list(buf)
     ph = d[:5]
     tot = sum(ph)
@@ -57,7 +58,8 @@ def main():
     # timeline histograms (10 ms bins from each block's start): lanes retiring, pixels fetched and their rays
     last = max([b for b in range(64) if d[64 + b] or d[192 + b]] or [0])
     out["timeline_10ms"] = [{"t_ms": 10 * b, "retired_lanes": d[64 + b], "pixels": d[192 + b],
-                             "rays_per_pixel": round(d[128 + b] / max(1, d[192 + b]), 1)} for b in range(last + 1)]
+                             "rays_per_pixel": round(d[128 + b] / max(1, d[192 + b]), 1),
+                             "max_rays_unit": d[256 + b]} for b in range(last + 1)]
     print(json.dumps(out, indent=1))
 
 
