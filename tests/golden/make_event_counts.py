@@ -5,7 +5,7 @@ into algorithmic bytes / flops per ray for the roofline.  Test in
     python tests/golden/make_event_counts.py   ->   tests/golden/event_counts.json
 
 Sample per config: every 64th 32x32 tile (shard 5 of 64) of the full-size frame at the config's spp
-(C1: the whole 320x180x4 frame; C5: every 1024th tile at 4 spp); per-unit seeding makes the sample a subset
+(C1: the whole 320x180x4 frame; C5: every 1024th tile from the centre column at 4 spp); per-unit seeding makes the sample a subset
 of the real frame.
 """
 import ctypes
@@ -27,8 +27,8 @@ def main():
     out = {}
     for name in ("C1", "C2", "C3", "C5"):
         scene, params = scenes.config_scene(name)
-        if name == "C5":  # 10M triangles: 16 of the 16,384 tiles at 4 spp (per-ray averages)
-            params = RenderParams(params.width, params.height, 4, 8, params.seed, 32, 32, 5, 1024)
+        if name == "C5":  # 10M triangles: 16 of the 16,384 tiles (the centre column) at 4 spp
+            params = RenderParams(params.width, params.height, 4, 8, params.seed, 32, 32, 64, 1024)  # centre column
         elif name != "C1":
             params = RenderParams(params.width, params.height, params.spp, 8, params.seed, 32, 32, 5, 64)
         d = scene.desc()
