@@ -150,10 +150,20 @@ struct Rng {
   uint32_t* end;   // LDS cursor: one past the newest ring block
   uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
+// The keystream block being drawn from lives in the lane's traversal-stack column in LDS, not in registers:
+// a lane only draws while it shades, and a lane that shades has finished its traversal, so its stack column
+// is free (entries 0..15; the kernel sizes the stack to >= 16).  A draw is then one ds_read2st64 at the
+// lane's word offset (the column is [entry][lane], conflict-free) instead of a 16-way register select, and
+// the block costs no VGPRs through the shading code.
 struct RngBlk {
-  uint32_t w[16];
-  uint32_t blk;  // block index held in w
+  uint32_t* col;  // LDS: this lane's stack column (word k at col[k * BLOCK])
+  uint32_t blk;   // block index held in the column
+  RPK_INLINE explicit RngBlk(uint32_t* c) : col(c), blk(0xFFFFFFFFu) {}
 };
+RPK_INLINE void col_store(RngBlk& b, const uint32_t w[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; k++) b.col[k * BLOCK] = w[k];
+}
 
 RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
   const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
@@ -181,30 +191,33 @@ RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT 
 // Block pos/16 into registers: from the ring, or generated in place when the ring ran dry.
 RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
   b.blk = r.pos >> 4;
+  uint32_t w[16];
   if (b.blk < *r.end) {
     DREG(DREG_RING_LOAD)
-    load_block(ring_slot(r, b.blk), b.w);
+    load_block(ring_slot(r, b.blk), w);
   } else {
     DREG(DREG_RNG_FALLBACK)
     uint32_t k[8];
     load_key(r, k);
-    chacha12(k, b.blk, b.w);
-    store_block(ring_slot(r, b.blk), b.w);
+    chacha12(k, b.blk, w);
+    store_block(ring_slot(r, b.blk), w);
     *r.end = b.blk + 1;
   }
+  col_store(b, w);
 }
 
 // A new pixel: key from the RNG contract seed, block 0 (shared by the main stream and the jitter of
 // samples 0-3, render.rs:74-82) generated once into both caches and into registers.
 RPK_INLINE void rng_begin_pixel(Rng& r, RngBlk& b, uint64_t seed) {
   DREG(DREG_BEGIN_PIXEL)
-  uint32_t k[8];
+  uint32_t k[8], w[16];
   seed_key(seed, k);
   store_key(r, k);
-  chacha12(k, 0, b.w);
+  chacha12(k, 0, w);
   b.blk = 0;
-  store_block(ring_slot(r, 0), b.w);
-  store_block(jit_slot(r, 0), b.w);
+  store_block(ring_slot(r, 0), w);
+  store_block(jit_slot(r, 0), w);
+  col_store(b, w);
   r.pos = 0;
   *r.end = 1;
   r.jtag[0] = 0;
@@ -260,13 +273,7 @@ RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
 RPK_INLINE uint64_t next_u64(Rng& r, RngBlk& b) {
   if ((r.pos >> 4) != b.blk) rng_load(r, b);
   const uint32_t i = r.pos & 15u;
-  uint32_t lo = b.w[0], hi = b.w[1];
-#pragma unroll
-  for (int k = 1; k < 8; k++) {
-    const bool m = i == 2u * k;
-    lo = m ? b.w[2 * k] : lo;
-    hi = m ? b.w[2 * k + 1] : hi;
-  }
+  const uint32_t lo = b.col[i * BLOCK], hi = b.col[(i + 1u) * BLOCK];
   r.pos += 2;
   return ((uint64_t)hi << 32) | lo;
 }
@@ -952,7 +959,9 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   __syncthreads();
   uint32_t* stk = lds_stack + threadIdx.x;
 
-  uint32_t n_rays = 0, n_samples = 0, n_pixels = 0;
+  // per-WAVE totals (ballot popcounts: scalar registers, not three VGPRs through the shading code)
+  uint64_t n_rays = 0, n_samples = 0, n_pixels = 0;
+  DIAG(uint32_t lane_rays = 0;)
   bool overflow = false;
   DIAG(uint64_t ph[5] = {0, 0, 0, 0, 0}; uint64_t iters = 0, active = 0; TravDiag td; uint64_t t_prev = stamp();)
   DIAG(const uint64_t t_blk = __builtin_amdgcn_s_memrealtime(); uint64_t t_pix = t_blk, t_retire = t_blk; uint32_t rays_pix = 0;
@@ -1009,7 +1018,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   bool tdone = true;  // traversal of the current ray finished (or no ray)
   if (alive) {
     KArgsPtr A = kargs();
-    RngBlk rb;
+    RngBlk rb(stk);
     rng_begin_pixel(rng, rb, unit_seed(A, pi, pj, batch));  // RNG contract
     start_sample(rng, rb, 0, pi, pj, o, d);
     depth = A->P.max_bounce;
@@ -1052,10 +1061,12 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
     if (__ballot(alive) == 0) break;
 
+    n_rays += (uint64_t)__popcll(__ballot(alive && tdone));
+    bool ended_sample = false, ended_pixel = false;
     if (alive && tdone) {
       DIAG(active++;)
       DREG(DREG_SHADE)
-      n_rays++;
+      DIAG(lane_rays++;)
       HitRec hr;
       hr.t = ts.best;
       hr.u = ts.bu;
@@ -1117,7 +1128,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         // code is what decides the kernel's register budget)
         bool scattered = false;
         if (hit) {
-          RngBlk rb;
+          RngBlk rb(stk);
           rng_load(rng, rb);
           scattered = scatter_eval(*m, d, h, rng, rb, nd);
         }
@@ -1157,7 +1168,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         DREG(DREG_END_SAMPLE)
         KArgsPtr A = kargs();
         s++;
-        n_samples++;
+        ended_sample = true;
         if (s == unit_spp(A, batch)) {  // main.rs:86-87 (for this unit's batch of samples)
           DREG(DREG_END_PIXEL)
           if (PROBE) {
@@ -1180,14 +1191,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             part[3 * u + 2] = sum_z;
             A->P.partial_hits[u] = hits;
           }
-          n_pixels += batch == 0 ? 1u : 0u;
+          ended_pixel = batch == 0;
           DIAG(if (!PROBE) {
             const uint32_t b = tbin(t_pix);
-            atomicAdd(&A->diag[128 + b], (unsigned long long)(n_rays - rays_pix));
+            atomicAdd(&A->diag[128 + b], (unsigned long long)(lane_rays - rays_pix));
             atomicAdd(&A->diag[192 + b], 1ull);
-            atomicMax(&A->diag[256 + b], (unsigned long long)(n_rays - rays_pix));
+            atomicMax(&A->diag[256 + b], (unsigned long long)(lane_rays - rays_pix));
             t_pix = __builtin_amdgcn_s_memrealtime();
-            rays_pix = n_rays;
+            rays_pix = lane_rays;
           })
           uint32_t pi = 0, pj = 0;
           alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
@@ -1196,7 +1207,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           DIAG(if (!PROBE && !alive) atomicMax(&A->diag[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
           if (alive) {
             A = kargs();
-            RngBlk rb0;
+            RngBlk rb0(stk);
             rng_begin_pixel(rng, rb0, unit_seed(A, pi, pj, batch));
             s = 0;
             hits = 0;
@@ -1204,7 +1215,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           }
         }
         if (alive) {
-          RngBlk rb;
+          RngBlk rb(stk);
           rng_load(rng, rb);
           start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
           A = kargs();
@@ -1218,6 +1229,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         tdone = false;
       }
     }
+    n_samples += (uint64_t)__popcll(__ballot(ended_sample));
+    n_pixels += (uint64_t)__popcll(__ballot(ended_pixel));
     DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
   }
 
@@ -1244,9 +1257,11 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     if (!PROBE) atomicAdd(&dg[64 + tbin(t_retire)], 1ull);
   }
 #endif
-  atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);
-  atomicAdd(&blk_ctr[1], (unsigned long long)n_samples);
-  atomicAdd(&blk_ctr[2], (unsigned long long)n_pixels);
+  if ((threadIdx.x & 63u) == 0) {
+    atomicAdd(&blk_ctr[0], (unsigned long long)n_rays);
+    atomicAdd(&blk_ctr[1], (unsigned long long)n_samples);
+    atomicAdd(&blk_ctr[2], (unsigned long long)n_pixels);
+  }
   unsigned long long* ctr = kargs()->ctr;
   if (overflow) atomicOr(&ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
   __syncthreads();
