@@ -384,6 +384,12 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   out.background.kind = d->background.kind;
   out.background.tex = d->background.texture;
   out.background.needs_uv = d->background.kind == RP_EMIT_SKY_SPHERE && texture_reads_uv(d, d->background.texture);
+  if (d->background.kind == RP_EMIT_SKY_SPHERE && d->textures[d->background.texture].kind == RP_TEXTURE_IMAGE) {
+    const rpl::Texture& t = out.textures[d->background.texture];
+    out.background.img_w = t.width;
+    out.background.img_h = t.height;
+    out.background.img_off = (uint32_t)t.texel_offset;
+  }
   for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
 
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is

@@ -848,6 +848,9 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.background.kind = A->S.background.kind;
   S.background.tex = A->S.background.tex;
   S.background.needs_uv = A->S.background.needs_uv;
+  S.background.img_w = A->S.background.img_w;
+  S.background.img_h = A->S.background.img_h;
+  S.background.img_off = A->S.background.img_off;
   S.background.color[0] = A->S.background.color[0];
   S.background.color[1] = A->S.background.color[1];
   S.background.color[2] = A->S.background.color[2];
@@ -1117,10 +1120,22 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 #endif
         const bool t1 = ta || te;
         uint32_t tid1 = 0, px1 = 0;
+        // a miss under an Image sky sphere: size and offset are kernel arguments (scalar registers), so the
+        // texel load waits on no texture-table load
+        const bool sky_img = !hit && S.background.img_w != 0;
         if (t1) {
-          tid1 = tex_resolve(S, ta ? m->absorb_tex : emit_tex, h);
-          const rpl::Texture& t = S.texs[tid1];
-          if (t.kind == 3) px1 = S.texels[image_texel(t, h)];
+          if (sky_img) {
+            rpl::Texture t;
+            t.width = S.background.img_w;
+            t.height = S.background.img_h;
+            t.texel_offset = S.background.img_off;
+            tid1 = S.background.tex;
+            px1 = S.texels[image_texel(t, h)];
+          } else {
+            tid1 = tex_resolve(S, ta ? m->absorb_tex : emit_tex, h);
+            const rpl::Texture& t = S.texs[tid1];
+            if (t.kind == 3) px1 = S.texels[image_texel(t, h)];
+          }
         }
         // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
         V3 nd = v3(0.0, 0.0, 0.0);
@@ -1135,7 +1150,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
         if (t1) {
           DREG(DREG_TEX)
-          const V3 tv = tex_value(S, tid1, h, px1);
+          const V3 tv = sky_img ? v3(u8_unit(px1 & 0xffu), u8_unit((px1 >> 8) & 0xffu), u8_unit((px1 >> 16) & 0xffu))
+                                : tex_value(S, tid1, h, px1);
           if (ta) tex_ab = tv;
           else tex_em = tv;
         }

@@ -79,7 +79,8 @@ static_assert(sizeof(Texture) == 72 || sizeof(Texture) == 80, "Texture size");
 
 struct Emit {
   uint32_t kind, tex;  // tex only read for SkySphere
-  uint32_t needs_uv, pad;
+  uint32_t needs_uv, img_off;
+  uint32_t img_w, img_h;  // SkySphere over an Image (background): its size (img_w = 0 otherwise)
   double color[3];
 };
 
