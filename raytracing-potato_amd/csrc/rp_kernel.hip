@@ -206,44 +206,43 @@ RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
   col_store(b, w);
 }
 
-// A new pixel: key from the RNG contract seed, block 0 (shared by the main stream and the jitter of
-// samples 0-3, render.rs:74-82) generated once into both caches and into registers.
-RPK_INLINE void rng_begin_pixel(Rng& r, RngBlk& b, uint64_t seed) {
-  DREG(DREG_BEGIN_PIXEL)
-  uint32_t k[8], w[16];
-  seed_key(seed, k);
-  store_key(r, k);
-  chacha12(k, 0, w);
-  b.blk = 0;
-  store_block(ring_slot(r, 0), w);
-  store_block(jit_slot(r, 0), w);
-  col_store(b, w);
-  r.pos = 0;
-  *r.end = 1;
-  r.jtag[0] = 0;
-  r.jtag[BLOCK] = 0xFFFFFFFFu;
-}
-
-// The refill pass (wave-uniform call site).  `s` is the lane's in-flight sample, whose jitter is
-// already consumed; samples s+1.. need jitter blocks (s+1)/4 and the one after.
-RPK_INLINE void rng_refill(Rng& r, bool alive, uint32_t s, uint32_t spp) {
+// The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
+// samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
+// round, not started) gets its key from the unit's seed and keystream block 0 here, batched with the other
+// lanes' ChaCha work -- at the fetch site the whole wave paid a ChaCha block for each fetching lane.
+RPK_INLINE void rng_refill(Rng& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
   const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
   const uint32_t b1 = (s + 1) >> 2, b2 = b1 + 1;
-  const bool j1 = alive && 4 * b1 < spp && r.jtag[(b1 & 1u) * BLOCK] != b1;
-  const bool j2 = alive && 4 * b2 < spp && r.jtag[(b2 & 1u) * BLOCK] != b2;
-  const bool crit = alive && have <= RNG_CRIT;
-  const bool room = alive && (have < RING || j1 || j2);
+  const bool j1 = alive && !fresh && 4 * b1 < spp && r.jtag[(b1 & 1u) * BLOCK] != b1;
+  const bool j2 = alive && !fresh && 4 * b2 < spp && r.jtag[(b2 & 1u) * BLOCK] != b2;
+  const bool crit = alive && (fresh || have <= RNG_CRIT);
+  const bool room = alive && (fresh || have < RING || j1 || j2);
   if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
   if (room) {
     DREG(DREG_REFILL)
-    const bool main = crit || !(j1 || j2);
-    const uint32_t b = main ? end : (j1 ? b1 : b2);
+    const bool main = fresh || crit || !(j1 || j2);
+    const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
     uint32_t k[8], w[16];
-    load_key(r, k);
+    if (fresh) {
+      DREG(DREG_BEGIN_PIXEL)
+      seed_key(seed, k);
+      store_key(r, k);
+    } else {
+      load_key(r, k);
+    }
     chacha12(k, b, w);
     store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);
-    if (main) *r.end = end + 1;
-    else r.jtag[(b & 1u) * BLOCK] = b;
+    if (fresh) {  // block 0 is also the jitter block of samples 0-3 (render.rs:74-82)
+      store_block(jit_slot(r, 0), w);
+      r.pos = 0;
+      *r.end = 1;
+      r.jtag[0] = 0;
+      r.jtag[BLOCK] = 0xFFFFFFFFu;
+    } else if (main) {
+      *r.end = end + 1;
+    } else {
+      r.jtag[(b & 1u) * BLOCK] = b;
+    }
   }
 }
 
@@ -1019,15 +1018,9 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
   pipj = pi | (pj << 16);
   bool tdone = true;  // traversal of the current ray finished (or no ray)
-  if (alive) {
-    KArgsPtr A = kargs();
-    RngBlk rb(stk);
-    rng_begin_pixel(rng, rb, unit_seed(A, pi, pj, batch));  // RNG contract
-    start_sample(rng, rb, 0, pi, pj, o, d);
-    depth = A->P.max_bounce;
-    trav_init(load_scene(A), INF, ts);
-    tdone = false;
-  }
+  // Camera samples start at the top of the next round, after the refill pass: `start` = sample s is due,
+  // `fresh` = and it is the first of a unit whose key and block 0 the refill pass makes.
+  bool start = alive, fresh = alive;
   DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
 
   // Every lane of the wave stays in this loop until the whole wave has retired, so the ballots below
@@ -1038,7 +1031,23 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   for (;;) {
     DIAG(iters++;)
     DREG(DREG_ROUND)
-    rng_refill(rng, alive, s, unit_spp(kargs(), batch));
+    {
+      KArgsPtr A = kargs();
+      const uint64_t seed = fresh ? unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch) : 0ull;  // RNG contract
+      rng_refill(rng, alive, fresh, seed, start ? s - 1 : s, unit_spp(A, batch));
+    }
+    if (start) {
+      KArgsPtr A = kargs();
+      RngBlk rb(stk);
+      rng_load(rng, rb);
+      start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
+      depth = A->P.max_bounce;
+      T_x = T_y = T_z = 1.0;
+      first = true;
+      trav_init(load_scene(A), INF, ts);
+      tdone = false;
+      start = fresh = false;
+    }
     DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
     {
       KArgsPtr A = kargs();
@@ -1222,25 +1231,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           DIAG(if (!alive) t_retire = __builtin_amdgcn_s_memrealtime();)
           DIAG(if (!PROBE && !alive) atomicMax(&A->diag[11], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
           if (alive) {
-            A = kargs();
-            RngBlk rb0(stk);
-            rng_begin_pixel(rng, rb0, unit_seed(A, pi, pj, batch));
+            fresh = true;
             s = 0;
             hits = 0;
             sum_x = sum_y = sum_z = 0.0;
           }
         }
-        if (alive) {
-          RngBlk rb(stk);
-          rng_load(rng, rb);
-          start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
-          A = kargs();
-          depth = A->P.max_bounce;
-          T_x = T_y = T_z = 1.0;
-          first = true;
-        }
-      }
-      if (alive) {
+        start = alive;  // next round, after the refill pass
+      } else {
         trav_init(load_scene(kargs()), INF, ts);
         tdone = false;
       }
