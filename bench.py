@@ -7,8 +7,11 @@
 One step = one frame of the config (1920x1080x256 spp bunny scene with full materials by default),
 tile-sharded across the N ranks (tile t -> rank t % N, strong scaling: the frame is fixed), rendered
 by the persistent HIP kernel (librp.so) from scene data resident in HBM, followed by the RCCL
-all-gather of the framebuffer and the device-side de-interleave into frame order.  The timed region is
-K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is used.
+all-gather of the framebuffer and the device-side de-interleave into frame order.  With N > 1 two frames
+are in flight (frame k renders on stream k % 2 with its own rp_workspace), so the end of one frame -- its
+last units leave most of a small shard's GPU idle -- overlaps the start of the next (--inflight).  The
+timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over
+ranks is used.
 
 Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays /
 time.  roofline: algorithmic bytes per launch (the reference traversal's per-ray event counts,
@@ -84,6 +87,9 @@ def main():
     ap.add_argument("--cpu-spp", type=int, default=4)
     ap.add_argument("--cpu-workers", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight: consecutive frames alternate over this many streams and workspaces "
+                         "(0 = 1 on one GPU, 2 on several)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,18 +116,38 @@ def main():
     log(f"[rank {rank}] scene ready in {time.time() - t:.2f}s: {info}")
     sp = shard_params(params, rank, world)
     asm = FrameAssembler(params, world, dev)
-    buf = asm.new_shard_buffer()
-    ctr = torch.zeros(8, dtype=torch.int64, device=dev)
+    # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the
+    # end of one frame (its last units leave most of the GPU idle) overlaps the start of the next; the
+    # frame assembly (RCCL all-gather + scatter) runs on the main stream in frame order.  F = 1 is the
+    # plain sequential loop.
+    F = args.inflight if args.inflight > 0 else (1 if world == 1 else 2)
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [main_stream] if F == 1 else [torch.cuda.Stream(dev) for _ in range(F)]
+    wss = [None] + [ds.workspace() for _ in range(F - 1)]
+    bufs = [asm.new_shard_buffer() for _ in range(F)]
+    ctrs = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(F)]
+    freed = [None] * F  # event: the assembly of the buffer's previous frame is done
     frame = torch.zeros(params.height * params.width, 3, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    state = {"k": 0}
 
     def step(k_start=None, k_end=None):
+        i = state["k"] % F
+        state["k"] += 1
+        st = streams[i]
+        if freed[i] is not None:
+            st.wait_event(freed[i])
         if k_start is not None:
-            k_start.record(stream)
-        ds.render_device(sp, buf, ctr, stream=stream)
+            k_start.record(st)
+        ds.render_device(sp, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         if k_end is not None:
-            k_end.record(stream)
-        asm.gather(buf, out=frame)
+            k_end.record(st)
+        if st is not main_stream:
+            done = torch.cuda.Event()
+            done.record(st)
+            main_stream.wait_event(done)
+        asm.gather(bufs[i], out=frame)
+        freed[i] = torch.cuda.Event()
+        freed[i].record(main_stream)
 
     for w in range(args.warmup):
         step()
@@ -140,7 +166,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps / 1e3
-    c = ctr.cpu().tolist()
+    if F > 1:
+        # overlapping frames: a frame's events also span the neighbour frames' work, so the kernel rate is
+        # priced on the per-frame throughput time instead
+        kernel_s = elapsed / args.steps
+    c = ctrs[0].cpu().tolist()
     rays_step, samples_step, status = c[0], c[1], c[3]
     if status != 0:
         raise RuntimeError(f"render kernel reported status {status}")
@@ -168,6 +198,7 @@ def main():
                        "width": params.width, "height": params.height, "spp": params.spp,
                        "max_bounce": params.max_bounce, "seed": params.seed,
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather" if world > 1 else "1 GPU",
+                       "frames_in_flight": F,
                        "rays_per_frame": int(total_rays_step), "rays_per_sample": total_rays_step / total_samples_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

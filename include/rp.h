@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 2
+#define RP_ABI_VERSION 3
 
 /* Samples per RNG stream (see "Determinism" above). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -173,6 +173,7 @@ typedef struct rp_stats {
 } rp_stats;
 
 typedef struct rp_scene rp_scene;   /* opaque: device-resident scene + acceleration structure */
+typedef struct rp_workspace rp_workspace;  /* opaque: per-frame device state of a render (see below) */
 
 /* Library / device queries. */
 int rp_abi_version(void);
@@ -204,11 +205,24 @@ int rp_render(rp_scene* scene, const rp_camera* camera, const rp_render_params* 
  * device.  d_shard_rgb: shard_pixel_count*3 doubles in device memory, compact shard order.
  * d_shard_fg (nullable): shard_pixel_count floats.  d_counters (nullable): 4 uint64 in device memory
  * that receive {rays, samples, pixels, status}; they are zeroed on the stream before the launch.
- * No host synchronisation or copy happens inside.  A frame with spp > RP_SAMPLES_PER_STREAM uses a
- * scene-owned workspace (3 doubles + 1 uint32 per pixel and batch) allocated by the first call that
- * needs it: render once before capturing such calls into a hipGraph. */
+ * No host synchronisation or copy happens inside.  A frame with spp > RP_SAMPLES_PER_STREAM needs
+ * 3 doubles + 1 uint32 per pixel and batch of workspace memory, allocated by the first call that needs
+ * it: render once before capturing such calls into a hipGraph. */
 int rp_render_device(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
                      double* d_shard_rgb, float* d_shard_fg, uint64_t* d_counters, void* stream);
+
+/* Frames in flight.  A render's per-frame device state -- the keystream cache of the resident lanes,
+ * the unit-queue counters, the cost-probe and tile-order buffers, the multi-batch sums -- lives in a
+ * workspace.  The scene owns one, which rp_render and rp_render_device use (their frames must therefore
+ * be ordered on one stream).  Frames rendered with different workspaces may run concurrently on
+ * different streams: the end of one frame, when its last units leave most of the GPU idle, then
+ * overlaps the start of the next.  A workspace serves one frame at a time (the caller orders its reuse
+ * on streams); destroy workspaces before their scene.  Same arguments and results as rp_render_device. */
+int rp_workspace_create(rp_scene* scene, rp_workspace** out);
+void rp_workspace_destroy(rp_workspace* workspace);
+int rp_render_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
+                        const rp_render_params* params, double* d_shard_rgb, float* d_shard_fg,
+                        uint64_t* d_counters, void* stream);
 
 /* Closest-hit query (Hittable::hit on the root, hittable.rs:18 / bvh.rs:121) for n rays, synchronous,
  * host buffers.  rays: n * 8 doubles {origin xyz, direction xyz, t_min, t_max} (utility.rs:52-57).

@@ -57,6 +57,20 @@ int upload(const std::vector<T>& v, T** out) {
 
 }  // namespace
 
+// Per-frame device state of a render (include/rp.h rp_workspace): frames with different workspaces may
+// run concurrently on different streams.
+struct rp_workspace {
+  rp_scene* scene = nullptr;
+  uint64_t* d_ctr = nullptr;         // default counter block (CTR_N x u64)
+  uint64_t* d_probe_ctr = nullptr;   // counter block of the probe launch
+  uint32_t* d_tile_cost = nullptr;   // cost probe output, 2 x rpk::TILE_SORT_MAX entries
+  uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
+  uint32_t* d_slab = nullptr;        // keystream cache, one slab per resident render lane
+  double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames (grown on demand)
+  uint32_t* d_partial_hits = nullptr;
+  uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
+};
+
 struct rp_scene {
   int device = 0;
   rpk::KScene ks{};
@@ -68,15 +82,9 @@ struct rp_scene {
   rpl::Material* d_mats = nullptr;
   rpl::Texture* d_texs = nullptr;
   uint32_t* d_texels = nullptr;
-  uint64_t* d_ws = nullptr;  // default counter block (8 x u64)
   uint64_t* d_diag = nullptr;  // diagnostic counters (rpk::DIAG_N)
-  uint32_t* d_slab = nullptr;  // keystream cache, one slab per resident render lane
-  uint32_t* d_tile_cost = nullptr;   // cost probe output, rpk::TILE_SORT_MAX entries
-  double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames (grown on demand)
-  uint32_t* d_partial_hits = nullptr;
-  uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
-  uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
-  uint64_t* d_probe_ctr = nullptr;   // counter block of the probe launch
+  rp_workspace ws0;            // the scene's own workspace (rp_render, rp_render_device)
+  int n_workspaces = 0;        // live workspaces from rp_workspace_create
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
   uint32_t max_depth = 0;
   int num_cu = 0;
@@ -84,6 +92,30 @@ struct rp_scene {
 };
 
 namespace {
+
+void ws_release(rp_workspace* w) {
+  for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_tile_cost, (void*)w->d_tile_order,
+                  (void*)w->d_slab, (void*)w->d_partial, (void*)w->d_partial_hits})
+    if (p) (void)hipFree(p);
+  *w = rp_workspace{};
+}
+
+// Allocate a workspace for scene s (current device = the scene's): counters, probe/sort buffers and a
+// keystream slab for every lane the render grid can hold resident.
+int ws_alloc(rp_scene* s, rp_workspace* w) {
+  *w = rp_workspace{};
+  w->scene = s;
+  const uint64_t lanes = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu * rpk::RENDER_BLOCK;
+  if (hipMalloc(reinterpret_cast<void**>(&w->d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&w->d_probe_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&w->d_tile_cost), sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&w->d_tile_order), sizeof(uint32_t) * rpk::TILE_SORT_MAX) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess) {
+    ws_release(w);
+    return fail(RP_ENOMEM, "hipMalloc render workspace");
+  }
+  return RP_OK;
+}
 
 struct Tiling {
   uint32_t tw, th, shards, shard, tiles_x, tiles_y, n_tiles, n_shard_tiles;
@@ -152,10 +184,9 @@ int rp_device_count(int* count) {
 void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
+  ws_release(&s->ws0);
   for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_prim_refs, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
-                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_ws, (void*)s->d_diag, (void*)s->d_slab,
-                  (void*)s->d_tile_cost, (void*)s->d_tile_order, (void*)s->d_probe_ctr, (void*)s->d_partial,
-                  (void*)s->d_partial_hits})
+                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_diag})
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -193,11 +224,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
       (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
     return bail(rc);
-  if (hipMalloc(reinterpret_cast<void**>(&s->d_ws), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&s->d_probe_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&s->d_tile_cost), sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&s->d_tile_order), sizeof(uint32_t) * rpk::TILE_SORT_MAX) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&s->d_diag), sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess ||
+  if (hipMalloc(reinterpret_cast<void**>(&s->d_diag), sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess ||
       hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
     return bail(fail(RP_ENOMEM, "hipMalloc workspace"));
   s->ks.diag = s->d_diag;
@@ -226,10 +253,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   int bpc = 0;
   if (rpk::render_blocks_per_cu(s->ks.stack_depth, &bpc) != 0 || bpc < 1) bpc = 1;
   s->blocks_per_cu = bpc;
-  const uint64_t lanes = (uint64_t)s->num_cu * (uint64_t)bpc * rpk::RENDER_BLOCK;
-  if (hipMalloc(reinterpret_cast<void**>(&s->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess)
-    return bail(fail(RP_ENOMEM, "hipMalloc keystream cache"));
-  s->ks.rng_slab = s->d_slab;
+  if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);
   *out = s;
   return RP_OK;
 }
@@ -278,15 +302,47 @@ int rp_shard_unpack(const rp_render_params* p, const double* shard_buf, uint32_t
   return RP_OK;
 }
 
+int rp_workspace_create(rp_scene* s, rp_workspace** out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  DeviceGuard g(s->device);
+  rp_workspace* w = new rp_workspace();
+  int rc = ws_alloc(s, w);
+  if (rc) {
+    delete w;
+    return rc;
+  }
+  s->n_workspaces++;
+  *out = w;
+  return RP_OK;
+}
+
+void rp_workspace_destroy(rp_workspace* w) {
+  if (!w || !w->scene) return;
+  rp_scene* s = w->scene;
+  DeviceGuard g(s->device);
+  ws_release(w);
+  s->n_workspaces--;
+  delete w;
+}
+
 int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* d_rgb, float* d_fg,
                      uint64_t* d_counters, void* stream) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  return rp_render_device_ws(s, &s->ws0, cam, p, d_rgb, d_fg, d_counters, stream);
+}
+
+int rp_render_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
+                        float* d_fg, uint64_t* d_counters, void* stream) {
   if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
+  if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
   if (p->max_bounce < 1) return fail(RP_EINVAL, "max_bounce must be >= 1 (render.rs:97 assert!(depth >= 1))");
   DeviceGuard g(s->device);
-  uint64_t* ctr = d_counters ? d_counters : s->d_ws;
+  uint64_t* ctr = d_counters ? d_counters : w->d_ctr;
   hipStream_t st = (hipStream_t)stream;
   RP_HIP(hipMemsetAsync(ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
   if (t.n_slots == 0) return RP_OK;
@@ -324,21 +380,23 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
   kp.n_queue = t.n_slots * kp.nbatch;
   if (kp.n_queue >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units)");
   if (kp.nbatch > 1) {
-    if (kp.n_queue > s->partial_units) {  // scene-owned workspace, grown on the first call that needs it
-      if (s->d_partial) (void)hipFree(s->d_partial);
-      if (s->d_partial_hits) (void)hipFree(s->d_partial_hits);
-      s->d_partial = nullptr;
-      s->d_partial_hits = nullptr;
-      s->partial_units = 0;
-      if (hipMalloc(reinterpret_cast<void**>(&s->d_partial), sizeof(double) * 3 * kp.n_queue) != hipSuccess ||
-          hipMalloc(reinterpret_cast<void**>(&s->d_partial_hits), sizeof(uint32_t) * kp.n_queue) != hipSuccess)
+    if (kp.n_queue > w->partial_units) {  // workspace-owned, grown on the first call that needs it
+      if (w->d_partial) (void)hipFree(w->d_partial);
+      if (w->d_partial_hits) (void)hipFree(w->d_partial_hits);
+      w->d_partial = nullptr;
+      w->d_partial_hits = nullptr;
+      w->partial_units = 0;
+      if (hipMalloc(reinterpret_cast<void**>(&w->d_partial), sizeof(double) * 3 * kp.n_queue) != hipSuccess ||
+          hipMalloc(reinterpret_cast<void**>(&w->d_partial_hits), sizeof(uint32_t) * kp.n_queue) != hipSuccess)
         return fail(RP_ENOMEM, "hipMalloc sample-batch workspace");
-      s->partial_units = kp.n_queue;
+      w->partial_units = kp.n_queue;
     }
-    kp.partial = s->d_partial;
-    kp.partial_hits = s->d_partial_hits;
+    kp.partial = w->d_partial;
+    kp.partial_hits = w->d_partial_hits;
   }
   const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
+  rpk::KScene ks = s->ks;
+  ks.rng_slab = w->d_slab;
   auto grid_for = [&](uint64_t slots) {
     const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
     return (int)std::max<uint64_t>(1, std::min(want, resident));
@@ -358,16 +416,16 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
     pk.nbatch = 1;
     pk.spp_batch = 1;
     pk.n_queue = pk.n_slots;
-    pk.tile_cost = s->d_tile_cost;
-    RP_HIP(hipMemsetAsync(s->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
-    RP_HIP(hipMemsetAsync(s->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
-    int e = rpk::launch_render(s->ks, pk, d_rgb, nullptr, s->d_probe_ctr, grid_for(pk.n_slots), stream);
+    pk.tile_cost = w->d_tile_cost;
+    RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+    RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
+    int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, grid_for(pk.n_slots), stream);
     if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
-    e = rpk::launch_tile_sort(s->d_tile_cost, t.n_shard_tiles, pk.probe_px, s->d_tile_order, stream);
+    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
-    kp.tile_order = s->d_tile_order;
+    kp.tile_order = w->d_tile_order;
   }
-  int e = rpk::launch_render(s->ks, kp, d_rgb, d_fg, ctr, grid_for(kp.n_queue), stream);
+  int e = rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, grid_for(kp.n_queue), stream);
   if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
   if (kp.nbatch > 1) {
     e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);

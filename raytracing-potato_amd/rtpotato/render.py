@@ -33,9 +33,18 @@ class DeviceScene:
                 "device_bytes": nb.value}
 
     def close(self) -> None:
+        for w in list(getattr(self, "_workspaces", ())):
+            w.close()
         if getattr(self, "handle", None):
             F.rp().rp_scene_destroy(self.handle)
             self.handle = None
+
+    def workspace(self) -> "Workspace":
+        """A second (third, ...) per-frame workspace: frames rendered with different workspaces may run
+        concurrently on different streams (rp_workspace_create)."""
+        w = Workspace(self)
+        self.__dict__.setdefault("_workspaces", []).append(w)
+        return w
 
     def __del__(self):
         try:
@@ -63,18 +72,26 @@ class DeviceScene:
         return rgb, fg, {"rays": st.rays, "samples": st.samples, "pixels": st.pixels, "seconds": st.seconds}
 
     # ---- asynchronous device render (torch tensors, torch's current stream) ------------------------
-    def render_device(self, params: RenderParams, out, counters, fg=None, camera=None, stream=None) -> None:
+    def render_device(self, params: RenderParams, out, counters, fg=None, camera=None, stream=None,
+                      workspace: "Workspace | None" = None) -> None:
         """Render the shard into `out` (torch f64 tensor, >= shard_slot_count*3 elements) on `stream`
-        (torch stream; default: current).  counters: torch int64 tensor of 8 elements."""
+        (torch stream; default: current).  counters: torch int64 tensor of 8 elements.  workspace: one
+        from self.workspace() (default: the scene's own, rp_render_device)."""
         import torch
         cam = (camera or self.scene.camera).to_c()
         p = params.to_c()
         assert out.dtype == torch.float64 and out.is_cuda and out.numel() >= 3 * shard_slot_count(params)
         assert counters.dtype == torch.int64 and counters.numel() >= F.RP_COUNTERS_LEN
         s = stream if stream is not None else torch.cuda.current_stream(out.device)
-        F.check(F.rp().rp_render_device(self.handle, ctypes.byref(cam), ctypes.byref(p), out.data_ptr(),
-                                        fg.data_ptr() if fg is not None else None, counters.data_ptr(),
-                                        ctypes.c_void_p(s.cuda_stream)))
+        fgp = fg.data_ptr() if fg is not None else None
+        if workspace is None:
+            F.check(F.rp().rp_render_device(self.handle, ctypes.byref(cam), ctypes.byref(p), out.data_ptr(), fgp,
+                                            counters.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+        else:
+            assert workspace.scene is self and workspace.handle
+            F.check(F.rp().rp_render_device_ws(self.handle, workspace.handle, ctypes.byref(cam), ctypes.byref(p),
+                                               out.data_ptr(), fgp, counters.data_ptr(),
+                                               ctypes.c_void_p(s.cuda_stream)))
 
     def intersect(self, rays: np.ndarray):
         """Hittable::hit on the root for (n, 8) rays -> ((n, 9) hits, (n,) material ids)."""
@@ -83,6 +100,24 @@ class DeviceScene:
         mats = np.empty(len(r), dtype=np.uint32)
         F.check(F.rp().rp_intersect(self.handle, r.ctypes.data, len(r), hits.ctypes.data, mats.ctypes.data))
         return hits, mats
+
+
+class Workspace:
+    """rp_workspace: per-frame device state (keystream cache, queue counters, probe buffers, batch sums)."""
+
+    def __init__(self, scene: DeviceScene):
+        h = ctypes.c_void_p()
+        F.check(F.rp().rp_workspace_create(scene.handle, ctypes.byref(h)))
+        self.scene = scene
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            F.rp().rp_workspace_destroy(self.handle)
+            self.handle = None
+            ws = self.scene.__dict__.get("_workspaces", [])
+            if self in ws:
+                ws.remove(self)
 
 
 def unpack_shard(params: RenderParams, shard_buf: np.ndarray, channels: int = 3,

@@ -246,3 +246,28 @@ def test_c3_full_size_sampled_parity(gpu):
     assert st["pixels"] == params.width * params.height
     # size-independent property: rays per sample of the whole frame vs the sampled shard
     assert abs(st["rays"] / st["samples"] - ctr["rays"] / ctr["samples"]) < 0.25
+
+
+def test_workspaces_frames_in_flight(gpu):
+    """rp_render_device_ws: frames with two workspaces on two streams at once (70 spp, so the batch sums
+    live in the workspaces as well) equal the scene-workspace frame bit for bit, with the same ray count."""
+    import torch
+    from rtpotato.scene import shard_slot_count
+    scene, params = _scene("bunny_full", 64, 40, 70)
+    n = shard_slot_count(params)
+    with gpu.DeviceScene(scene) as ds:
+        ref = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+        c0 = torch.zeros(8, dtype=torch.int64, device="cuda")
+        ds.render_device(params, ref, c0)
+        torch.cuda.synchronize()
+        wss = [ds.workspace(), ds.workspace()]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        outs = [torch.zeros_like(ref) for _ in range(4)]
+        ctrs = [torch.zeros_like(c0) for _ in range(4)]
+        for k in range(4):  # frames k and k + 2 share a workspace and its stream
+            ds.render_device(params, outs[k], ctrs[k], stream=streams[k % 2], workspace=wss[k % 2])
+        torch.cuda.synchronize()
+        for k in range(4):
+            assert torch.equal(outs[k], ref)
+            assert int(ctrs[k][0]) == int(c0[0]) and int(ctrs[k][3]) == 0
+        wss[0].close()  # explicit destroy before the scene; the other one is destroyed with the scene

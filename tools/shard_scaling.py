@@ -19,13 +19,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--tile", type=int, default=0, help="square tile size (default: the config's)")
     a = ap.parse_args()
     from rtpotato import scenes
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
+    if a.tile:
+        params = replace(params, tile_w=a.tile, tile_h=a.tile)
     ds = DeviceScene(scene)
     ds.render(replace(params, spp=4))  # warm
-    out = {"config": a.config, "per_n": {}}
+    out = {"config": a.config, "tile": [params.tile_w, params.tile_h], "per_n": {}}
     t1 = None
     for n in [int(x) for x in a.ns.split(",")]:
         times, rays = [], 0
