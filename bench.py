@@ -7,7 +7,8 @@
 One step = one frame of the config (1920x1080x256 spp bunny scene with full materials by default),
 tile-sharded across the N ranks (tile t -> rank t % N, strong scaling: the frame is fixed), rendered
 by the persistent HIP kernel (librp.so) from scene data resident in HBM, followed by the RCCL
-all-gather of the framebuffer and the device-side de-interleave into frame order.  With N > 1 two frames
+output stage (to_srgb_u8 -> B, G, R, A bytes, rp_shard_to_bgra8), the RCCL all-gather of those 4 bytes
+per pixel and the device-side de-interleave into frame order (the body of the reference's output.tga).  With N > 1 two frames
 are in flight (frame k renders on stream k % 2 with its own rp_workspace), so the end of one frame -- its
 last units leave most of a small shard's GPU idle -- overlaps the start of the next (--inflight).  The
 timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over
@@ -125,9 +126,10 @@ def main():
     streams = [main_stream] if F == 1 else [torch.cuda.Stream(dev) for _ in range(F)]
     wss = [None] + [ds.workspace() for _ in range(F - 1)]
     bufs = [asm.new_shard_buffer() for _ in range(F)]
+    bgras = [asm.new_bgra_buffer() for _ in range(F)]
     ctrs = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(F)]
     freed = [None] * F  # event: the assembly of the buffer's previous frame is done
-    frame = torch.zeros(params.height * params.width, 3, dtype=torch.float64, device=dev)
+    frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
     def step(k_start=None, k_end=None):
@@ -141,11 +143,12 @@ def main():
         ds.render_device(sp, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         if k_end is not None:
             k_end.record(st)
+        ds.to_bgra8(sp, bufs[i], bgras[i], stream=st)  # output stage: to_srgb_u8 bytes in TGA order
         if st is not main_stream:
             done = torch.cuda.Event()
             done.record(st)
             main_stream.wait_event(done)
-        asm.gather(bufs[i], out=frame)
+        asm.gather_bgra(bgras[i], out=frame)
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 
@@ -199,6 +202,7 @@ def main():
                        "max_bounce": params.max_bounce, "seed": params.seed,
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather" if world > 1 else "1 GPU",
                        "frames_in_flight": F,
+                       "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(total_rays_step), "rays_per_sample": total_rays_step / total_samples_step},
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,

@@ -224,6 +224,18 @@ int rp_render_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camer
                         const rp_render_params* params, double* d_shard_rgb, float* d_shard_fg,
                         uint64_t* d_counters, void* stream);
 
+/* Output stage on the device: the reference's to_srgb_u8 (utility.rs:212-220, alpha 255) of every slot of
+ * a compact shard buffer, bytes in tga::save's pixel order B, G, R, A (image.rs:116-137), so a gathered
+ * and de-interleaved frame is the body of the reference's output.tga (18-byte header: rph_tga_save).
+ * d_shard_bgra: shard_pixel_count * 4 bytes, 4-byte aligned.  Asynchronous on `stream`.  Bytes are
+ * identical to to_srgb_u8 evaluated with the host libm's pow: the device looks x up in the 255
+ * thresholds of that step function (rp_srgb_thresholds), it evaluates no pow of its own. */
+int rp_shard_to_bgra8(rp_scene* scene, const rp_render_params* params, const double* d_shard_rgb,
+                      uint8_t* d_shard_bgra, void* stream);
+/* The threshold table of rp_shard_to_bgra8: out[k] (k = 1..255) is the smallest x whose to_srgb_u8 byte
+ * is >= k; out[0] = -inf.  256 doubles.  Host only (no device needed). */
+int rp_srgb_thresholds(double* out);
+
 /* Closest-hit query (Hittable::hit on the root, hittable.rs:18 / bvh.rs:121) for n rays, synchronous,
  * host buffers.  rays: n * 8 doubles {origin xyz, direction xyz, t_min, t_max} (utility.rs:52-57).
  * out_hit: n * 9 doubles {t, position xyz, normal xyz, u, v} (utility.rs:84-89), t = +inf on a miss.

@@ -161,9 +161,59 @@ bool tile_order_enabled() {
   return v;
 }
 
+// to_srgb_u8's byte for one channel (utility.rs:212-216), in the host libm: the reference's arithmetic
+// (Rust's f64::powf is the platform pow).  Same expression as rph_to_srgb_u8 (rp_host.cpp).
+uint32_t srgb_byte(double x) {
+  if (x < 0.0) x = 0.0;
+  if (x > 1.0) x = 1.0;
+  const double y = 255.0 * std::pow(x, 1.0 / 2.2);
+  return !(y > 0.0) ? 0u : (y >= 255.0 ? 255u : (uint32_t)y);
+}
+
+// thr[k] = the smallest double x in [0, 1] with srgb_byte(x) >= k (bisection over the bit patterns of
+// non-negative doubles, which order like their values); computed once.
+const rpk::SrgbTable& srgb_table() {
+  static const rpk::SrgbTable tab = [] {
+    rpk::SrgbTable t{};
+    t.thr[0] = -HUGE_VAL;
+    for (uint32_t k = 1; k < 256; k++) {
+      uint64_t lo = 0, hi = 0x3FF0000000000000ull;  // srgb_byte(0) = 0 < k <= 255 = srgb_byte(1)
+      while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        double x;
+        std::memcpy(&x, &mid, sizeof x);
+        if (srgb_byte(x) >= k) hi = mid;
+        else lo = mid;
+      }
+      std::memcpy(&t.thr[k], &hi, sizeof hi);
+    }
+    return t;
+  }();
+  return tab;
+}
+
 }  // namespace
 
 extern "C" {
+
+int rp_srgb_thresholds(double* out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  std::memcpy(out, srgb_table().thr, sizeof(double) * 256);
+  return RP_OK;
+}
+
+int rp_shard_to_bgra8(rp_scene* s, const rp_render_params* p, const double* d_shard_rgb, uint8_t* d_shard_bgra,
+                      void* stream) {
+  if (!s || !d_shard_rgb || !d_shard_bgra) return fail(RP_EINVAL, "scene and buffers must be non-NULL");
+  if (reinterpret_cast<uintptr_t>(d_shard_bgra) % 4 != 0) return fail(RP_EINVAL, "d_shard_bgra must be 4-byte aligned");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  DeviceGuard g(s->device);
+  int e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, t.n_slots, d_shard_bgra, stream);
+  if (e != 0) return fail(RP_EHIP, std::string("output stage launch: ") + hipGetErrorString((hipError_t)e));
+  return RP_OK;
+}
 
 int rp_abi_version(void) { return RP_ABI_VERSION; }
 

@@ -100,6 +100,13 @@ int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32
 // Final pass of a multi-batch frame: per shard slot, the batch sums added in batch order, / spp.
 int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void* stream);
 
+// Output stage: thresholds of to_srgb_u8 (thr[k] = smallest x whose byte is >= k, k = 1..255; thr[0] unused)
+// and the launch converting n slots of linear f64 RGB into B, G, R, 255 bytes (4-byte aligned output).
+struct SrgbTable {
+  double thr[256];
+};
+int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_t* bgra, void* stream);
+
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t stack_depth, int* blocks);
 

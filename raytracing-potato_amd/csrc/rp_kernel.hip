@@ -1360,6 +1360,40 @@ int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void
   return (int)hipGetLastError();
 }
 
+// Output stage (utility.rs:212-220 to_srgb_u8, image.rs:116-137 tga::save pixel order): per shard slot,
+// linear f64 RGB -> B, G, R, 255 bytes.  `(255 * clamp(x, 0, 1).powf(1/2.2)) as u8` is a monotone step
+// function of x, so the byte is the number of its 255 thresholds (the smallest x reaching 1, 2, ..., 255,
+// found on the host with the host libm's pow -- the reference's own arithmetic) that x reaches: an 8-step
+// binary search in an LDS copy of the table, no device pow, bit-identical by construction.  NaN reaches
+// no threshold (Rust's saturating `as u8` maps NaN to 0), values above 1 reach all 255.
+__global__ void __launch_bounds__(256) srgb_bgra_kernel(const SrgbTable tab, const double* __restrict__ rgb,
+                                                       uint64_t n, uint32_t* __restrict__ bgra) {
+  __shared__ double thr[256];
+  thr[threadIdx.x] = tab.thr[threadIdx.x];
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    uint32_t px = 0xff000000u;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const double x = rgb[3 * i + c];
+      uint32_t k = 0;
+#pragma unroll
+      for (uint32_t step = 128; step; step >>= 1)
+        if (x >= thr[k + step]) k += step;
+      px |= k << (8 * (2 - c));  // byte 0 = B, 1 = G, 2 = R, 3 = A
+    }
+    bgra[i] = px;
+  }
+}
+
+int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_t* bgra, void* stream) {
+  if (n == 0) return 0;
+  const uint64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
+  hipLaunchKernelGGL(srgb_bgra_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, tab, rgb, n,
+                     reinterpret_cast<uint32_t*>(bgra));
+  return (int)hipGetLastError();
+}
+
 // Bitonic sort of the probed tiles in LDS, one block: key = inverted (longest sample: 4 bits, mean rays per
 // probed pixel x 16: 14 bits) << 14 | k, so an ascending sort orders by descending cost, ties by shard
 // tile index.  Padding keys sort last.

@@ -106,7 +106,7 @@ _host = None
 RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_create", "rp_scene_destroy",
               "rp_scene_info", "rp_shard_pixel_count", "rp_shard_unpack", "rp_render", "rp_render_device",
               "rp_intersect", "rp_diagnostics", "rp_workspace_create", "rp_workspace_destroy",
-              "rp_render_device_ws"]
+              "rp_render_device_ws", "rp_shard_to_bgra8", "rp_srgb_thresholds"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_last_error"]
 
@@ -152,6 +152,8 @@ def rp() -> ctypes.CDLL:
     lib.rp_workspace_destroy.restype = None
     lib.rp_render_device_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p,
                                         c_void_p, c_void_p, c_void_p]
+    lib.rp_shard_to_bgra8.argtypes = [c_void_p, POINTER(rp_render_params), c_void_p, c_void_p, c_void_p]
+    lib.rp_srgb_thresholds.argtypes = [c_void_p]
     lib.rp_intersect.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
     lib.rp_diagnostics.argtypes = [c_void_p, c_void_p, c_uint32, c_int]
     _rp = lib

@@ -63,3 +63,28 @@ class FrameAssembler:
             out = torch.zeros(p.height * p.width, 3, dtype=shard_buf.dtype, device=shard_buf.device)
         out.view(-1, 3)[self.dst] = gathered.view(-1, 3)[self.src]
         return out.view(p.height, p.width, 3)
+
+    def new_bgra_buffer(self):
+        import torch
+        return torch.zeros(4 * self.slots, dtype=torch.uint8, device=self.device)
+
+    def gather_bgra(self, shard_bgra, group=None, out=None):
+        """Like gather() for the output stage's bytes (DeviceScene.to_bgra8): 4 bytes per pixel instead of
+        24, moved and scattered as one int32 each; returns the (h, w, 4) B, G, R, A frame -- the body of
+        the reference's output.tga (rtpotato.render.tga_bytes)."""
+        import torch
+        import torch.distributed as dist
+        p = self.params
+        words = shard_bgra.view(torch.int32)
+        if self.world > 1:
+            gathered = torch.empty(self.world * self.slots, dtype=torch.int32, device=words.device)
+            if dist.get_backend(group) == "gloo":
+                dist.all_gather(list(gathered.view(self.world, -1).unbind(0)), words, group=group)
+            else:
+                dist.all_gather_into_tensor(gathered, words, group=group)
+        else:
+            gathered = words
+        if out is None:
+            out = torch.zeros(p.height * p.width * 4, dtype=torch.uint8, device=words.device)
+        out.view(torch.int32)[self.dst] = gathered[self.src]
+        return out.view(p.height, p.width, 4)

@@ -93,6 +93,18 @@ class DeviceScene:
                                                out.data_ptr(), fgp, counters.data_ptr(),
                                                ctypes.c_void_p(s.cuda_stream)))
 
+    def to_bgra8(self, params: RenderParams, shard_rgb, out, stream=None) -> None:
+        """Output stage on the device (rp_shard_to_bgra8): the shard's linear f64 RGB (`shard_rgb`, torch
+        f64) -> to_srgb_u8 bytes in TGA order B, G, R, A into `out` (torch uint8, >= 4 * slots)."""
+        import torch
+        n = shard_slot_count(params)
+        assert shard_rgb.dtype == torch.float64 and shard_rgb.is_cuda and shard_rgb.numel() >= 3 * n
+        assert out.dtype == torch.uint8 and out.is_cuda and out.numel() >= 4 * n
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        p = params.to_c()
+        F.check(F.rp().rp_shard_to_bgra8(self.handle, ctypes.byref(p), shard_rgb.data_ptr(), out.data_ptr(),
+                                         ctypes.c_void_p(s.cuda_stream)))
+
     def intersect(self, rays: np.ndarray):
         """Hittable::hit on the root for (n, 8) rays -> ((n, 9) hits, (n,) material ids)."""
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
@@ -129,6 +141,26 @@ def unpack_shard(params: RenderParams, shard_buf: np.ndarray, channels: int = 3,
     p = params.to_c()
     F.check(F.rp().rp_shard_unpack(ctypes.byref(p), src.ctypes.data, channels, frame.ctypes.data))
     return frame
+
+
+def srgb_thresholds() -> np.ndarray:
+    """The 256-entry threshold table of the device output stage (rp_srgb_thresholds; host only)."""
+    t = np.empty(256, dtype=np.float64)
+    F.check(F.rp().rp_srgb_thresholds(t.ctypes.data))
+    return t
+
+
+def tga_bytes(width: int, height: int, bgra) -> bytes:
+    """tga::save (image.rs:116-137): 18-byte header (uncompressed true colour, 32 bpp) + the frame's
+    B, G, R, A bytes in row order, row 0 = bottom -- the file rph_tga_save writes."""
+    hd = bytearray(18)
+    hd[2] = 2
+    hd[12:14] = int(width).to_bytes(2, "little")
+    hd[14:16] = int(height).to_bytes(2, "little")
+    hd[16] = 32
+    body = np.ascontiguousarray(bgra, dtype=np.uint8).reshape(-1)
+    assert body.size == 4 * width * height
+    return bytes(hd) + body.tobytes()
 
 
 def device_count() -> int:

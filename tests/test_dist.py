@@ -37,10 +37,19 @@ def _worker(rank, world, port, result_dir):
     b = buf.view(-1, 3)
     b[:len(pix)][torch.as_tensor(ok)] = torch.as_tensor(frame.reshape(-1, 3)[pix[ok]])
     out = asm.gather(buf)
+    # the output-stage bytes (B, G, R, A per slot, as rp_shard_to_bgra8 writes them) gather the same way
+    from rtpotato import _ffi as F
+    lin = np.ascontiguousarray(buf.numpy())
+    rgba = np.zeros((lin.size // 3, 4), dtype=np.uint8)
+    F.host().rph_to_srgb_u8(lin.ctypes.data, lin.size // 3, rgba.ctypes.data)
+    bgra = asm.new_bgra_buffer()
+    bgra.copy_(torch.as_tensor(rgba[:, [2, 1, 0, 3]].reshape(-1)))
+    out8 = asm.gather_bgra(bgra)
     rays = torch.tensor([ctr["rays"]], dtype=torch.int64)
     dist.all_reduce(rays)
     if rank == 0:
         np.save(os.path.join(result_dir, "frame.npy"), out.numpy())
+        np.save(os.path.join(result_dir, "frame8.npy"), out8.numpy())
         np.save(os.path.join(result_dir, "rays.npy"), rays.numpy())
     dist.destroy_process_group()
 
@@ -56,6 +65,10 @@ def test_gather_rebuilds_frame(tmp_path, world):
     ref, _, ctr = oracle_render(scene, RenderParams(75, 41, 2, 8, 77, 16, 16), threads=4)
     assert np.array_equal(got, ref)
     assert int(np.load(tmp_path / "rays.npy")[0]) == ctr["rays"]
+    from rtpotato import _ffi as F
+    rgba = np.zeros((41 * 75, 4), dtype=np.uint8)
+    F.host().rph_to_srgb_u8(np.ascontiguousarray(ref).ctypes.data, 41 * 75, rgba.ctypes.data)
+    assert np.array_equal(np.load(tmp_path / "frame8.npy").reshape(-1, 4), rgba[:, [2, 1, 0, 3]])
 
 
 def test_max_slots_and_shard_partition():
