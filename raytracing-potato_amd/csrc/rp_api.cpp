@@ -152,6 +152,19 @@ uint32_t trav_threshold() {
   return v;
 }
 
+// Acceleration-structure builder: the host binned SAH (rp_bvh.cpp, the better tree) unless the scene is
+// large enough for its single-threaded build to dominate setup, then the device LBVH (rp_bvh_gpu.hip).
+// RP_BVH_BUILDER=host|gpu forces one (read per scene).
+enum : uint32_t { GPU_BUILD_MIN_PRIMS = 1u << 20 };
+bool use_gpu_builder(uint32_t n_hittables) {
+  if (n_hittables < 2) return false;
+  if (const char* e = std::getenv("RP_BVH_BUILDER")) {
+    if (std::strcmp(e, "gpu") == 0) return true;
+    if (std::strcmp(e, "host") == 0) return false;
+  }
+  return n_hittables >= GPU_BUILD_MIN_PRIMS;
+}
+
 // Cost-ordered tile scheduling (rp_kernel.h); RP_TILE_ORDER=0 restores plain shard order (for A/B timing).
 bool tile_order_enabled() {
   static const bool v = [] {
@@ -257,6 +270,8 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
 
   rpb::PackedScene ps;
   rpb::BuildOptions opt;
+  const bool gpu_build = use_gpu_builder(desc->n_hittables);
+  opt.tables_only = gpu_build;
   // tuning knobs for experiments (the defaults are the measured best): leaf size and SAH cost ratio
   if (const char* e = std::getenv("RP_BVH_MAX_LEAF")) opt.max_leaf = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("RP_BVH_COST_TRAVERSE")) opt.cost_traverse = std::strtod(e, nullptr);
@@ -268,9 +283,39 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->device = device;
   s->num_cu = prop.multiProcessorCount;
   auto bail = [&](int code) { rp_scene_destroy(s); return code; };
-  if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
-      (rc = upload(ps.prim_refs, &s->d_prim_refs)) ||
-      (rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
+  uint64_t n_tree_nodes = ps.nodes.size(), n_tree_prims = ps.prims.size();
+  if (gpu_build) {
+    rpb::PrimInput pin;
+    if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
+    rpg::GpuTree gt;
+    if ((rc = rpg::build_gpu(pin, opt.max_leaf, gt, err))) return bail(fail(rc, err));
+    s->d_nodes = gt.d_nodes;
+    s->d_prims = gt.d_prims;
+    s->d_prim_refs = gt.d_prim_refs;
+    ps.root = 0;
+    ps.max_depth = gt.max_depth;
+    ps.n_leaves = gt.n_leaves;
+    n_tree_nodes = gt.n_nodes;
+    n_tree_prims = pin.prims.size();
+    if (const char* e = std::getenv("RP_BVH_CHECK"); e && std::strcmp(e, "1") == 0) {
+      // test hook: the structural self-check of the host builder on the device-built tree
+      rpb::PackedScene chk;
+      chk.nodes.resize(n_tree_nodes);
+      chk.prims.resize(n_tree_prims);
+      chk.prim_refs.resize(n_tree_prims);
+      RP_HIP(hipMemcpy(chk.nodes.data(), s->d_nodes, sizeof(rpl::Node4) * n_tree_nodes, hipMemcpyDeviceToHost));
+      RP_HIP(hipMemcpy(chk.prims.data(), s->d_prims, sizeof(rpl::Prim) * n_tree_prims, hipMemcpyDeviceToHost));
+      RP_HIP(hipMemcpy(chk.prim_refs.data(), s->d_prim_refs, sizeof(rpl::PrimRef) * n_tree_prims, hipMemcpyDeviceToHost));
+      chk.root = 0;
+      chk.max_depth = gt.max_depth;
+      chk.n_leaves = gt.n_leaves;
+      if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
+    }
+  } else if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
+             (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
+    return bail(rc);
+  }
+  if ((rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
       (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
     return bail(rc);
@@ -293,11 +338,11 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
   // a shading lane keeps its current keystream block in entries 0..15 of its (empty) stack column
   if (s->ks.stack_depth < 16) s->ks.stack_depth = 16;
-  s->n_nodes = ps.nodes.size();
+  s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
   s->max_depth = ps.max_depth;
-  s->device_bytes = sizeof(rpl::Node4) * ps.nodes.size() + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * ps.prims.size() +
+  s->device_bytes = sizeof(rpl::Node4) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
   int bpc = 0;

@@ -392,6 +392,8 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   }
   for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
 
+  if (opt.tables_only) return RP_OK;
+
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is
   //      independent of visit order except exact-t ties)
   uint32_t n = d->n_hittables;
@@ -463,6 +465,64 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
       pr.v[0] = (uint32_t)(vbase[h.mesh] + i0);
       pr.v[1] = (uint32_t)(vbase[h.mesh] + i1);
       pr.v[2] = (uint32_t)(vbase[h.mesh] + i2);
+    }
+  }
+  return RP_OK;
+}
+
+// One primitive record + reference (the packing of build(), in hittable order).
+static void pack_prim(const rp_scene_desc* d, const std::vector<uint64_t>& vbase, uint32_t id, rpl::Prim& p,
+                      rpl::PrimRef& pr) {
+  const rp_hittable& h = d->hittables[id];
+  std::memset(&p, 0, sizeof p);
+  std::memset(&pr, 0, sizeof pr);
+  pr.src = id;
+  if (h.kind == RP_HITTABLE_SPHERE) {
+    p.kind = rpl::PRIM_SPHERE;
+    p.material = h.material;
+    for (int c = 0; c < 3; c++) p.g[c] = h.center[c];
+    p.g[3] = h.radius;
+  } else {
+    const rp_mesh& m = d->meshes[h.mesh];
+    uint32_t i0 = m.indices[h.triangle], i1 = m.indices[h.triangle + 1], i2 = m.indices[h.triangle + 2];
+    const double* a = m.positions + 3 * (size_t)i0;
+    const double* b = m.positions + 3 * (size_t)i1;
+    const double* c = m.positions + 3 * (size_t)i2;
+    p.kind = rpl::PRIM_TRIANGLE;
+    p.material = m.material;
+    for (int k2 = 0; k2 < 3; k2++) {
+      p.g[k2] = a[k2];
+      p.g[3 + k2] = a[k2] - b[k2];  // ba, hittable.rs:71
+      p.g[6 + k2] = a[k2] - c[k2];  // ca, hittable.rs:72
+    }
+    pr.v[0] = (uint32_t)(vbase[h.mesh] + i0);
+    pr.v[1] = (uint32_t)(vbase[h.mesh] + i1);
+    pr.v[2] = (uint32_t)(vbase[h.mesh] + i2);
+  }
+}
+
+int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err) {
+  const uint32_t n = d->n_hittables;
+  if (n > rpl::MAX_PRIMS) { err = "too many hittables for the node encoding"; return RP_EINVAL; }
+  if ((uint64_t)n * sizeof(rpl::Prim) > 0xFFFFFFFFull) { err = "too many hittables for 32-bit device offsets"; return RP_EINVAL; }
+  std::vector<uint64_t> vbase(d->n_meshes + 1, 0);
+  for (uint32_t i = 0; i < d->n_meshes; i++) vbase[i + 1] = vbase[i] + d->meshes[i].n_vertices;
+  out.prims.resize(n);
+  out.refs.resize(n);
+  out.boxes.resize(6 * (size_t)n);
+  for (int k = 0; k < 3; k++) {
+    out.cmin[k] = std::numeric_limits<double>::infinity();
+    out.cmax[k] = -std::numeric_limits<double>::infinity();
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    pack_prim(d, vbase, i, out.prims[i], out.refs[i]);
+    const Box b = hittable_box(d, d->hittables[i]);
+    for (int k = 0; k < 3; k++) {
+      out.boxes[6 * (size_t)i + k] = b.lo[k];
+      out.boxes[6 * (size_t)i + 3 + k] = b.hi[k];
+      const double c = 0.5 * (b.lo[k] + b.hi[k]);
+      out.cmin[k] = std::fmin(out.cmin[k], c);
+      out.cmax[k] = std::fmax(out.cmax[k], c);
     }
   }
   return RP_OK;

@@ -21,6 +21,7 @@ struct BuildOptions {
   uint32_t bins = 32;           // SAH bins per axis
   double cost_traverse = 1.0;   // relative cost of one node (two child boxes)
   double cost_intersect = 1.0;  // relative cost of one primitive test
+  bool tables_only = false;     // shading tables only (nodes/prims left empty: the device builder makes them)
 };
 
 struct PackedScene {
@@ -44,8 +45,34 @@ int validate(const rp_scene_desc* d, std::string& err);
 // Builds the acceleration structure and the packed scene.  Assumes validate() passed.
 int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std::string& err);
 
+// Primitive records in hittable order (Prim, PrimRef with src = hittable id), their exact f64 boxes
+// (hittable.rs:124-147; lo xyz, hi xyz) and the bounds of the box centroids: the device builder's input.
+struct PrimInput {
+  std::vector<rpl::Prim> prims;
+  std::vector<rpl::PrimRef> refs;
+  std::vector<double> boxes;  // 6 per primitive
+  double cmin[3], cmax[3];
+};
+int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err);
+
 // Structural self-check of a packed tree: every primitive referenced exactly once, every child box
 // contains its subtree's primitive boxes, no cycles.  Returns RP_OK or RP_EINTERNAL (message in err).
 int check(const PackedScene& s, std::string& err);
 
 }  // namespace rpb
+
+namespace rpg {
+
+// A tree built on the device (rp_bvh_gpu.hip): device buffers in the rp_layout.h format, owned by the caller.
+struct GpuTree {
+  rpl::Node4* d_nodes = nullptr;  // n_nodes used (capacity: one per primitive)
+  rpl::Prim* d_prims = nullptr;   // leaf order
+  rpl::PrimRef* d_prim_refs = nullptr;
+  uint64_t n_nodes = 0, n_leaves = 0;
+  uint32_t max_depth = 0;
+};
+
+// LBVH (Karras 2012) + wide collapse on the current device.  Needs >= 2 primitives.
+int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::string& err);
+
+}  // namespace rpg

@@ -1,0 +1,384 @@
+// rp_bvh_gpu.hip -- acceleration-structure build on the device, for scenes whose
+// host binned-SAH build (rp_bvh.cpp) would dominate setup (config C5: 10 M triangles).
+//
+// Replaces Bvh::new / make_bvh / split (bvh.rs:36-91) like the host builder does: the tree shape is not
+// part of the contract, only the packed layout of rp_layout.h, which is identical, so
+// the render and intersect kernels run unchanged.  Pipeline (Karras 2012 LBVH, then a wide collapse):
+//   1. 30-bit Morton code of each primitive's box centroid, key = code << 32 | primitive (unique keys);
+//   2. device radix sort of the keys (hipCUB);
+//   3. one thread per inner node finds its key range and split (the binary radix tree of Karras 2012);
+//   4. bottom-up f64 boxes: each leaf walks to the root, the second arrival at a node unions its
+//      children's boxes (the exact min/max of AABB::union, utility.rs:130-135);
+//   5. collapse into 4-wide nodes, one launch per level: a wide node takes its binary node's children
+//      and opens the inner child of largest surface area until it has four (the host collapser's rule);
+//      a subtree of <= max_leaf primitives -- a contiguous run of the sorted order -- becomes a leaf;
+//   6. primitive records permuted into leaf (= sorted) order; child boxes rounded outward to f32.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <string>
+#include <vector>
+
+#include "rp_bvh.h"
+
+namespace rpg {
+
+namespace {
+
+constexpr uint32_t BIN_LEAF = 0x80000000u;  // binary child reference: leaf (sorted position) vs inner node
+
+struct Box6 {
+  double lo[3], hi[3];
+};
+
+__device__ __forceinline__ uint32_t expand_bits10(uint32_t v) {  // 10 bits -> every third bit of 30
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+
+__global__ void morton_kernel(uint32_t n, const Box6* __restrict__ boxes, double3 cmin, double3 scale,
+                              uint64_t* __restrict__ keys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const Box6 b = boxes[i];
+  const double c[3] = {0.5 * (b.lo[0] + b.hi[0]), 0.5 * (b.lo[1] + b.hi[1]), 0.5 * (b.lo[2] + b.hi[2])};
+  const double m[3] = {cmin.x, cmin.y, cmin.z}, s[3] = {scale.x, scale.y, scale.z};
+  uint32_t code = 0;
+  for (int k = 0; k < 3; k++) {
+    double q = (c[k] - m[k]) * s[k];
+    q = q < 0.0 ? 0.0 : (q > 1023.0 ? 1023.0 : q);  // NaN-free: boxes are finite (validated)
+    code |= expand_bits10((uint32_t)q) << (2 - k);
+  }
+  keys[i] = ((uint64_t)code << 32) | i;
+}
+
+__device__ __forceinline__ int delta(const uint64_t* keys, uint32_t n, int i, int j) {
+  if (j < 0 || j >= (int)n) return -1;
+  return __clzll(keys[i] ^ keys[j]);  // keys are unique: < 64
+}
+
+// Karras 2012, Fig. 4: inner node i of n - 1.  Children are inner nodes or leaves (sorted positions).
+__global__ void radix_tree_kernel(uint32_t n, const uint64_t* __restrict__ keys, uint32_t* __restrict__ left,
+                                  uint32_t* __restrict__ right, uint32_t* __restrict__ parent_inner,
+                                  uint32_t* __restrict__ parent_leaf, uint32_t* __restrict__ first,
+                                  uint32_t* __restrict__ last) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int)n - 1) return;
+  const int d = delta(keys, n, i, i + 1) - delta(keys, n, i, i - 1) >= 0 ? 1 : -1;
+  const int dmin = delta(keys, n, i, i - d);
+  int lmax = 2;
+  while (delta(keys, n, i, i + lmax * d) > dmin) lmax *= 2;
+  int l = 0;
+  for (int t = lmax / 2; t >= 1; t /= 2)
+    if (delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+  const int j = i + l * d;
+  const int dnode = delta(keys, n, i, j);
+  int s = 0;
+  for (int div = 2;; div *= 2) {
+    const int t = (l + div - 1) / div;
+    if (delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    if (t <= 1) break;
+  }
+  const int g = i + s * d + (d < 0 ? -1 : 0);
+  const int lo = i < j ? i : j, hi = i < j ? j : i;
+  first[i] = (uint32_t)lo;
+  last[i] = (uint32_t)hi;
+  if (lo == g) {
+    left[i] = BIN_LEAF | (uint32_t)g;
+    parent_leaf[g] = (uint32_t)i;
+  } else {
+    left[i] = (uint32_t)g;
+    parent_inner[g] = (uint32_t)i;
+  }
+  if (hi == g + 1) {
+    right[i] = BIN_LEAF | (uint32_t)(g + 1);
+    parent_leaf[g + 1] = (uint32_t)i;
+  } else {
+    right[i] = (uint32_t)(g + 1);
+    parent_inner[g + 1] = (uint32_t)i;
+  }
+}
+
+__device__ __forceinline__ double load_coherent(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ Box6 child_box(uint32_t c, const Box6* leaf_boxes, const uint32_t* order,
+                                         const Box6* node_boxes) {
+  Box6 b;
+  if (c & BIN_LEAF) {
+    b = leaf_boxes[order[c & ~BIN_LEAF]];  // written before the build: plain loads
+  } else {
+    const double* p = node_boxes[c].lo;  // written by another thread of this launch
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = load_coherent(p + k);
+      b.hi[k] = load_coherent(p + 3 + k);
+    }
+  }
+  return b;
+}
+
+// Bottom-up boxes: the second thread to reach an inner node computes it (the first stops there).
+__global__ void boxes_kernel(uint32_t n, const Box6* __restrict__ leaf_boxes, const uint32_t* __restrict__ order,
+                             const uint32_t* __restrict__ left, const uint32_t* __restrict__ right,
+                             const uint32_t* __restrict__ parent_inner, const uint32_t* __restrict__ parent_leaf,
+                             Box6* node_boxes, uint32_t* visits) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  uint32_t p = parent_leaf[k];
+  for (;;) {
+    __threadfence();
+    if (atomicAdd(&visits[p], 1u) == 0u) return;
+    __threadfence();
+    const Box6 a = child_box(left[p], leaf_boxes, order, node_boxes);
+    const Box6 b = child_box(right[p], leaf_boxes, order, node_boxes);
+    Box6 u;
+    for (int c = 0; c < 3; c++) {
+      u.lo[c] = fmin(a.lo[c], b.lo[c]);
+      u.hi[c] = fmax(a.hi[c], b.hi[c]);
+    }
+    double* q = node_boxes[p].lo;
+    for (int c = 0; c < 3; c++) {
+      __hip_atomic_store(q + c, u.lo[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(q + 3 + c, u.hi[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (p == 0) return;
+    p = parent_inner[p];
+  }
+}
+
+__device__ __forceinline__ double area(const Box6& b) {  // rp_bvh.cpp Box::area
+  const double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+  if (!(dx >= 0) || !(dy >= 0) || !(dz >= 0)) return 0.0;
+  return 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+
+struct Frontier {
+  uint32_t bin;   // binary inner node
+  uint32_t wide;  // its wide node
+};
+
+__device__ __forceinline__ uint32_t bin_count(uint32_t c, const uint32_t* first, const uint32_t* last) {
+  return (c & BIN_LEAF) ? 1u : last[c] - first[c] + 1u;
+}
+
+// One level of the collapse: every frontier entry fills its wide node and appends its inner wide
+// children to the next frontier.
+__global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur, Frontier* __restrict__ next,
+                                uint32_t* __restrict__ counters /* [0] wide nodes, [1] next frontier, [2] leaves */,
+                                uint32_t max_leaf, const Box6* __restrict__ leaf_boxes,
+                                const uint32_t* __restrict__ order, const uint32_t* __restrict__ left,
+                                const uint32_t* __restrict__ right, const uint32_t* __restrict__ first,
+                                const uint32_t* __restrict__ last, const Box6* __restrict__ node_boxes,
+                                rpl::Node4* __restrict__ nodes) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_cur) return;
+  const Frontier f = cur[t];
+  uint32_t kids[4] = {left[f.bin], right[f.bin], 0u, 0u};
+  uint32_t nk = 2;
+  while (nk < 4) {
+    int best = -1;
+    double best_area = -1.0;
+    for (uint32_t k = 0; k < nk; k++) {
+      const uint32_t c = kids[k];
+      if ((c & BIN_LEAF) || bin_count(c, first, last) <= max_leaf) continue;  // leaves are not opened
+      const double a = area(node_boxes[c]);
+      if (a > best_area) {
+        best_area = a;
+        best = (int)k;
+      }
+    }
+    if (best < 0) break;
+    const uint32_t open = kids[best];
+    kids[best] = left[open];
+    kids[nk++] = right[open];
+  }
+  rpl::Node4 nd;
+  for (uint32_t k = 0; k < 4; k++) {
+    nd.pad[k] = 0;
+    if (k >= nk) {
+      nd.lo_x[k] = nd.lo_y[k] = nd.lo_z[k] = __builtin_huge_valf();
+      nd.hi_x[k] = nd.hi_y[k] = nd.hi_z[k] = -__builtin_huge_valf();
+      nd.child[k] = rpl::ENTRY_EMPTY;
+      continue;
+    }
+    const uint32_t c = kids[k];
+    const Box6 b = (c & BIN_LEAF) ? leaf_boxes[order[c & ~BIN_LEAF]] : node_boxes[c];
+    // f64 -> f32 rounded outward (conservative child boxes, rp_layout.h)
+    nd.lo_x[k] = __double2float_rd(b.lo[0]);
+    nd.hi_x[k] = __double2float_ru(b.hi[0]);
+    nd.lo_y[k] = __double2float_rd(b.lo[1]);
+    nd.hi_y[k] = __double2float_ru(b.hi[1]);
+    nd.lo_z[k] = __double2float_rd(b.lo[2]);
+    nd.hi_z[k] = __double2float_ru(b.hi[2]);
+    const uint32_t cnt = bin_count(c, first, last);
+    if (cnt <= max_leaf) {
+      const uint32_t lo = (c & BIN_LEAF) ? (c & ~BIN_LEAF) : first[c];
+      nd.child[k] = rpl::ENTRY_LEAF | ((cnt - 1u) << rpl::LEAF_SHIFT) | lo;
+      atomicAdd(&counters[2], 1u);
+    } else {
+      const uint32_t w = atomicAdd(&counters[0], 1u);
+      nd.child[k] = w;
+      next[atomicAdd(&counters[1], 1u)] = Frontier{c, w};
+    }
+  }
+  nodes[f.wide] = nd;
+}
+
+__global__ void permute_kernel(uint32_t n, const uint32_t* __restrict__ order, const rpl::Prim* __restrict__ prims_in,
+                               const rpl::PrimRef* __restrict__ refs_in, rpl::Prim* __restrict__ prims,
+                               rpl::PrimRef* __restrict__ refs) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t i = order[k];
+  prims[k] = prims_in[i];
+  refs[k] = refs_in[i];
+}
+
+__global__ void order_kernel(uint32_t n, const uint64_t* __restrict__ keys, uint32_t* __restrict__ order) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) order[k] = (uint32_t)keys[k];
+}
+
+unsigned grid(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// Temporaries are freed on every path; on success the caller owns out.d_nodes / d_prims / d_prim_refs.
+int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::string& err) {
+  out = GpuTree{};
+  const uint32_t n = (uint32_t)in.prims.size();
+  if (n < 2) {
+    err = "device BVH build needs at least 2 primitives";
+    return RP_EINVAL;
+  }
+  if (max_leaf < 1 || max_leaf > rpl::LEAF_MAX) {
+    err = "max_leaf out of range";
+    return RP_EINVAL;
+  }
+  std::vector<void*> tmp;
+  hipError_t e = hipSuccess;
+  auto alloc = [&](void** p, size_t bytes) {
+    if (e != hipSuccess) return;
+    e = hipMalloc(p, bytes);
+    if (e == hipSuccess) tmp.push_back(*p);
+    else *p = nullptr;
+  };
+  Box6* d_boxes = nullptr;
+  rpl::Prim* d_prims_in = nullptr;
+  rpl::PrimRef* d_refs_in = nullptr;
+  uint64_t *d_keys = nullptr, *d_keys_sorted = nullptr;
+  uint32_t *d_order = nullptr, *d_left = nullptr, *d_right = nullptr, *d_pin = nullptr, *d_pleaf = nullptr;
+  uint32_t *d_first = nullptr, *d_last = nullptr, *d_visits = nullptr, *d_ctr = nullptr;
+  Box6* d_nboxes = nullptr;
+  Frontier *d_fa = nullptr, *d_fb = nullptr;
+  alloc((void**)&d_boxes, sizeof(Box6) * n);
+  alloc((void**)&d_prims_in, sizeof(rpl::Prim) * n);
+  alloc((void**)&d_refs_in, sizeof(rpl::PrimRef) * n);
+  alloc((void**)&d_keys, sizeof(uint64_t) * n);
+  alloc((void**)&d_keys_sorted, sizeof(uint64_t) * n);
+  alloc((void**)&d_order, sizeof(uint32_t) * n);
+  alloc((void**)&d_left, sizeof(uint32_t) * n);
+  alloc((void**)&d_right, sizeof(uint32_t) * n);
+  alloc((void**)&d_pin, sizeof(uint32_t) * n);
+  alloc((void**)&d_pleaf, sizeof(uint32_t) * n);
+  alloc((void**)&d_first, sizeof(uint32_t) * n);
+  alloc((void**)&d_last, sizeof(uint32_t) * n);
+  alloc((void**)&d_visits, sizeof(uint32_t) * n);
+  alloc((void**)&d_ctr, sizeof(uint32_t) * 4);
+  alloc((void**)&d_nboxes, sizeof(Box6) * n);
+  alloc((void**)&d_fa, sizeof(Frontier) * n);
+  alloc((void**)&d_fb, sizeof(Frontier) * n);
+  // outputs: at most n - 1 wide nodes (each inner wide node has >= 2 children)
+  if (e == hipSuccess) e = hipMalloc((void**)&out.d_nodes, sizeof(rpl::Node4) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&out.d_prims, sizeof(rpl::Prim) * n);
+  if (e == hipSuccess) e = hipMalloc((void**)&out.d_prim_refs, sizeof(rpl::PrimRef) * n);
+  void* d_sort_tmp = nullptr;
+  size_t sort_bytes = 0;
+  auto cleanup = [&](int code, const std::string& msg) {
+    for (void* p : tmp) (void)hipFree(p);
+    if (d_sort_tmp) (void)hipFree(d_sort_tmp);
+    if (code != RP_OK) {
+      if (out.d_nodes) (void)hipFree(out.d_nodes);
+      if (out.d_prims) (void)hipFree(out.d_prims);
+      if (out.d_prim_refs) (void)hipFree(out.d_prim_refs);
+      out = GpuTree{};
+      err = msg;
+    }
+    return code;
+  };
+  if (e != hipSuccess) return cleanup(RP_ENOMEM, std::string("hipMalloc (device BVH build): ") + hipGetErrorString(e));
+#define RPG_CHECK(what)                                                                              \
+  do {                                                                                               \
+    e = hipGetLastError();                                                                           \
+    if (e != hipSuccess) return cleanup(RP_EHIP, std::string(what) + ": " + hipGetErrorString(e));   \
+  } while (0)
+  e = hipMemcpy(d_boxes, in.boxes.data(), sizeof(Box6) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_prims_in, in.prims.data(), sizeof(rpl::Prim) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_refs_in, in.refs.data(), sizeof(rpl::PrimRef) * n, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(d_visits, 0, sizeof(uint32_t) * n);
+  if (e == hipSuccess) e = hipMemset(d_ctr, 0, sizeof(uint32_t) * 4);
+  if (e != hipSuccess) return cleanup(RP_EHIP, std::string("upload (device BVH build): ") + hipGetErrorString(e));
+
+  const unsigned B = 256;
+  double3 cmin = make_double3(in.cmin[0], in.cmin[1], in.cmin[2]);
+  double sc[3];
+  for (int k = 0; k < 3; k++) {
+    const double ext = in.cmax[k] - in.cmin[k];
+    sc[k] = ext > 0.0 ? 1024.0 / ext : 0.0;
+  }
+  hipLaunchKernelGGL(morton_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_boxes, cmin,
+                     make_double3(sc[0], sc[1], sc[2]), d_keys);
+  RPG_CHECK("morton");
+  e = hipcub::DeviceRadixSort::SortKeys(nullptr, sort_bytes, d_keys, d_keys_sorted, (int)n, 0, 62);
+  if (e == hipSuccess) e = hipMalloc(&d_sort_tmp, sort_bytes);
+  if (e == hipSuccess) e = hipcub::DeviceRadixSort::SortKeys(d_sort_tmp, sort_bytes, d_keys, d_keys_sorted, (int)n, 0, 62);
+  if (e != hipSuccess) return cleanup(RP_EHIP, std::string("radix sort: ") + hipGetErrorString(e));
+  hipLaunchKernelGGL(order_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_keys_sorted, d_order);
+  RPG_CHECK("order");
+  hipLaunchKernelGGL(radix_tree_kernel, dim3(grid(n - 1, B)), dim3(B), 0, nullptr, n, d_keys_sorted, d_left, d_right,
+                     d_pin, d_pleaf, d_first, d_last);
+  RPG_CHECK("radix tree");
+  hipLaunchKernelGGL(boxes_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_boxes, d_order, d_left, d_right,
+                     d_pin, d_pleaf, d_nboxes, d_visits);
+  RPG_CHECK("boxes");
+  // collapse, level by level from the root (binary inner node 0 -> wide node 0)
+  const Frontier root{0u, 0u};
+  const uint32_t one = 1u;
+  e = hipMemcpy(d_fa, &root, sizeof root, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_ctr, &one, sizeof one, hipMemcpyHostToDevice);  // wide node 0 taken
+  if (e != hipSuccess) return cleanup(RP_EHIP, std::string("collapse setup: ") + hipGetErrorString(e));
+  uint32_t n_cur = 1, depth = 0;
+  for (;;) {
+    e = hipMemset(d_ctr + 1, 0, sizeof(uint32_t));
+    if (e != hipSuccess) return cleanup(RP_EHIP, std::string("collapse: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(collapse_kernel, dim3(grid(n_cur, B)), dim3(B), 0, nullptr, d_fa, n_cur, d_fb, d_ctr, max_leaf,
+                       d_boxes, d_order, d_left, d_right, d_first, d_last, d_nboxes, out.d_nodes);
+    RPG_CHECK("collapse");
+    uint32_t ctr[4];
+    e = hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return cleanup(RP_EHIP, std::string("collapse: ") + hipGetErrorString(e));
+    if (ctr[0] > n) return cleanup(RP_EINTERNAL, "device BVH build: wide node overflow");
+    if (ctr[1] == 0) {
+      out.n_nodes = ctr[0];
+      out.n_leaves = ctr[2];
+      break;
+    }
+    depth++;
+    n_cur = ctr[1];
+    std::swap(d_fa, d_fb);
+  }
+  out.max_depth = depth;
+  hipLaunchKernelGGL(permute_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_order, d_prims_in, d_refs_in,
+                     out.d_prims, out.d_prim_refs);
+  RPG_CHECK("permute");
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return cleanup(RP_EHIP, std::string("device BVH build: ") + hipGetErrorString(e));
+#undef RPG_CHECK
+  return cleanup(RP_OK, "");
+}
+
+}  // namespace rpg

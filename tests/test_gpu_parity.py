@@ -169,8 +169,12 @@ def test_render_device_torch(gpu):
     assert int(ctr[0]) == st["rays"] and int(ctr[3]) == 0
 
 
-def test_intersect_rays(gpu):
-    """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle."""
+@pytest.mark.parametrize("builder", ["host", "gpu"])
+def test_intersect_rays(gpu, monkeypatch, builder):
+    """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle --
+    over the host SAH tree and the device-built LBVH (RP_BVH_BUILDER)."""
+    monkeypatch.setenv("RP_BVH_BUILDER", builder)
+    monkeypatch.setenv("RP_BVH_CHECK", "1")
     from oracle import oracle_py as O
     from rtpotato import scenes
     rng = np.random.default_rng(5)
@@ -271,3 +275,18 @@ def test_workspaces_frames_in_flight(gpu):
             assert torch.equal(outs[k], ref)
             assert int(ctrs[k][0]) == int(c0[0]) and int(ctrs[k][3]) == 0
         wss[0].close()  # explicit destroy before the scene; the other one is destroyed with the scene
+
+
+@pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000), ("three_balls", None)])
+def test_device_bvh_builder(gpu, monkeypatch, name, arg):
+    """Scenes over the device-built tree (rp_bvh_gpu.hip: LBVH + wide collapse), with the host builder's
+    structural self-check on the downloaded tree (RP_BVH_CHECK): same image and ray counts as the oracle."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    monkeypatch.setenv("RP_BVH_BUILDER", "gpu")
+    monkeypatch.setenv("RP_BVH_CHECK", "1")
+    sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
+    with gpu.DeviceScene(sc) as ds:
+        info = ds.info()
+        assert info["nodes"] >= 1 and (info["max_depth"] >= 4 or name == "three_balls")
+    _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED))
