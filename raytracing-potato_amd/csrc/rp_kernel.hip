@@ -150,19 +150,30 @@ struct Rng {
   uint32_t* end;   // LDS cursor: one past the newest ring block
   uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
-// The keystream block being drawn from lives in the lane's traversal-stack column in LDS, not in registers:
-// a lane only draws while it shades, and a lane that shades has finished its traversal, so its stack column
-// is free (entries 0..15; the kernel sizes the stack to >= 16).  A draw is then one ds_read2st64 at the
-// lane's word offset (the column is [entry][lane], conflict-free) instead of a 16-way register select, and
-// the block costs no VGPRs through the shading code.
+// The keystream block being drawn from lives in the TOP 17 entries of the lane's traversal-stack column in
+// LDS, not in registers: a tag word (entry D-17) and the block's 16 words (entries D-16..D-1).  A lane only
+// draws while it shades, when its traversal is over, and a draw is one ds_read2st64 at the lane's word
+// offset (the column is [entry][lane], conflict-free) instead of a 16-way register select.  The block stays
+// valid across rays until a traversal's stack reaches it: pushes write a prefix [0, m] of the column, so
+// the top region was written iff the tag entry was, and a stack entry (node index < 2^28, or a leaf/empty
+// entry with bit 31 set) never looks like a tag (bit 30 set, bit 31 clear).  rng_sync checks the tag once
+// per shading site; the kernel sizes the stack to >= 17 entries.
+static constexpr uint32_t RNG_TAG = 0x40000000u;
+RPK_INLINE uint32_t kargs_stack_depth();  // S.stack_depth from the kernel arguments (defined with KArgs)
 struct RngBlk {
-  uint32_t* col;  // LDS: this lane's stack column (word k at col[k * BLOCK])
-  uint32_t blk;   // block index held in the column
-  RPK_INLINE explicit RngBlk(uint32_t* c) : col(c), blk(0xFFFFFFFFu) {}
+  uint32_t* col;  // LDS: word k of the block at col[k * BLOCK]; the tag at col[-BLOCK]
+  uint32_t& blk;  // block index held in the column (0xFFFFFFFF = none); lives across rays
+  RPK_INLINE RngBlk(uint32_t* c, uint32_t& b) : col(c), blk(b) {}
 };
+RPK_INLINE uint32_t* rng_col(uint32_t* stk) { return stk + (kargs_stack_depth() - 16u) * BLOCK; }
 RPK_INLINE void col_store(RngBlk& b, const uint32_t w[16]) {
 #pragma unroll
   for (int k = 0; k < 16; k++) b.col[k * BLOCK] = w[k];
+  b.col[-(int)BLOCK] = RNG_TAG | b.blk;
+}
+// After a traversal: forget the block if the stack overwrote it.
+RPK_INLINE void rng_sync(RngBlk& b) {
+  if (b.col[-(int)BLOCK] != (RNG_TAG | b.blk)) b.blk = 0xFFFFFFFFu;
 }
 
 RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
@@ -864,6 +875,7 @@ RPK_INLINE KArgsPtr kargs() {
   asm volatile("" : "+s"(p));
   return p;
 }
+RPK_INLINE uint32_t kargs_stack_depth() { return kargs()->S.stack_depth; }
 
 // Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
 // tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
@@ -1021,6 +1033,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   // Camera samples start at the top of the next round, after the refill pass: `start` = sample s is due,
   // `fresh` = and it is the first of a unit whose key and block 0 the refill pass makes.
   bool start = alive, fresh = alive;
+  uint32_t rblk = 0xFFFFFFFFu;  // keystream block held in the top of the lane's stack column (RngBlk)
   DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
 
   // Every lane of the wave stays in this loop until the whole wave has retired, so the ballots below
@@ -1038,8 +1051,9 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     }
     if (start) {
       KArgsPtr A = kargs();
-      RngBlk rb(stk);
-      rng_load(rng, rb);
+      RngBlk rb(rng_col(stk), rblk);
+      if (fresh) rb.blk = 0xFFFFFFFFu;  // a new stream: block 0 of the column (if any) is another unit's
+      else rng_sync(rb);
       start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
       depth = A->P.max_bounce;
       T_x = T_y = T_z = 1.0;
@@ -1152,8 +1166,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         // code is what decides the kernel's register budget)
         bool scattered = false;
         if (hit) {
-          RngBlk rb(stk);
-          rng_load(rng, rb);
+          RngBlk rb(rng_col(stk), rblk);
+          rng_sync(rb);
           scattered = scatter_eval(*m, d, h, rng, rb, nd);
         }
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
