@@ -213,7 +213,8 @@ def main():
                                   "kernel time; the wide SAH tree visits ~9x fewer boxes and the bunny scene is "
                                   "cache-resident, so it exceeds HBM peak; traffic = measured memory-side bytes; the "
                                   "kernel is FP64/VALU-issue bound (fp64_vector)") if args.config != "C5" else
-                                 ("10M-triangle scene (2.75 GB device data, deep BVH): the HBM-bound config")},
+                                 (f"10M-triangle scene ({info['device_bytes'] / 1e9:.2f} GB device data, deep BVH, "
+                                  "beyond the 256 MB Infinity Cache): the memory-bound config")},
             "fp64_vector": {"achieved": round(achieved_tf, 3), "peak": FP64_VECTOR_PEAK_TF, "unit": "TFLOP/s",
                             "frac": round(achieved_tf / FP64_VECTOR_PEAK_TF, 4), "flops_per_ray": round(fpr, 1)},
             "cpu_baseline": None,
