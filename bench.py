@@ -207,7 +207,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src and f"{traffic_src} (rocprofv3 PMC, build {traffic_git})",
-                         "kernel": "rpk::render_kernel<false>", "kernel_ms": round(kernel_s * 1e3, 3),
+                         "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3),
                          "bytes_per_ray": round(bpr, 1),
                          "note": ("achieved = the reference traversal's algorithmic bytes per ray (SURVEY 8d) x rays / "
                                   "kernel time; the wide SAH tree visits ~9x fewer boxes and the bunny scene is "

@@ -66,6 +66,7 @@ struct rp_workspace {
   uint32_t* d_tile_cost = nullptr;   // cost probe output, 2 x rpk::TILE_SORT_MAX entries
   uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
   uint32_t* d_slab = nullptr;        // keystream cache, one slab per resident render lane
+  uint32_t* d_spill = nullptr;       // traversal-stack overflow entries of every resident lane (deep trees)
   double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames (grown on demand)
   uint32_t* d_partial_hits = nullptr;
   uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
@@ -95,7 +96,7 @@ namespace {
 
 void ws_release(rp_workspace* w) {
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_tile_cost, (void*)w->d_tile_order,
-                  (void*)w->d_slab, (void*)w->d_partial, (void*)w->d_partial_hits})
+                  (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial, (void*)w->d_partial_hits})
     if (p) (void)hipFree(p);
   *w = rp_workspace{};
 }
@@ -110,7 +111,9 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
       hipMalloc(reinterpret_cast<void**>(&w->d_probe_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&w->d_tile_cost), sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX) != hipSuccess ||
       hipMalloc(reinterpret_cast<void**>(&w->d_tile_order), sizeof(uint32_t) * rpk::TILE_SORT_MAX) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess) {
+      hipMalloc(reinterpret_cast<void**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess ||
+      hipMalloc(reinterpret_cast<void**>(&w->d_spill),
+                lanes * sizeof(uint32_t) * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth)) != hipSuccess) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
   }
@@ -345,8 +348,28 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->device_bytes = sizeof(rpl::Node4) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
+  // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
+  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
+  // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  RP_LDS_DEPTH forces a
+  // depth (>= 17) for tests and tuning.
+  s->ks.lds_depth = s->ks.stack_depth;
   int bpc = 0;
-  if (rpk::render_blocks_per_cu(s->ks.stack_depth, &bpc) != 0 || bpc < 1) bpc = 1;
+  if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, &bpc) != 0 || bpc < 1) bpc = 1;
+  int bpc_spill = 0;
+  if (rpk::render_blocks_per_cu(17, true, &bpc_spill) == 0 && bpc_spill > bpc) {
+    uint32_t L = s->ks.stack_depth - 1;
+    int b = 0;
+    while (L > 17 && (rpk::render_blocks_per_cu(L, true, &b) != 0 || b < bpc_spill)) L--;
+    s->ks.lds_depth = L;
+    bpc = bpc_spill;
+  }
+  if (const char* e = std::getenv("RP_LDS_DEPTH")) {
+    const uint32_t L = (uint32_t)std::strtoul(e, nullptr, 10);
+    if (L >= 17 && L < s->ks.stack_depth) {
+      s->ks.lds_depth = L;
+      if (rpk::render_blocks_per_cu(L, true, &bpc) != 0 || bpc < 1) bpc = 1;
+    }
+  }
   s->blocks_per_cu = bpc;
   if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);
   *out = s;
@@ -492,6 +515,7 @@ int rp_render_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, cons
   const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
   rpk::KScene ks = s->ks;
   ks.rng_slab = w->d_slab;
+  ks.spill = w->d_spill;
   auto grid_for = [&](uint64_t slots) {
     const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
     return (int)std::max<uint64_t>(1, std::min(want, resident));

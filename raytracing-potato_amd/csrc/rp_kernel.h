@@ -17,9 +17,11 @@ struct KScene {
   const uint32_t* texels;
   rpl::Emit background;
   uint32_t root;
-  uint32_t stack_depth;  // LDS traversal stack entries per lane (>= max_depth + 2)
+  uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
+  uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
   uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
+  uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) entries
 };
 
 // Bytes of keystream cache (ChaCha key, ring of main-stream blocks, jitter blocks) per resident lane of
@@ -108,7 +110,7 @@ struct SrgbTable {
 int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_t* bgra, void* stream);
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
-int render_blocks_per_cu(uint32_t stack_depth, int* blocks);
+int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
 
 // Closest-hit query kernel (one ray per thread).
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,

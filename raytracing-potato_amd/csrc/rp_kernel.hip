@@ -159,13 +159,13 @@ struct Rng {
 // entry with bit 31 set) never looks like a tag (bit 30 set, bit 31 clear).  rng_sync checks the tag once
 // per shading site; the kernel sizes the stack to >= 17 entries.
 static constexpr uint32_t RNG_TAG = 0x40000000u;
-RPK_INLINE uint32_t kargs_stack_depth();  // S.stack_depth from the kernel arguments (defined with KArgs)
+RPK_INLINE uint32_t kargs_lds_depth();  // S.lds_depth from the kernel arguments (defined with KArgs)
 struct RngBlk {
   uint32_t* col;  // LDS: word k of the block at col[k * BLOCK]; the tag at col[-BLOCK]
   uint32_t& blk;  // block index held in the column (0xFFFFFFFF = none); lives across rays
   RPK_INLINE RngBlk(uint32_t* c, uint32_t& b) : col(c), blk(b) {}
 };
-RPK_INLINE uint32_t* rng_col(uint32_t* stk) { return stk + (kargs_stack_depth() - 16u) * BLOCK; }
+RPK_INLINE uint32_t* rng_col(uint32_t* stk) { return stk + (kargs_lds_depth() - 16u) * BLOCK; }
 RPK_INLINE void col_store(RngBlk& b, const uint32_t w[16]) {
 #pragma unroll
   for (int k = 0; k < 16; k++) b.col[k * BLOCK] = w[k];
@@ -482,9 +482,23 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
   }
 }
 
+// Stack entry i of a lane: in its LDS column (entry i at stk[i * stride]) or, for SPILL kernels, entries
+// >= S.lds_depth in the lane's global overflow run (S.spill[spl + i - lds_depth], L2-resident) -- a deep
+// tree (config C5: 43 entries) then keeps the LDS of four blocks per CU.
+template <bool SPILL>
+RPK_INLINE void stk_put(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, uint32_t i, uint32_t v) {
+  if (!SPILL || i < S.lds_depth) stk[i * stride] = v;
+  else S.spill[spl + i - S.lds_depth] = v;
+}
+template <bool SPILL>
+RPK_INLINE uint32_t stk_get(const KScene& S, const uint32_t* stk, uint32_t stride, uint32_t spl, uint32_t i) {
+  return (!SPILL || i < S.lds_depth) ? stk[i * stride] : S.spill[spl + i - S.lds_depth];
+}
+
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY (the
-// parked leaf is always consumed inside a step).
-RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const Ray32& r, V3 o, V3 d,
+// parked leaf is always consumed inside a step).  `spl`: the lane's first spill entry (SPILL kernels).
+template <bool SPILL>
+RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
   double best = ts.best;
@@ -557,29 +571,36 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
                            (uint32_t)(tn[3] != INFF);
     const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
-    stk[sp * stride] = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]);
-    stk[(sp + 1u) * stride] = k == 3u ? cc[2] : cc[1];
-    stk[(sp + 2u) * stride] = cc[1];
+    const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
+    if (!SPILL || sp + 2u < S.lds_depth) {
+      stk[sp * stride] = e0;
+      stk[(sp + 1u) * stride] = e1;
+      stk[(sp + 2u) * stride] = cc[1];
+    } else {
+      stk_put<SPILL>(S, stk, stride, spl, sp, e0);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 1u, e1);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, cc[1]);
+    }
     sp += k;
     if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
       overflow = true;
       sp = cap;
     }
     if (n_hit) cur = cc[0];
-    else cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+    else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
 #ifndef RPK_NO_SPECULATIVE
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
     // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.
     if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
       leaf = cur;
-      cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+      cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
     }
     if (__ballot(leaf == 0u) == 0) break;
 #endif
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
-    cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+    cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
   // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
@@ -593,7 +614,7 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, const
     if (++k == kend) {
       if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
         leaf = cur;
-        cur = sp ? stk[(--sp) * stride] : rpl::ENTRY_EMPTY;
+        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
         k = leaf & rpl::LEAF_FIRST_MASK;
         kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
       } else {
@@ -613,7 +634,7 @@ RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, 
   setup_ray32(o, d, tmin, r);
   TravState t;
   trav_init(S, tmax, t);
-  while (t.cur != rpl::ENTRY_EMPTY) trav_step(S, stk, stride, r, o, d, tmin, t, overflow, td);
+  while (t.cur != rpl::ENTRY_EMPTY) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
   hr.u = t.bu;
   hr.v = t.bv;
@@ -866,6 +887,8 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.background.color[2] = A->S.background.color[2];
   S.root = A->S.root;
   S.stack_depth = A->S.stack_depth;
+  S.lds_depth = A->S.lds_depth;
+  S.spill = A->S.spill;
   S.rng_slab = A->S.rng_slab;
   return S;
 }
@@ -875,7 +898,7 @@ RPK_INLINE KArgsPtr kargs() {
   asm volatile("" : "+s"(p));
   return p;
 }
-RPK_INLINE uint32_t kargs_stack_depth() { return kargs()->S.stack_depth; }
+RPK_INLINE uint32_t kargs_lds_depth() { return kargs()->S.lds_depth; }
 
 // Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
 // tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
@@ -959,7 +982,7 @@ RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint
 #endif
 // PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
 // and timings of the frame kernel never mix with it.
-template <bool PROBE>
+template <bool PROBE, bool SPILL>
 __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
@@ -1067,15 +1090,17 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       KArgsPtr A = kargs();
       const KScene S = load_scene(A);
       const uint32_t thr = A->P.trav_threshold;
+      // the lane's spill run (SPILL kernels): lane index x spill entries per lane
+      const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + tid) * (S.stack_depth - S.lds_depth) : 0u;
       Ray32 r;
       setup_ray32(o, d, RAY_EPSILON, r);
       for (;;) {
         if (alive && !tdone) {
           DREG(DREG_STEP)
 #ifdef RPK_DIAG
-          trav_step(S, stk, BLOCK, r, o, d, RAY_EPSILON, ts, overflow, &td);
+          trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
 #else
-          trav_step(S, stk, BLOCK, r, o, d, RAY_EPSILON, ts, overflow);
+          trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
 #endif
           tdone = ts.cur == rpl::ENTRY_EMPTY;
         }
@@ -1328,7 +1353,8 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
 
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters, int grid,
                   void* stream) {
-  const size_t lds = (size_t)s.stack_depth * BLOCK * sizeof(uint32_t);
+  const size_t lds = (size_t)s.lds_depth * BLOCK * sizeof(uint32_t);
+  const bool spill = s.lds_depth < s.stack_depth;
   KArgs a;
   a.S = s;
   a.P = p;
@@ -1336,8 +1362,10 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.out_fg = out_fg;
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
-  if (p.probe) hipLaunchKernelGGL(render_kernel<true>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(render_kernel<false>, dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  if (p.probe && spill) hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  else if (p.probe) hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  else if (spill) hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 
@@ -1453,9 +1481,10 @@ int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32
 
 uint64_t rng_slab_bytes_per_lane() { return (uint64_t)SLAB_N * sizeof(uint4); }
 
-int render_blocks_per_cu(uint32_t stack_depth, int* blocks) {
-  const size_t lds = (size_t)stack_depth * BLOCK * sizeof(uint32_t);
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false>, BLOCK, lds);
+int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks) {
+  const size_t lds = (size_t)lds_depth * BLOCK * sizeof(uint32_t);
+  if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true>, BLOCK, lds);
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false>, BLOCK, lds);
 }
 
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,

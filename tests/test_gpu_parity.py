@@ -290,3 +290,15 @@ def test_device_bvh_builder(gpu, monkeypatch, name, arg):
         info = ds.info()
         assert info["nodes"] >= 1 and (info["max_depth"] >= 4 or name == "three_balls")
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED))
+
+
+@pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
+def test_spilled_traversal_stack(gpu, monkeypatch, name, arg):
+    """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
+    deep trees such as C5's use): forced here with RP_LDS_DEPTH=17, so nearly every traversal spills and
+    the keystream block in the column's top is clobbered by almost every ray -- same image as the oracle."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    monkeypatch.setenv("RP_LDS_DEPTH", "17")
+    sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED))

@@ -15,7 +15,7 @@ import os
 import subprocess
 import sys
 
-KERNEL = "rpk::render_kernel<false>"
+KERNEL = "rpk::render_kernel<false, "  # the frame kernel (either stack variant), not the probe
 
 
 def counter(dirname, name):
