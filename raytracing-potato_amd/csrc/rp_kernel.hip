@@ -171,10 +171,6 @@ RPK_INLINE void col_store(RngBlk& b, const uint32_t w[16]) {
   for (int k = 0; k < 16; k++) b.col[k * BLOCK] = w[k];
   b.col[-(int)BLOCK] = RNG_TAG | b.blk;
 }
-// After a traversal: forget the block if the stack overwrote it.
-RPK_INLINE void rng_sync(RngBlk& b) {
-  if (b.col[-(int)BLOCK] != (RNG_TAG | b.blk)) b.blk = 0xFFFFFFFFu;
-}
 
 RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
   const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
@@ -215,6 +211,13 @@ RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
     *r.end = b.blk + 1;
   }
   col_store(b, w);
+}
+
+// At a shading site, after a traversal: make the column hold block pos/16 if the stack overwrote it or the
+// stream moved on -- one load for every lane of the wave that needs it, before the material's draw sites
+// diverge (a load inside them runs once per material branch).
+RPK_INLINE void rng_ready(const Rng& r, RngBlk& b) {
+  if (b.col[-(int)BLOCK] != (RNG_TAG | b.blk) || (r.pos >> 4) != b.blk) rng_load(r, b);
 }
 
 // The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
@@ -1076,7 +1079,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       KArgsPtr A = kargs();
       RngBlk rb(rng_col(stk), rblk);
       if (fresh) rb.blk = 0xFFFFFFFFu;  // a new stream: block 0 of the column (if any) is another unit's
-      else rng_sync(rb);
+      rng_ready(rng, rb);
       start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
       depth = A->P.max_bounce;
       T_x = T_y = T_z = 1.0;
@@ -1192,7 +1195,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         bool scattered = false;
         if (hit) {
           RngBlk rb(rng_col(stk), rblk);
-          rng_sync(rb);
+          rng_ready(rng, rb);
           scattered = scatter_eval(*m, d, h, rng, rb, nd);
         }
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
