@@ -96,12 +96,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a one-GPU box (never for measurements): every rank on device
+    # RP_BENCH_DEVICE, collectives over RP_BENCH_BACKEND (gloo)
+    if "RP_BENCH_DEVICE" in os.environ:
+        local = int(os.environ["RP_BENCH_DEVICE"])
+    backend = os.environ.get("RP_BENCH_BACKEND", "nccl")
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from dataclasses import replace
     from rtpotato import scenes
