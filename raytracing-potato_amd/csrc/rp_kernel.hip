@@ -295,6 +295,35 @@ RPK_INLINE uint64_t next_u64(Rng& r, RngBlk& b) {
 RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
 RPK_INLINE double gen_f64(Rng& r, RngBlk& b) { return u64_to_f64(next_u64(r, b)); }
 
+// Rejection loops (UnitBall / UnitSphere tries) read their draws straight from the ring: the RING blocks
+// of a lane are one circular run of 16*RING words in its slab, so stream word a sits at ring word
+// a % (16*RING) while its block is held (blocks [end - RING, end)).  A loop makes sure every block its
+// next tries touch is there (ring_ensure: in place generation, rare, as rng_load's fallback), then loads
+// and evaluates RPK_TRIES tries at once and keeps the first accepted one -- the draws consumed, and so the
+// stream, are exactly the sequential loop's.  A wave iterates until its slowest lane accepts: with
+// acceptance p a lane needs a geometric number of tries, and the wave's maximum over its ~20 shading lanes
+// is ~5 single tries for the ball (p = pi/6); RPK_TRIES per round cuts the rounds, and each round pays one
+// ring-load latency instead of per-draw block checks and LDS column reloads.
+#ifndef RPK_TRIES
+#define RPK_TRIES 2
+#endif
+static_assert(RING * 16 == 128, "ring_u64 indexes the ring as 128 words");
+RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
+  while (last_blk >= *r.end) {
+    DREG(DREG_RNG_FALLBACK)
+    const uint32_t b = *r.end;
+    uint32_t k[8], w[16];
+    load_key(r, k);
+    chacha12(k, b, w);
+    store_block(ring_slot(r, b), w);
+    *r.end = b + 1;
+  }
+}
+RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64 from stream words a, a+1 (a even)
+  const uint2 v = reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
+  return u64_to_f64(((uint64_t)v.y << 32) | v.x);
+}
+
 // ------------------------------------------------------------------ math -------------------------
 
 struct V3 { double x, y, z; };
@@ -796,13 +825,25 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
     case 1: {  // Lambert (material.rs:115-130)
       DREG(DREG_LAMBERT)
       if (dot(h.n, d) > 0.0) return false;
-      double x, y, s;
-      do {  // UnitSphere (randomness.rs:58-73)
+      double x = 0.0, y = 0.0, s = 0.0;
+      // UnitSphere (randomness.rs:58-73): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
         DREG(DREG_LOOP_LAMBERT)
-        x = 2.0 * gen_f64(rng, rb) - 1.0;
-        y = 2.0 * gen_f64(rng, rb) - 1.0;
-        s = x * x + y * y;
-      } while (!(s < 1.0));
+        ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
+        double tx[RPK_TRIES], ty[RPK_TRIES];
+#pragma unroll
+        for (int j = 0; j < RPK_TRIES; j++) {
+          tx[j] = ring_f64(rng, a + 4u * j);
+          ty[j] = ring_f64(rng, a + 4u * j + 2u);
+        }
+        bool done = false;
+#pragma unroll
+        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+          const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0, qs = qx * qx + qy * qy;
+          if (qs < 1.0) { x = qx; y = qy; s = qs; rng.pos = a + 4u * (j + 1); done = true; }
+        }
+        if (done) break;
+      }
       const double q = 2.0 * sqrt(1.0 - s);
       nd = normalize(add(h.n, v3(x * q, y * q, 1.0 - 2.0 * s)));
       return true;
@@ -810,13 +851,26 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
     case 2: {  // Metal (material.rs:132-152)
       DREG(DREG_METAL)
       if (dot(h.n, d) > 0.0) return false;
-      double x, y, z;
-      do {  // UnitBall (randomness.rs:39-53)
+      double x = 0.0, y = 0.0, z = 0.0;
+      // UnitBall (randomness.rs:39-53): tries of 3 draws, RPK_TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 6u * RPK_TRIES) {
         DREG(DREG_LOOP_METAL)
-        x = 2.0 * gen_f64(rng, rb) - 1.0;
-        y = 2.0 * gen_f64(rng, rb) - 1.0;
-        z = 2.0 * gen_f64(rng, rb) - 1.0;
-      } while (!((x * x + y * y) + z * z < 1.0));
+        ring_ensure(rng, (a + 6u * RPK_TRIES - 1u) >> 4);
+        double tx[RPK_TRIES], ty[RPK_TRIES], tz[RPK_TRIES];
+#pragma unroll
+        for (int j = 0; j < RPK_TRIES; j++) {
+          tx[j] = ring_f64(rng, a + 6u * j);
+          ty[j] = ring_f64(rng, a + 6u * j + 2u);
+          tz[j] = ring_f64(rng, a + 6u * j + 4u);
+        }
+        bool done = false;
+#pragma unroll
+        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+          const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0, qz = 2.0 * tz[j] - 1.0;
+          if ((qx * qx + qy * qy) + qz * qz < 1.0) { x = qx; y = qy; z = qz; rng.pos = a + 6u * (j + 1); done = true; }
+        }
+        if (done) break;
+      }
       const V3 r = normalize(add(reflect(d, h.n), smul(m.scatter_param, v3(x, y, z))));
       if (dot(h.n, r) < 0.0) return false;
       nd = r;
@@ -961,11 +1015,24 @@ RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint
   const uint32_t w0 = jw.x, w1 = jw.y, w2 = jw.z, w3 = jw.w;
   const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
   const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
-  double dx, dy;
-  do {  // UnitDisk (randomness.rs:21-34)
-    dx = 2.0 * gen_f64(rng, rb) - 1.0;
-    dy = 2.0 * gen_f64(rng, rb) - 1.0;
-  } while (!(dx * dx + dy * dy < 1.0));
+  double dx = 0.0, dy = 0.0;
+  // UnitDisk (randomness.rs:21-34): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
+  for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
+    ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
+    double tx[RPK_TRIES], ty[RPK_TRIES];
+#pragma unroll
+    for (int j = 0; j < RPK_TRIES; j++) {
+      tx[j] = ring_f64(rng, a + 4u * j);
+      ty[j] = ring_f64(rng, a + 4u * j + 2u);
+    }
+    bool done = false;
+#pragma unroll
+    for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+      const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0;
+      if (qx * qx + qy * qy < 1.0) { dx = qx; dy = qy; rng.pos = a + 4u * (j + 1); done = true; }
+    }
+    if (done) break;
+  }
   A = kargs();
   // tan(fov/2) is computed on the host (render.rs:33 is a per-camera constant; same libm as the reference)
   const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
@@ -978,7 +1045,9 @@ RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint
   o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
 }
 
-#ifdef RPK_W4
+#if defined(RPK_WAVES)  // occupancy experiments (tools/build_variant.sh -DRPK_WAVES=5 with RP_LDS_DEPTH)
+#define RPK_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(RPK_WAVES)))
+#elif defined(RPK_W4)
 #define RPK_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #else
 #define RPK_RENDER_ATTR
