@@ -339,7 +339,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
   // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
-  // a lane keeps its keystream block in the top 17 entries of its stack column (tag + 16 words)
+  // floor of 17 entries: the spill split below never keeps fewer in LDS (RP_LDS_DEPTH tests force 17)
   if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
   s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;

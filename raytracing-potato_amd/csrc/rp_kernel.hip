@@ -150,28 +150,6 @@ struct Rng {
   uint32_t* end;   // LDS cursor: one past the newest ring block
   uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
-// The keystream block being drawn from lives in the TOP 17 entries of the lane's traversal-stack column in
-// LDS, not in registers: a tag word (entry D-17) and the block's 16 words (entries D-16..D-1).  A lane only
-// draws while it shades, when its traversal is over, and a draw is one ds_read2st64 at the lane's word
-// offset (the column is [entry][lane], conflict-free) instead of a 16-way register select.  The block stays
-// valid across rays until a traversal's stack reaches it: pushes write a prefix [0, m] of the column, so
-// the top region was written iff the tag entry was, and a stack entry (node index < 2^28, or a leaf/empty
-// entry with bit 31 set) never looks like a tag (bit 30 set, bit 31 clear).  rng_sync checks the tag once
-// per shading site; the kernel sizes the stack to >= 17 entries.
-static constexpr uint32_t RNG_TAG = 0x40000000u;
-RPK_INLINE uint32_t kargs_lds_depth();  // S.lds_depth from the kernel arguments (defined with KArgs)
-struct RngBlk {
-  uint32_t* col;  // LDS: word k of the block at col[k * BLOCK]; the tag at col[-BLOCK]
-  uint32_t& blk;  // block index held in the column (0xFFFFFFFF = none); lives across rays
-  RPK_INLINE RngBlk(uint32_t* c, uint32_t& b) : col(c), blk(b) {}
-};
-RPK_INLINE uint32_t* rng_col(uint32_t* stk) { return stk + (kargs_lds_depth() - 16u) * BLOCK; }
-RPK_INLINE void col_store(RngBlk& b, const uint32_t w[16]) {
-#pragma unroll
-  for (int k = 0; k < 16; k++) b.col[k * BLOCK] = w[k];
-  b.col[-(int)BLOCK] = RNG_TAG | b.blk;
-}
-
 RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
   const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
   k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
@@ -194,31 +172,6 @@ RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
 }
 RPK_INLINE uint4* ring_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_RING + 4 * (b % RING); }
 RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT + 4 * (b & 1u); }
-
-// Block pos/16 into registers: from the ring, or generated in place when the ring ran dry.
-RPK_INLINE void rng_load(const Rng& r, RngBlk& b) {
-  b.blk = r.pos >> 4;
-  uint32_t w[16];
-  if (b.blk < *r.end) {
-    DREG(DREG_RING_LOAD)
-    load_block(ring_slot(r, b.blk), w);
-  } else {
-    DREG(DREG_RNG_FALLBACK)
-    uint32_t k[8];
-    load_key(r, k);
-    chacha12(k, b.blk, w);
-    store_block(ring_slot(r, b.blk), w);
-    *r.end = b.blk + 1;
-  }
-  col_store(b, w);
-}
-
-// At a shading site, after a traversal: make the column hold block pos/16 if the stack overwrote it or the
-// stream moved on -- one load for every lane of the wave that needs it, before the material's draw sites
-// diverge (a load inside them runs once per material branch).
-RPK_INLINE void rng_ready(const Rng& r, RngBlk& b) {
-  if (b.col[-(int)BLOCK] != (RNG_TAG | b.blk) || (r.pos >> 4) != b.blk) rng_load(r, b);
-}
 
 // The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
 // samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
@@ -283,24 +236,15 @@ RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
   return v;
 }
 
-RPK_INLINE uint64_t next_u64(Rng& r, RngBlk& b) {
-  if ((r.pos >> 4) != b.blk) rng_load(r, b);
-  const uint32_t i = r.pos & 15u;
-  const uint32_t lo = b.col[i * BLOCK], hi = b.col[(i + 1u) * BLOCK];
-  r.pos += 2;
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
 RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
-RPK_INLINE double gen_f64(Rng& r, RngBlk& b) { return u64_to_f64(next_u64(r, b)); }
-
-// Rejection loops (UnitBall / UnitSphere tries) read their draws straight from the ring: the RING blocks
-// of a lane are one circular run of 16*RING words in its slab, so stream word a sits at ring word
-// a % (16*RING) while its block is held (blocks [end - RING, end)).  A loop makes sure every block its
-// next tries touch is there (ring_ensure: in place generation, rare, as rng_load's fallback), then loads
-// and evaluates RPK_TRIES tries at once and keeps the first accepted one -- the draws consumed, and so the
-// stream, are exactly the sequential loop's.  A wave iterates until its slowest lane accepts: with
+// Every draw reads the ring directly: the RING blocks of a lane are one circular run of 16*RING words in
+// its slab (L2-resident), so stream word a sits at ring word a % (16*RING) while its block is held
+// (blocks [end - RING, end)).  A draw site makes sure every block it touches is there (ring_ensure:
+// generated in place when the refill pass has not made it yet, rare) and loads its u64 words with one
+// dwordx2 each.  Rejection loops (UnitBall / UnitSphere / UnitDisk) load and evaluate RPK_TRIES tries at
+// once and keep the first accepted one -- the draws consumed, and so the stream, are exactly the
+// sequential loop's.  A wave iterates until its slowest lane accepts: with
 // acceptance p a lane needs a geometric number of tries, and the wave's maximum over its ~20 shading lanes
 // is ~5 single tries for the ball (p = pi/6); RPK_TRIES per round cuts the rounds, and each round pays one
 // ring-load latency instead of per-draw block checks and LDS column reloads.
@@ -308,6 +252,10 @@ RPK_INLINE double gen_f64(Rng& r, RngBlk& b) { return u64_to_f64(next_u64(r, b))
 #define RPK_TRIES 2
 #endif
 static_assert(RING * 16 == 128, "ring_u64 indexes the ring as 128 words");
+RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64 from stream words a, a+1 (a even)
+  const uint2 v = reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
+  return u64_to_f64(((uint64_t)v.y << 32) | v.x);
+}
 RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
   while (last_blk >= *r.end) {
     DREG(DREG_RNG_FALLBACK)
@@ -319,9 +267,12 @@ RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
     *r.end = b + 1;
   }
 }
-RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64 from stream words a, a+1 (a even)
-  const uint2 v = reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
-  return u64_to_f64(((uint64_t)v.y << 32) | v.x);
+// One Standard f64 draw (rand 0.8 gen::<f64>, two stream words)
+RPK_INLINE double gen_f64(Rng& r) {
+  ring_ensure(r, r.pos >> 4);
+  const double x = ring_f64(r, r.pos);
+  r.pos += 2;
+  return x;
 }
 
 // ------------------------------------------------------------------ math -------------------------
@@ -820,7 +771,7 @@ RPK_INLINE V3 absorb_eval(const rpl::Material& m, V3 tex) {
 }
 
 // material.rs:27-34, 115-179 Scatter::evaluate.  Returns true and the new direction when scattered.
-RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, RngBlk& rb, V3& nd) {
+RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& rng, V3& nd) {
   switch (m.scatter_kind) {
     case 1: {  // Lambert (material.rs:115-130)
       DREG(DREG_LAMBERT)
@@ -887,7 +838,7 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
       const double x = 1.0 + dot(n, d);
       const double x2 = x * x;
       const double reflectance = r0 + (1.0 - r0) * (x * (x2 * x2));  // powi(5), LLVM binary expansion
-      if (gen_f64(rng, rb) < reflectance) {              // Bernoulli (randomness.rs:78-82)
+      if (gen_f64(rng) < reflectance) {              // Bernoulli (randomness.rs:78-82)
         nd = reflect(d, n);
       } else {
         const double cos_theta = dot(n, d);          // refract (utility.rs:111-119)
@@ -955,7 +906,6 @@ RPK_INLINE KArgsPtr kargs() {
   asm volatile("" : "+s"(p));
   return p;
 }
-RPK_INLINE uint32_t kargs_lds_depth() { return kargs()->S.lds_depth; }
 
 // Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
 // tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
@@ -1008,7 +958,7 @@ RPK_INLINE uint32_t unit_spp(KArgsPtr A, uint32_t batch) {
 // One camera sample (main.rs:75-76): make_uv_jitter draws 2s, 2s+1 of a CLONE of the pixel-start
 // stream (render.rs:74-82) = keystream words 4s..4s+3 = block s/4 at offset 4(s%4); Camera::shoot
 // (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
-RPK_INLINE void start_sample(Rng& rng, RngBlk& rb, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
+RPK_INLINE void start_sample(Rng& rng, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
   DREG(DREG_START_SAMPLE)
   KArgsPtr A = kargs();
   const uint4 jw = rng_jitter(rng, s);
@@ -1128,7 +1078,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   // Camera samples start at the top of the next round, after the refill pass: `start` = sample s is due,
   // `fresh` = and it is the first of a unit whose key and block 0 the refill pass makes.
   bool start = alive, fresh = alive;
-  uint32_t rblk = 0xFFFFFFFFu;  // keystream block held in the top of the lane's stack column (RngBlk)
   DIAG({ uint64_t t = stamp(); ph[0] += t - t_prev; t_prev = t; })
 
   // Every lane of the wave stays in this loop until the whole wave has retired, so the ballots below
@@ -1146,10 +1095,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     }
     if (start) {
       KArgsPtr A = kargs();
-      RngBlk rb(rng_col(stk), rblk);
-      if (fresh) rb.blk = 0xFFFFFFFFu;  // a new stream: block 0 of the column (if any) is another unit's
-      rng_ready(rng, rb);
-      start_sample(rng, rb, s, pipj & 0xFFFFu, pipj >> 16, o, d);
+      start_sample(rng, s, pipj & 0xFFFFu, pipj >> 16, o, d);
       depth = A->P.max_bounce;
       T_x = T_y = T_z = 1.0;
       first = true;
@@ -1259,14 +1205,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         }
         // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
         V3 nd = v3(0.0, 0.0, 0.0);
-        // this ray's keystream block, in registers only around the scatter (the live set of the shading
-        // code is what decides the kernel's register budget)
         bool scattered = false;
-        if (hit) {
-          RngBlk rb(rng_col(stk), rblk);
-          rng_ready(rng, rb);
-          scattered = scatter_eval(*m, d, h, rng, rb, nd);
-        }
+        if (hit) scattered = scatter_eval(*m, d, h, rng, nd);
         V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
         if (t1) {
           DREG(DREG_TEX)
