@@ -238,6 +238,16 @@ RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
 
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
 RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
+// The same value from the two keystream words, as hi * 2^-32 + (lo >> 11) * 2^-53: both terms and the sum
+// k * 2^-53 (k < 2^53) are exact, so the FMA returns the identical double in 2 cvt + 1 mul + 1 FMA.
+RPK_INLINE double words_f64(uint32_t lo, uint32_t hi) {
+  return __builtin_fma((double)hi, 0x1p-32, (double)(lo >> 11) * 0x1p-53);
+}
+// 2 * words_f64 - 1 (the distributions' `2.0 * r - 1.0`, randomness.rs:24,42,61): 2g = k * 2^-52 is exact and
+// so is k * 2^-52 - 1 (a multiple of 2^-52 of magnitude <= 1), whatever the order -- two exact FMAs.
+RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
+  return __builtin_fma((double)hi, 0x1p-31, __builtin_fma((double)(lo >> 11), 0x1p-52, -1.0));
+}
 // Every draw reads the ring directly: the RING blocks of a lane are one circular run of 16*RING words in
 // its slab (L2-resident), so stream word a sits at ring word a % (16*RING) while its block is held
 // (blocks [end - RING, end)).  A draw site makes sure every block it touches is there (ring_ensure:
@@ -252,9 +262,16 @@ RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 900
 #define RPK_TRIES 2
 #endif
 static_assert(RING * 16 == 128, "ring_u64 indexes the ring as 128 words");
-RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64 from stream words a, a+1 (a even)
-  const uint2 v = reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
-  return u64_to_f64(((uint64_t)v.y << 32) | v.x);
+RPK_INLINE uint2 ring_u64(const Rng& r, uint32_t a) {  // stream words a, a+1 (a even)
+  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
+}
+RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64
+  const uint2 v = ring_u64(r, a);
+  return words_f64(v.x, v.y);
+}
+RPK_INLINE double ring_sym(const Rng& r, uint32_t a) {  // 2 * Standard f64 - 1
+  const uint2 v = ring_u64(r, a);
+  return words_sym(v.x, v.y);
 }
 RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
   while (last_blk >= *r.end) {
@@ -784,13 +801,13 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
         double tx[RPK_TRIES], ty[RPK_TRIES];
 #pragma unroll
         for (int j = 0; j < RPK_TRIES; j++) {
-          tx[j] = ring_f64(rng, a + 4u * j);
-          ty[j] = ring_f64(rng, a + 4u * j + 2u);
+          tx[j] = ring_sym(rng, a + 4u * j);
+          ty[j] = ring_sym(rng, a + 4u * j + 2u);
         }
         bool done = false;
 #pragma unroll
         for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
-          const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0, qs = qx * qx + qy * qy;
+          const double qx = tx[j], qy = ty[j], qs = qx * qx + qy * qy;
           if (qs < 1.0) { x = qx; y = qy; s = qs; rng.pos = a + 4u * (j + 1); done = true; }
         }
         if (done) break;
@@ -810,14 +827,14 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, Rng& r
         double tx[RPK_TRIES], ty[RPK_TRIES], tz[RPK_TRIES];
 #pragma unroll
         for (int j = 0; j < RPK_TRIES; j++) {
-          tx[j] = ring_f64(rng, a + 6u * j);
-          ty[j] = ring_f64(rng, a + 6u * j + 2u);
-          tz[j] = ring_f64(rng, a + 6u * j + 4u);
+          tx[j] = ring_sym(rng, a + 6u * j);
+          ty[j] = ring_sym(rng, a + 6u * j + 2u);
+          tz[j] = ring_sym(rng, a + 6u * j + 4u);
         }
         bool done = false;
 #pragma unroll
         for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
-          const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0, qz = 2.0 * tz[j] - 1.0;
+          const double qx = tx[j], qy = ty[j], qz = tz[j];
           if ((qx * qx + qy * qy) + qz * qz < 1.0) { x = qx; y = qy; z = qz; rng.pos = a + 6u * (j + 1); done = true; }
         }
         if (done) break;
@@ -963,8 +980,8 @@ RPK_INLINE void start_sample(Rng& rng, uint32_t s, uint32_t pi, uint32_t pj, V3&
   KArgsPtr A = kargs();
   const uint4 jw = rng_jitter(rng, s);
   const uint32_t w0 = jw.x, w1 = jw.y, w2 = jw.z, w3 = jw.w;
-  const double ju = ((double)pi + u64_to_f64(((uint64_t)w1 << 32) | w0)) / (double)A->P.W;
-  const double jv = ((double)pj + u64_to_f64(((uint64_t)w3 << 32) | w2)) / (double)A->P.H;
+  const double ju = ((double)pi + words_f64(w0, w1)) / (double)A->P.W;
+  const double jv = ((double)pj + words_f64(w2, w3)) / (double)A->P.H;
   double dx = 0.0, dy = 0.0;
   // UnitDisk (randomness.rs:21-34): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
   for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
@@ -972,13 +989,13 @@ RPK_INLINE void start_sample(Rng& rng, uint32_t s, uint32_t pi, uint32_t pj, V3&
     double tx[RPK_TRIES], ty[RPK_TRIES];
 #pragma unroll
     for (int j = 0; j < RPK_TRIES; j++) {
-      tx[j] = ring_f64(rng, a + 4u * j);
-      ty[j] = ring_f64(rng, a + 4u * j + 2u);
+      tx[j] = ring_sym(rng, a + 4u * j);
+      ty[j] = ring_sym(rng, a + 4u * j + 2u);
     }
     bool done = false;
 #pragma unroll
     for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
-      const double qx = 2.0 * tx[j] - 1.0, qy = 2.0 * ty[j] - 1.0;
+      const double qx = tx[j], qy = ty[j];
       if (qx * qx + qy * qy < 1.0) { dx = qx; dy = qy; rng.pos = a + 4u * (j + 1); done = true; }
     }
     if (done) break;

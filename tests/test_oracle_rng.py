@@ -132,3 +132,26 @@ def test_noise_integer_wrapping(oracle):
     for args in [(0, 0, 0, 0), (1, -2, 3, 4), (-7, 123456789, -987654321, 2**40), (2**62, -(2**62), 5, -1)]:
         assert oracle.lib().or_noise_integer(*args) == ref(*args)
     assert oracle.lib().or_noise_real(1, 2, 3, 4) == ref(1, 2, 3, 4) / float(2**63 - 1)
+
+
+def test_kernel_draw_conversion_is_exact():
+    """The kernel's two-FMA forms of rand 0.8's Standard f64 (rp_kernel.hip words_f64 / words_sym) equal
+    `(u >> 11) * 2^-53` and `2.0 * that - 1.0` (randomness.rs:24,42,61) bit for bit: every term is exact.
+    Checked with the host libm's correctly rounded fma over random and edge-case words."""
+    import ctypes
+    import struct
+    libm = ctypes.CDLL("libm.so.6")
+    fma = libm.fma
+    fma.restype = ctypes.c_double
+    fma.argtypes = [ctypes.c_double] * 3
+    rng = np.random.default_rng(7)
+    words = [int(x) for x in rng.integers(0, 2**64, size=20000, dtype=np.uint64)]
+    words += [0, 1, 2**11 - 1, 2**11, 2**32 - 1, 2**32, 2**63, 2**64 - 1, 2**64 - 2**11, 2**64 - 2**11 - 1]
+    bits = lambda x: struct.pack("<d", x)
+    for u in words:
+        lo, hi = u & 0xFFFFFFFF, u >> 32
+        ref = float(u >> 11) * (1.0 / 9007199254740992.0)
+        f = fma(float(hi), 2.0**-32, float(lo >> 11) * 2.0**-53)
+        sym = fma(float(hi), 2.0**-31, fma(float(lo >> 11), 2.0**-52, -1.0))
+        assert bits(f) == bits(ref), u
+        assert bits(sym) == bits(2.0 * ref - 1.0), u
