@@ -136,7 +136,12 @@ static constexpr uint32_t RING = RPK_RING;
 #define RPK_W4
 #endif
 static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
-#ifdef RPK_W4
+// RPK_COLD_LDS (experiment): 4 waves/SIMD with the pixel sum and throughput in LDS; the host then keeps
+// ~19 stack entries in LDS and spills deeper ones (render_blocks_per_cu picks the split).
+#if defined(RPK_W4) && !defined(RPK_COLD_LDS)
+#define RPK_COLD_SLAB
+#endif
+#ifdef RPK_COLD_SLAB
 static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
 #else
 static constexpr uint32_t SLAB_N = SLAB_COLD;
@@ -214,26 +219,25 @@ RPK_INLINE void rng_refill(Rng& r, bool alive, bool fresh, uint64_t seed, uint32
 }
 
 // Jitter words 4s..4s+3 of the pixel-start stream (block s/4).
+// Keystream block b of the lane's key into dst, for the rare draw that finds its block not made yet.  Out
+// of line: the kernel is ~50 KB of code against a 64 KB instruction cache shared by two CUs, and each
+// inlined ChaCha12 is ~2.5 KB that only the fallback paths execute.
+__device__ __attribute__((noinline)) void gen_block(const uint4* slab, uint32_t b, uint4* dst) {
+  const uint4 a = slab[SLAB_KEY], c = slab[SLAB_KEY + 1];
+  const uint32_t k[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  uint32_t w[16];
+  chacha12(k, b, w);
+  store_block(dst, w);
+}
+
 RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
   const uint32_t b = s >> 2;
-  if (r.jtag[(b & 1u) * BLOCK] == b) return jit_slot(r, b)[s & 3u];
-  DREG(DREG_JIT_FALLBACK)
-  uint32_t k[8], w[16];
-  load_key(r, k);
-  chacha12(k, b, w);
-  store_block(jit_slot(r, b), w);
-  r.jtag[(b & 1u) * BLOCK] = b;
-  const uint32_t o = (s & 3u) * 4u;
-  uint4 v = make_uint4(w[0], w[1], w[2], w[3]);
-#pragma unroll
-  for (int q = 1; q < 4; q++) {
-    const bool m = o == 4u * q;
-    v.x = m ? w[4 * q] : v.x;
-    v.y = m ? w[4 * q + 1] : v.y;
-    v.z = m ? w[4 * q + 2] : v.z;
-    v.w = m ? w[4 * q + 3] : v.w;
+  if (r.jtag[(b & 1u) * BLOCK] != b) {
+    DREG(DREG_JIT_FALLBACK)
+    gen_block(r.slab, b, jit_slot(r, b));
+    r.jtag[(b & 1u) * BLOCK] = b;
   }
-  return v;
+  return jit_slot(r, b)[s & 3u];
 }
 
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
@@ -277,10 +281,7 @@ RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
   while (last_blk >= *r.end) {
     DREG(DREG_RNG_FALLBACK)
     const uint32_t b = *r.end;
-    uint32_t k[8], w[16];
-    load_key(r, k);
-    chacha12(k, b, w);
-    store_block(ring_slot(r, b), w);
+    gen_block(r.slab, b, ring_slot(r, b));
     *r.end = b + 1;
   }
 }
@@ -1046,7 +1047,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   // ---- lane state: one pixel's path at a time.  Hot state (ray, throughput, radiance, traversal)
   // in registers; cold per-pixel state (pixel sum, slot/pixel/sample counters, keystream cursors) in
   // LDS, structure-of-arrays so every access is bank-conflict-free; keystream blocks in the slab.
-#ifndef RPK_W4
+#ifndef RPK_COLD_SLAB
   __shared__ double c_sum[3 * BLOCK];
   __shared__ double c_T[3 * BLOCK];
 #endif
@@ -1058,7 +1059,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   uint32_t& s = c_u[3 * BLOCK + tid];
   uint32_t& hits = c_u[4 * BLOCK + tid];
   uint32_t& batch = c_u[2 * BLOCK + tid];
-#ifdef RPK_W4
+#ifdef RPK_COLD_SLAB
   double* cold = reinterpret_cast<double*>(reinterpret_cast<uint4*>(kargs()->S.rng_slab) +
                                            ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N + SLAB_COLD);
   double& sum_x = cold[0];
