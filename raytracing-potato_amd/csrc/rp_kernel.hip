@@ -260,8 +260,8 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 // once and keep the first accepted one -- the draws consumed, and so the stream, are exactly the
 // sequential loop's.  A wave iterates until its slowest lane accepts: with
 // acceptance p a lane needs a geometric number of tries, and the wave's maximum over its ~20 shading lanes
-// is ~5 single tries for the ball (p = pi/6); RPK_TRIES per round cuts the rounds, and each round pays one
-// ring-load latency instead of per-draw block checks and LDS column reloads.
+// is ~5 single tries for the ball (p = pi/6); each round pays one ring-load latency.  (Before, a draw
+// checked its block and the wave copied a 16-word block into LDS whenever any lane crossed one.)
 #ifndef RPK_TRIES
 #define RPK_TRIES 2
 #endif
