@@ -146,7 +146,19 @@ static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput
 #else
 static constexpr uint32_t SLAB_N = SLAB_COLD;
 #endif
-static constexpr uint32_t RNG_CRIT = 2;    // a lane holding <= this many blocks forces a refill pass
+#ifndef RPK_RNG_CRIT
+#define RPK_RNG_CRIT 2
+#endif
+static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
+// Traversal wave-level exits (trav_step): leave the inner-node loop once at most RPK_LEAF_BREAK lanes of the
+// wave still look for a leaf (C3: 0 -> 3 is -2.7 % frame time), and the leaf loop once at most
+// RPK_PRIM_BREAK lanes still test primitives (their remaining run is parked as a leaf entry).
+#ifndef RPK_LEAF_BREAK
+#define RPK_LEAF_BREAK 3
+#endif
+#ifndef RPK_PRIM_BREAK
+#define RPK_PRIM_BREAK 0
+#endif    // a lane holding <= this many blocks forces a refill pass
 static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // ... as do this many lanes with room
 
 struct Rng {
@@ -422,6 +434,8 @@ struct TravState {
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
 };
 
+RPK_INLINE bool trav_done(const TravState& t) { return t.cur == rpl::ENTRY_EMPTY && t.leaf == 0u; }
+
 RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
   t.best = tmax;
   t.bu = 0.0;
@@ -496,8 +510,8 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const uint32_t* stk, uint32_t strid
   return (!SPILL || i < S.lds_depth) ? stk[i * stride] : S.spill[spl + i - S.lds_depth];
 }
 
-// One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY (the
-// parked leaf is always consumed inside a step).  `spl`: the lane's first spill entry (SPILL kernels).
+// One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
+// parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
 template <bool SPILL>
 RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
@@ -596,7 +610,9 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
       leaf = cur;
       cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
     }
-    if (__ballot(leaf == 0u) == 0) break;
+    // ... and once at most RPK_LEAF_BREAK lanes still look for one, the wave moves on to the leaves: the
+    // last few descents ran with most of the wave idle (those lanes resume their descent next step)
+    if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= RPK_LEAF_BREAK) break;
 #endif
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
@@ -622,6 +638,11 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
         leaf = 0u;
       }
     }
+    if (RPK_PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= RPK_PRIM_BREAK) {
+      // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
+      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
+      break;
+    }
   }
   ts.cur = cur;
   ts.sp = sp;
@@ -635,7 +656,7 @@ RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, 
   setup_ray32(o, d, tmin, r);
   TravState t;
   trav_init(S, tmax, t);
-  while (t.cur != rpl::ENTRY_EMPTY) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
+  while (!trav_done(t)) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
   hr.u = t.bu;
   hr.v = t.bv;
@@ -1138,7 +1159,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 #else
           trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
 #endif
-          tdone = ts.cur == rpl::ENTRY_EMPTY;
+          tdone = trav_done(ts);
         }
         const uint64_t act = __ballot(alive && !tdone);
         const uint64_t waiting = __ballot(alive && tdone);
