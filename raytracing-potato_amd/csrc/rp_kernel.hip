@@ -613,6 +613,9 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
     // ... and once at most RPK_LEAF_BREAK lanes still look for one, the wave moves on to the leaves: the
     // last few descents ran with most of the wave idle (those lanes resume their descent next step)
     if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= RPK_LEAF_BREAK) break;
+#ifdef RPK_NODE_BREAK  // experiment: leave once at most this many lanes are still descending at all
+    if ((uint32_t)__popcll(__ballot(true)) <= RPK_NODE_BREAK) break;
+#endif
 #endif
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
