@@ -19,7 +19,7 @@ namespace rpb {
 struct BuildOptions {
   uint32_t max_leaf = 4;        // primitives per leaf at most (<= rpl::LEAF_MAX)
   uint32_t bins = 32;           // SAH bins per axis
-  double cost_traverse = 1.0;   // relative cost of one node (two child boxes)
+  double cost_traverse = 0.7;   // relative cost of one node (two child boxes); C3 sweep 0.35-1.5: 0.7 best (-1..2 %)
   double cost_intersect = 1.0;  // relative cost of one primitive test
   bool tables_only = false;     // shading tables only (nodes/prims left empty: the device builder makes them)
 };
