@@ -278,6 +278,7 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   // tuning knobs for experiments (the defaults are the measured best): leaf size and SAH cost ratio
   if (const char* e = std::getenv("RP_BVH_MAX_LEAF")) opt.max_leaf = (uint32_t)std::strtoul(e, nullptr, 10);
   if (const char* e = std::getenv("RP_BVH_COST_TRAVERSE")) opt.cost_traverse = std::strtod(e, nullptr);
+  if (const char* e = std::getenv("RP_ALWAYS_MAX")) opt.always_max = (uint32_t)std::strtoul(e, nullptr, 10);
   rc = rpb::build(desc, opt, ps, err);
   if (rc != RP_OK) return fail(rc, err);
 
@@ -336,6 +337,8 @@ int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   s->ks.texels = s->d_texels;
   s->ks.background = ps.background;
   s->ks.root = ps.root;
+  s->ks.always_first = ps.always_first;  // 0 / 0 for a device-built tree
+  s->ks.n_always = ps.n_always;
   // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
   // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;

@@ -407,12 +407,40 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     for (int k = 0; k < 3; k++) refs[i].c[k] = 0.5 * (refs[i].box.lo[k] + refs[i].box.hi[k]);
     refs[i].id = i;
   }
+  // always-tested primitives (BuildOptions::always_max): out of the tree, appended after its leaves
+  std::vector<uint32_t> always;
+  if (opt.always_max > 0 && n > 1) {
+    const uint32_t m = std::min<uint32_t>(opt.always_max, n - 1);
+    std::vector<uint32_t> idx(n);
+    for (uint32_t i = 0; i < n; i++) idx[i] = i;
+    std::partial_sort(idx.begin(), idx.begin() + m, idx.end(),
+                      [&](uint32_t a, uint32_t b) { return refs[a].box.area() > refs[b].box.area(); });
+    Box rest;
+    rest.reset();
+    for (uint32_t i = m; i < n; i++) rest.grow(refs[idx[i]].box);
+    const double ra = rest.area();
+    for (uint32_t j = 0; j < m; j++)
+      if (std::isfinite(refs[idx[j]].box.area()) && refs[idx[j]].box.area() > 0.0 &&
+          refs[idx[j]].box.area() >= opt.always_ratio * ra)
+        always.push_back(idx[j]);
+    std::sort(always.begin(), always.end());
+    if (!always.empty()) {
+      std::vector<Ref> tree_refs;
+      tree_refs.reserve(n - always.size());
+      for (uint32_t i = 0, a = 0; i < n; i++) {
+        if (a < always.size() && always[a] == i) { a++; continue; }
+        tree_refs.push_back(refs[i]);
+      }
+      refs.swap(tree_refs);
+    }
+  }
+  const uint32_t n_tree = (uint32_t)refs.size();
   std::vector<uint32_t> order;
   order.reserve(n);
   std::vector<BinNode> bin;
-  bin.reserve(n ? 2 * (size_t)n : 1);
+  bin.reserve(n_tree ? 2 * (size_t)n_tree : 1);
   Builder B{opt, refs, bin, order};
-  if (n == 0) {
+  if (n_tree == 0) {
     rpl::Node4 root{};
     for (int c = 0; c < 4; c++) {
       root.lo_x[c] = root.lo_y[c] = root.lo_z[c] = std::numeric_limits<float>::infinity();
@@ -425,7 +453,7 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     Box all;
     all.reset();
     for (auto& r : refs) all.grow(r.box);
-    B.build(0, n, all);
+    B.build(0, n_tree, all);
     out.nodes.reserve(bin.size() / 2 + 1);
     Collapser C{bin, out.nodes};
     C.emit(0, 0);
@@ -433,6 +461,9 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   }
   out.root = 0;
   out.n_leaves = B.n_leaves;
+  out.always_first = (uint32_t)order.size();
+  out.n_always = (uint32_t)always.size();
+  for (uint32_t a : always) order.push_back(a);
 
   // ---- primitives in leaf order
   out.prims.resize(order.size() ? order.size() : 1);
@@ -586,7 +617,7 @@ int check(const PackedScene& s, std::string& err) {
       st.push_back({n.child[c], it.depth + 1, (int)it.entry, c});
     }
   }
-  size_t expect = s.prims.size();
+  size_t expect = s.prims.size() - s.n_always;  // the always-tested tail is outside the tree
   if (np != expect && !(np == 0 && s.prims.size() == 1)) {
     err = "primitive count mismatch";
     return RP_EINTERNAL;

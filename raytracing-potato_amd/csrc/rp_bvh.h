@@ -22,6 +22,11 @@ struct BuildOptions {
   double cost_traverse = 0.7;   // relative cost of one node (two child boxes); C3 sweep 0.35-1.5: 0.7 best (-1..2 %)
   double cost_intersect = 1.0;  // relative cost of one primitive test
   bool tables_only = false;     // shading tables only (nodes/prims left empty: the device builder makes them)
+  // Primitives kept out of the tree and tested first for every ray: among the always_max largest boxes
+  // (surface area), those at least always_ratio times the area of the box of everything else (config C3's
+  // ground sphere, r = 1000 under a bunny of size ~0.2).  always_max = 0 disables.
+  uint32_t always_max = 4;
+  double always_ratio = 4.0;
 };
 
 struct PackedScene {
@@ -36,6 +41,7 @@ struct PackedScene {
   rpl::Emit background{};
   uint32_t root = 0;
   uint32_t max_depth = 0;             // deepest wide node (root = 0)
+  uint32_t always_first = 0, n_always = 0;  // prims[always_first, +n_always): outside the tree, tested first
   uint64_t n_leaves = 0;
 };
 

@@ -440,6 +440,47 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
     float best32 = up(best);
     int64_t bestp = -1;
     uint64_t visits = 0, tests = 0;
+    auto test = [&](uint32_t k) {
+      tests++;
+      const rpl::Prim& p = ps.prims[k];
+      if (p.kind == rpl::PRIM_TRIANGLE) {
+        const double* g = p.g;
+        const double pa[3] = {g[0] - o[0], g[1] - o[1], g[2] - o[2]};
+        const double ba[3] = {g[3], g[4], g[5]}, ca[3] = {g[6], g[7], g[8]};
+        double det = ba[0] * ca[1] * d[2] + ba[1] * ca[2] * d[0] + ba[2] * ca[0] * d[1] - ba[0] * ca[2] * d[1] -
+                     ba[1] * ca[0] * d[2] - ba[2] * ca[1] * d[0];
+        if (std::fabs(det) < 1e-7) return;
+        double inv_det = 1.0 / det;
+        double t = (pa[0] * (ba[1] * ca[2] - ba[2] * ca[1]) + pa[1] * (ba[2] * ca[0] - ba[0] * ca[2]) +
+                    pa[2] * (ba[0] * ca[1] - ba[1] * ca[0])) * inv_det;
+        double u = (pa[0] * (ca[1] * d[2] - ca[2] * d[1]) + pa[1] * (ca[2] * d[0] - ca[0] * d[2]) +
+                    pa[2] * (ca[0] * d[1] - ca[1] * d[0])) * inv_det;
+        double v = (pa[0] * (ba[2] * d[1] - ba[1] * d[2]) + pa[1] * (ba[0] * d[2] - ba[2] * d[0]) +
+                    pa[2] * (ba[1] * d[0] - ba[0] * d[1])) * inv_det;
+        double w = 1.0 - u - v;
+        if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) return;
+        best = t;
+        bestp = ps.prim_refs[k].src;
+      } else {
+        const double tc[3] = {o[0] - p.g[0], o[1] - p.g[1], o[2] - p.g[2]};
+        double a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
+        double hb = (d[0] * tc[0] + d[1] * tc[1]) + d[2] * tc[2];
+        double cq = ((tc[0] * tc[0] + tc[1] * tc[1]) + tc[2] * tc[2]) - p.g[3] * p.g[3];
+        double delta = hb * hb - a * cq;
+        if (delta <= 0.0) return;
+        double sq = std::sqrt(delta);
+        double t = (-hb - sq) / a;
+        if (t < tmin || t > best) {
+          t = (-hb + sq) / a;
+          if (t < tmin || t > best) return;
+        }
+        best = t;
+        bestp = ps.prim_refs[k].src;
+      }
+      best32 = up(best);
+    };
+    // the always-tested primitives first (rp_bvh.h BuildOptions::always_max), as the kernel does
+    for (uint32_t k = ps.always_first; k < ps.always_first + ps.n_always; k++) test(k);
     std::vector<uint32_t> stack;
     uint32_t cur = ps.root;
     for (;;) {
@@ -471,45 +512,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
       }
       if (cur == rpl::ENTRY_EMPTY) break;
       const uint32_t first = cur & rpl::LEAF_FIRST_MASK, cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
-      for (uint32_t k = first; k < first + cnt; k++) {
-        tests++;
-        const rpl::Prim& p = ps.prims[k];
-        if (p.kind == rpl::PRIM_TRIANGLE) {
-          const double* g = p.g;
-          const double pa[3] = {g[0] - o[0], g[1] - o[1], g[2] - o[2]};
-          const double ba[3] = {g[3], g[4], g[5]}, ca[3] = {g[6], g[7], g[8]};
-          double det = ba[0] * ca[1] * d[2] + ba[1] * ca[2] * d[0] + ba[2] * ca[0] * d[1] - ba[0] * ca[2] * d[1] -
-                       ba[1] * ca[0] * d[2] - ba[2] * ca[1] * d[0];
-          if (std::fabs(det) < 1e-7) continue;
-          double inv_det = 1.0 / det;
-          double t = (pa[0] * (ba[1] * ca[2] - ba[2] * ca[1]) + pa[1] * (ba[2] * ca[0] - ba[0] * ca[2]) +
-                      pa[2] * (ba[0] * ca[1] - ba[1] * ca[0])) * inv_det;
-          double u = (pa[0] * (ca[1] * d[2] - ca[2] * d[1]) + pa[1] * (ca[2] * d[0] - ca[0] * d[2]) +
-                      pa[2] * (ca[0] * d[1] - ca[1] * d[0])) * inv_det;
-          double v = (pa[0] * (ba[2] * d[1] - ba[1] * d[2]) + pa[1] * (ba[0] * d[2] - ba[2] * d[0]) +
-                      pa[2] * (ba[1] * d[0] - ba[0] * d[1])) * inv_det;
-          double w = 1.0 - u - v;
-          if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) continue;
-          best = t;
-          bestp = ps.prim_refs[k].src;
-        } else {
-          const double tc[3] = {o[0] - p.g[0], o[1] - p.g[1], o[2] - p.g[2]};
-          double a = (d[0] * d[0] + d[1] * d[1]) + d[2] * d[2];
-          double hb = (d[0] * tc[0] + d[1] * tc[1]) + d[2] * tc[2];
-          double cq = ((tc[0] * tc[0] + tc[1] * tc[1]) + tc[2] * tc[2]) - p.g[3] * p.g[3];
-          double delta = hb * hb - a * cq;
-          if (delta <= 0.0) continue;
-          double sq = std::sqrt(delta);
-          double t = (-hb - sq) / a;
-          if (t < tmin || t > best) {
-            t = (-hb + sq) / a;
-            if (t < tmin || t > best) continue;
-          }
-          best = t;
-          bestp = ps.prim_refs[k].src;
-        }
-        best32 = up(best);
-      }
+      for (uint32_t k = first; k < first + cnt; k++) test(k);
       if (stack.empty()) cur = rpl::ENTRY_EMPTY;
       else { cur = stack.back(); stack.pop_back(); }
     }

@@ -497,6 +497,18 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
   }
 }
 
+// A new ray: the always-tested primitives (KScene::n_always: boxes that dwarf the rest of the scene, kept
+// out of the tree by the host builder) get their exact tests here, one wave-uniform loop over the same
+// primitive for every starting lane, instead of a divergent leaf test deep in the prim loop; their hit
+// also bounds the traversal from the root.  The closest hit is the tree's (any test order, up to exact-t
+// ties).
+RPK_INLINE void trav_begin(const KScene& S, V3 o, V3 d, double tmin, double tmax, TravState& t) {
+  trav_init(S, tmax, t);
+  double best = t.best;
+  for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++) prim_test(S, k, o, d, tmin, best, t);
+  t.best = best;
+}
+
 // Stack entry i of a lane: in its LDS column (entry i at stk[i * stride]) or, for SPILL kernels, entries
 // >= S.lds_depth in the lane's global overflow run (S.spill[spl + i - lds_depth], L2-resident) -- a deep
 // tree (config C5: 43 entries) then keeps the LDS of four blocks per CU.
@@ -658,7 +670,7 @@ RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, 
   Ray32 r;
   setup_ray32(o, d, tmin, r);
   TravState t;
-  trav_init(S, tmax, t);
+  trav_begin(S, o, d, tmin, tmax, t);
   while (!trav_done(t)) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
   hr.u = t.bu;
@@ -936,6 +948,8 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.background.color[1] = A->S.background.color[1];
   S.background.color[2] = A->S.background.color[2];
   S.root = A->S.root;
+  S.always_first = A->S.always_first;
+  S.n_always = A->S.n_always;
   S.stack_depth = A->S.stack_depth;
   S.lds_depth = A->S.lds_depth;
   S.spill = A->S.spill;
@@ -1117,6 +1131,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
   pipj = pi | (pj << 16);
   bool tdone = true;  // traversal of the current ray finished (or no ray)
+  bool newray = false;  // a ray started since the last traversal round (always-tested prims pending)
   // Camera samples start at the top of the next round, after the refill pass: `start` = sample s is due,
   // `fresh` = and it is the first of a unit whose key and block 0 the refill pass makes.
   bool start = alive, fresh = alive;
@@ -1143,6 +1158,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       first = true;
       trav_init(load_scene(A), INF, ts);
       tdone = false;
+      newray = true;
       start = fresh = false;
     }
     DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
@@ -1152,6 +1168,15 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       const uint32_t thr = A->P.trav_threshold;
       // the lane's spill run (SPILL kernels): lane index x spill entries per lane
       const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + tid) * (S.stack_depth - S.lds_depth) : 0u;
+      // camera rays and scattered rays started since the last round: the always-tested primitives (trav_begin),
+      // at one site for both
+      if (newray) {
+        double best = ts.best;
+        for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++)
+          prim_test(S, k, o, d, RAY_EPSILON, best, ts);
+        ts.best = best;
+        newray = false;
+      }
       Ray32 r;
       setup_ray32(o, d, RAY_EPSILON, r);
       for (;;) {
@@ -1334,6 +1359,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       } else {
         trav_init(load_scene(kargs()), INF, ts);
         tdone = false;
+        newray = true;
       }
     }
     n_samples += (uint64_t)__popcll(__ballot(ended_sample));

@@ -295,10 +295,24 @@ def test_device_bvh_builder(gpu, monkeypatch, name, arg):
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
 def test_spilled_traversal_stack(gpu, monkeypatch, name, arg):
     """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
-    deep trees such as C5's use): forced here with RP_LDS_DEPTH=17, so nearly every traversal spills and
-    the keystream block in the column's top is clobbered by almost every ray -- same image as the oracle."""
+    deep trees such as C5's use): forced here with RP_LDS_DEPTH=17, so nearly every traversal spills --
+    same image as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
     monkeypatch.setenv("RP_LDS_DEPTH", "17")
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
     _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED))
+
+
+@pytest.mark.parametrize("always_max", ["0", "4"])
+def test_always_tested_primitives(gpu, monkeypatch, always_max):
+    """Primitives whose box dwarfs the rest of the scene (the C3 ground sphere) are kept out of the tree and
+    tested first for every ray (rp_bvh.h BuildOptions::always_max, the default 4); RP_ALWAYS_MAX=0 puts
+    them back in the tree.  Same image as the oracle either way, on the full-materials bunny scene (ground,
+    two balls, bunny) and on two_balls (a scene of two spheres only)."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    monkeypatch.setenv("RP_ALWAYS_MAX", always_max)
+    for name in ("bunny_full", "two_balls"):
+        sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
+        _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED))
