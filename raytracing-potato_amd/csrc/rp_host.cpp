@@ -497,7 +497,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
             tnear = std::fmax(tnear, std::fmin(a, b));
             tfar = std::fmin(tfar, std::fmax(a, b));
           }
-          const bool hit = tnear <= std::fma(std::fabs(tfar), 0x1p-19f, tfar) + slack && nd.child[c] != rpl::ENTRY_EMPTY;
+          const bool hit = std::fma(tnear, 1.0f - 0x1p-19f, -slack) <= tfar && nd.child[c] != rpl::ENTRY_EMPTY;
           tn[c] = hit ? tnear : INFINITY;
           cc[c] = nd.child[c];
         }

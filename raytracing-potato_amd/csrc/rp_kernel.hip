@@ -361,8 +361,13 @@ struct TravDiag {
 // t^ = fma(lo, inv, -oinv).  Against the exact t = (lo - o) / d:
 //     |t^ - t| <= 5u |t| + |o - o32| |inv| (1 + 6u) + u |o32 inv|        (u = 2^-24)
 // so with D = max over axes of the last two terms, a box whose exact interval meets [t_min, best] at
-// some t* > 0 satisfies  tnear^ - tfar^ <= 10u t* + 2D  <=  2^-19 |tfar^| + 3D.  The test below passes
-// every such box (it may pass a few more): no primitive the reference's f64 test reaches is culled.
+// some t* > 0 satisfies  tnear^ <= t*(1 + 5u) + D  and  tfar^ >= t*(1 - 5u) - D  (the near planes behind
+// the origin and tmin32 <= t* do not raise tnear^; every far plane lies at or beyond t*).  The test
+//     fma(tnear^, 1 - 2^-19, -slack) <= tfar^                    (slack >= 3D)
+// then passes every such box: its exact left side is <= t*(1+5u)(1-2^-19) + D - slack <= t*(1-5u) - 2D
+// - 22u t*, which leaves 22u t* + D to absorb the FMA's rounding (<= u (tnear^ + slack)).  It may pass a
+// few more boxes, never fewer: no primitive the reference's f64 test reaches is culled.  An empty slot
+// (lo = +inf, hi = -inf) gives tnear^ = +inf, tfar^ = -inf and fails.
 // Slopes are clamped to |inv| <= 2^64 (axis-parallel rays), so every t^ is finite.
 struct Ray32 {
   float ix, iy, iz;     // rcp(fl(d))
@@ -569,13 +574,12 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
         TN[q][e] = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
         TF[q][e] = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
       }
-      // tnear <= tfar + 2^-19 |tfar| + slack (section 4.2 of DESIGN.md), as packed FMA + add
-      const f2 lim = pk_fma(f2{fabsf(TF[q][0]), fabsf(TF[q][1])}, f2{0x1p-19f, 0x1p-19f}, TF[q]) +
-                     f2{r.slack, r.slack};
+      // fma(tnear, 1 - 2^-19, -slack) <= tfar (section 4.2 of DESIGN.md): one packed FMA per pair
+      const f2 lhs = pk_fma(TN[q], f2{1.0f - 0x1p-19f, 1.0f - 0x1p-19f}, f2{-r.slack, -r.slack});
 #pragma unroll
       for (int e = 0; e < 2; e++) {
         const int c = 2 * q + e;
-        tn[c] = TN[q][e] <= lim[e] ? TN[q][e] : __builtin_huge_valf();
+        tn[c] = lhs[e] <= TF[q][e] ? TN[q][e] : __builtin_huge_valf();
       }
     }
     // sort (tn, entry) ascending: misses (+inf) go last
