@@ -158,6 +158,9 @@ static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
 #endif
 #ifndef RPK_PRIM_BREAK
 #define RPK_PRIM_BREAK 0
+#endif
+#ifndef RPK_BATCH_BELOW
+#define RPK_BATCH_BELOW 64
 #endif    // a lane holding <= this many blocks forces a refill pass
 static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // ... as do this many lanes with room
 
@@ -529,7 +532,7 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const uint32_t* stk, uint32_t strid
 
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
-template <bool SPILL>
+template <bool SPILL, bool BATCH = false>
 RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
@@ -661,6 +664,69 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
       // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
       if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
       break;
+    }
+    // batched variant: the sequential loop runs while many lanes test; the stragglers' runs are batched
+    if (BATCH && (uint32_t)__popcll(__ballot(leaf != 0u)) <= RPK_BATCH_BELOW) break;
+  }
+  if (BATCH) {
+    // Batched leaf tests (experiment, RPK_BATCH_LEAF; all 64 lanes of the wave call this, lanes without a
+    // leaf as helpers): every lane's current run [k, kend) becomes jobs P..P+n-1 (P = exclusive prefix of
+    // the runs' sizes over the lanes), lane L takes job base + L, finds the owner (largest lane with
+    // P <= job) by a 6-step ds_bpermute search, tests the owner's ray against the owner's best, and each
+    // owner reduces its results in job order (min t, a later primitive wins a tie: the sequential order).
+    const uint32_t lane = __lane_id();
+    while (__ballot(leaf != 0u)) {
+      const uint32_t n = leaf != 0u ? kend - k : 0u;  // 1..8
+      uint32_t P = 0, T = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint64_t m = __ballot((n >> b) & 1u);
+        P += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+        T += (uint32_t)__popcll(m) << b;
+      }
+      for (uint32_t base = 0; base < T; base += 64u) {
+        DIAG(if (td) td->tests++;)
+        DREG(DREG_PRIM)
+        const uint32_t j = base + lane;
+        uint32_t own = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+          const uint32_t cand = own + step;
+          if ((uint32_t)__shfl((int)P, (int)cand) <= j) own = cand;
+        }
+        const uint32_t Po = (uint32_t)__shfl((int)P, (int)own), ko = (uint32_t)__shfl((int)k, (int)own);
+        const V3 oo = v3(__shfl(o.x, (int)own), __shfl(o.y, (int)own), __shfl(o.z, (int)own));
+        const V3 dd = v3(__shfl(d.x, (int)own), __shfl(d.y, (int)own), __shfl(d.z, (int)own));
+        double bt = __shfl(best, (int)own);
+        TravState tmp;
+        tmp.bestp = -1;
+        tmp.bu = 0.0;
+        tmp.bv = 0.0;
+        if (j < T) prim_test(S, ko + (j - Po), oo, dd, tmin, bt, tmp);
+        const double tres = tmp.bestp >= 0 ? bt : __builtin_nan("");
+        // owners: results of jobs P + i in this round, in order
+        int win = -1;
+        for (uint32_t i = 0; __ballot(i < n); i++) {
+          const uint32_t jj = P + i;
+          const bool mine = i < n && jj >= base && jj < base + 64u;
+          const double ti = __shfl(tres, (int)((jj - base) & 63u));
+          if (mine && ti <= best) { best = ti; win = (int)(jj - base); }
+        }
+        const double uw = __shfl(tmp.bu, win & 63), vw = __shfl(tmp.bv, win & 63);
+        const int pw = __shfl(tmp.bestp, win & 63);
+        if (win >= 0) { ts.bestp = pw; ts.bu = uw; ts.bv = vw; }
+      }
+      // every run is done: the next leaf of each lane, as the sequential loop chains them
+      if (leaf != 0u) {
+        if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+          leaf = cur;
+          cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+          k = leaf & rpl::LEAF_FIRST_MASK;
+          kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+        } else {
+          leaf = 0u;
+        }
+      }
     }
   }
   ts.cur = cur;
@@ -1131,6 +1197,12 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   hits = 0;
   sum_x = sum_y = sum_z = 0.0;
   TravState ts;
+  ts.cur = rpl::ENTRY_EMPTY;  // no ray: done (RPK_BATCH_LEAF steps every lane)
+  ts.leaf = 0u;
+  ts.sp = 0u;
+  ts.best = 0.0;
+  ts.bestp = -1;
+  ts.bu = ts.bv = 0.0;
   uint32_t pi = 0, pj = 0;
   bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
   pipj = pi | (pj << 16);
@@ -1184,6 +1256,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       Ray32 r;
       setup_ray32(o, d, RAY_EPSILON, r);
       for (;;) {
+#ifdef RPK_BATCH_LEAF
+        // every lane steps (idle lanes hold cur = EMPTY, no leaf: they only help with the leaf tests)
+        {
+          DREG(DREG_STEP)
+          trav_step<SPILL, true>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+          if (alive) tdone = trav_done(ts);
+        }
+#else
         if (alive && !tdone) {
           DREG(DREG_STEP)
 #ifdef RPK_DIAG
@@ -1193,6 +1273,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 #endif
           tdone = trav_done(ts);
         }
+#endif
         const uint64_t act = __ballot(alive && !tdone);
         const uint64_t waiting = __ballot(alive && tdone);
         if (act == 0 || (waiting != 0 && (uint32_t)__popcll(act) < thr)) break;
