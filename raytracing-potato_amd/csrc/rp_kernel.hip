@@ -129,16 +129,18 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 #define RPK_RNG_BATCH 48
 #endif
 static constexpr uint32_t RING = RPK_RING;
-// Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs; the pixel sum and path throughput live in
-// the lane's slab instead of LDS, and a few cold values spill to scratch) -- measured 3.7% faster on C3
-// than 3 waves/SIMD with that state in LDS (-DRPK_W3).
+// Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs) -- measured 3.7% faster on C3 than
+// 3 waves/SIMD with the whole traversal stack in LDS (-DRPK_W3).
 #ifndef RPK_W3
 #define RPK_W4
 #endif
 static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
-// RPK_COLD_LDS (experiment): 4 waves/SIMD with the pixel sum and throughput in LDS; the host then keeps
-// ~19 stack entries in LDS and spills deeper ones (render_blocks_per_cu picks the split).
-#if defined(RPK_W4) && !defined(RPK_COLD_LDS)
+// The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS; the
+// host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to the lane's global run
+// (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).  -DRPK_COLD_IN_SLAB keeps them
+// in the keystream slab instead (v31 and before): C3 +2.6 %, C5 +4.6 % frame time -- the slab shrinks
+// from 720 to 672 B per lane and the shading site loses 6 global loads and 6 stores.
+#if defined(RPK_W4) && defined(RPK_COLD_IN_SLAB)
 #define RPK_COLD_SLAB
 #endif
 #ifdef RPK_COLD_SLAB
@@ -280,9 +282,9 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 #ifndef RPK_TRIES
 #define RPK_TRIES 2
 #endif
-static_assert(RING * 16 == 128, "ring_u64 indexes the ring as 128 words");
+static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * RING words (a power of two)");
 RPK_INLINE uint2 ring_u64(const Rng& r, uint32_t a) {  // stream words a, a+1 (a even)
-  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & 127u) >> 1];
+  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RING - 1u)) >> 1];
 }
 RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64
   const uint2 v = ring_u64(r, a);
