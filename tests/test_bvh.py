@@ -159,3 +159,24 @@ def test_wide_tree_is_shallow():
     # 4 971 hittables: the 4-wide SAH tree (node cost 0.7 of a primitive test, rp_bvh.h) has ~1 700 nodes
     # at depth 8; the reference's binary median tree has 9 937 nodes at depth 14
     assert depth <= 12 and nodes < 2000, list(st)
+
+
+def test_giant_primitives_tested_first():
+    """The host builder keeps primitives whose box dwarfs the rest of the scene out of the tree and tests
+    them first for every ray (rp_bvh.h BuildOptions::always_max): in the C3 scene the ground sphere
+    (r = 1000) is tested by every ray, including rays that miss every box of the tree; in earth (one
+    sphere, nothing to single out) a ray that misses the root tests nothing."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    for name, always in (("bunny_full", True), ("earth", False)):
+        scene = scenes.CATALOGUE[name]()
+        rays = _rays_for(scene, 2000, 9)
+        rays[:1000, 3:6] = np.array([0.0, 1.0, 0.0])  # straight up: misses the bunny and both balls
+        rays[:1000, 0:3] = np.array([0.0, 5.0, 0.0])
+        d = scene.desc()
+        out = np.zeros((len(rays), 3), dtype=np.uint64)
+        F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), out.ctypes.data))
+        if always:
+            assert (out[:, 1] >= 1).all()
+        else:
+            assert (out[:1000, 1] == 0).all()
