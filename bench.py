@@ -5,21 +5,25 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one frame of the config (1920x1080x256 spp bunny scene with full materials by default),
-tile-sharded across the N ranks (tile t -> rank t % N, strong scaling: the frame is fixed), rendered
-by the persistent HIP kernel (librp.so) from scene data resident in HBM, followed by the RCCL
-output stage (to_srgb_u8 -> B, G, R, A bytes, rp_shard_to_bgra8), the RCCL all-gather of those 4 bytes
-per pixel and the device-side de-interleave into frame order (the body of the reference's output.tga).  With N > 1 two frames
-are in flight (frame k renders on stream k % 2 with its own rp_workspace), so the end of one frame -- its
-last units leave most of a small shard's GPU idle -- overlaps the start of the next (--inflight).  The
-timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over
-ranks is used.
+tile-sharded across the N ranks (tile t -> rank t % N, strong scaling: the frame is fixed), rendered by the
+persistent HIP kernel (librp.so) from scene data resident in HBM, followed by librp's frame gather
+(rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
+xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
+output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the
+RCCL communicator and takes the barrier and max-time reduction.  With N > 1 two frames are in flight (frame
+k renders on stream k % 2 with its own rp_workspace), so the end of one frame overlaps the start of the
+next (--inflight).  The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both
+sides; the max over ranks is used.
 
-Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays /
-time.  roofline: algorithmic bytes per launch (the reference traversal's per-ray event counts,
-tests/golden/event_counts.json, x SURVEY.md 8d bytes per event, x rays in the launch) / the render
-kernel's average duration measured with HIP events on the stream it runs on.  cpu_baseline: the CPU
-oracle's restatement of the reference driver (main.rs:36-106: LIFO tile queue, 4 worker threads) on a
-bounded sample of the same scene, rank 0, N = 1 only.
+Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays / time.
+roofline: the render kernel's measured memory-side traffic per ray (rocprofv3 PMC record
+committed under profiles/, tools/roofline.py) x this launch's rays / the launch's duration measured with HIP
+events on its stream, against the 8 TB/s HBM peak; beside it the VALU-issue fraction from the same record's
+SQ counters (the bound of the cache-resident bunny configs) and, for reference, the rate the reference's
+own traversal would need (its event counts x SURVEY.md 8d bytes per event).  cpu_baseline: the CPU
+oracle's -O3 restatement of the reference driver (main.rs:36-106: LIFO tile queue, worker threads with
+their own StdRng) on a bounded sample of the same scene, at the reference's 4 workers and at 16, rank 0,
+N = 1 only.
 """
 from __future__ import annotations
 
@@ -36,46 +40,78 @@ sys.path[:0] = [REPO, os.path.join(REPO, "raytracing-potato_amd")]
 
 METRIC = "Mrays/s at 1920×1080×256spp bunny scene; 1/2/4/8-GPU scaling + %HBM roofline"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-FP64_VECTOR_PEAK_TF = 78.6   # spec-sheet FP64 vector (not in the container guide)
-# SURVEY.md 8d algorithmic bytes / flops per event (reference f64 layout)
+SIMDS = 1024                 # 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9             # MI355X_MICROARCH.md max clock
+# a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md "Wave scheduling")
+VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
+# SURVEY.md 8d algorithmic bytes per event of the REFERENCE traversal (reference tree, f64 layout)
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
-FLOPS = {"box_tests": 25, "tri_tests": 81, "sphere_tests": 25, "tri_hits": 0, "texels": 0}
+CPU_WORKERS = (4, 16)        # main.rs:27 num_workers = 4; 16 = the GPU box's CPU share per GPU
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_per_ray(config: str):
+def reference_equivalent(config: str):
+    """Bytes per ray the reference's own traversal would fetch (tests/golden/event_counts.json)."""
     ev = json.load(open(os.path.join(REPO, "tests", "golden", "event_counts.json")))
-    per = ev[config]["per_ray"]
-    return (sum(BYTES[k] * per[k] for k in BYTES), sum(FLOPS[k] * per[k] for k in FLOPS), ev[config])
+    per = ev["C3" if config == "C4" else config]["per_ray"]
+    return sum(BYTES[k] * per[k] for k in BYTES)
 
 
-def pmc_traffic(config: str):
-    """HBM-side bytes per launch of the frame kernel from the committed rocprofv3 PMC record
-    (tools/pmc_traffic.py: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), or None."""
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"{config.lower()}_pmc_traffic.json")), reverse=True):
+def kernel_record(config: str):
+    """The newest committed per-ray record of the frame kernel for this config (tools/roofline.py over
+    rocprofv3 --pmc passes): memory-side bytes per ray, VALU / SALU instructions per ray, cycle budget."""
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"{config.lower()}_roofline.json")), reverse=True):
         rec = json.load(open(f))
-        return rec["traffic_bytes"], os.path.relpath(f, REPO), rec.get("git")
-    return None, None, None
+        rec["source"] = os.path.relpath(f, REPO)
+        return rec
+    return None
 
 
-def cpu_baseline(config: str, spp: int, workers: int):
-    """The reference driver restated (oracle): 1920x1080 at `spp`, `workers` threads."""
+def host_cpu():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        phys = len({(l.split(":")[1].strip()) for l in open("/proc/cpuinfo") if l.startswith("core id")}) or None
+        sockets = len({(l.split(":")[1].strip()) for l in open("/proc/cpuinfo") if l.startswith("physical id")}) or 1
+        phys = phys * sockets if phys else None
+    except OSError:
+        phys = None
+    return {"model": model, "logical_cpus": os.cpu_count(), "physical_cores": phys,
+            "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
+def cpu_baseline(config: str, spp: int, workers_list):
+    """The reference driver restated (oracle, -O3, no per-event counters): 1920x1080 at `spp`."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     scene, params = scenes.config_scene(config)
     d = scene.desc()
-    os_ = O.OracleScene(d.addr(), d)
+    os_ = O.OracleScene(d.addr(), d, fast=True)
     cam = scene.camera.to_c()
-    secs, ctr, _ = os_.baseline(ctypes.addressof(cam), params.width, params.height, spp, params.max_bounce, 32,
-                                workers, params.seed)
+    runs = []
+    for workers in workers_list:
+        secs, ctr, _ = os_.baseline(ctypes.addressof(cam), params.width, params.height, spp, params.max_bounce, 32,
+                                    workers, params.seed)
+        runs.append({"workers": workers, "value": ctr["rays"] / secs / 1e6, "seconds": round(secs, 3),
+                     "rays": ctr["rays"]})
+        log(f"[rank 0] cpu baseline {workers} workers: {runs[-1]['value']:.2f} Mrays/s in {secs:.1f}s")
     os_.close()
-    return {"value": ctr["rays"] / secs / 1e6, "unit": "Mrays/s", "cores": workers, "kind": "port",
-            "sample": f"{config} scene {params.width}x{params.height}x{spp}spp (GPU runs {params.spp}spp), "
-                      f"{ctr['rays']} rays in {secs:.2f}s; C restatement of main.rs:36-106 (tile queue, "
-                      f"{workers} workers = main.rs:27 default); Rust reference unbuildable here"}
+    best = max(runs, key=lambda r: r["value"])
+    return {"value": best["value"], "unit": "Mrays/s", "cores": best["workers"], "kind": "port",
+            "sample": f"{config} scene {params.width}x{params.height}x{spp}spp (GPU runs {params.spp}spp); C "
+                      f"restatement (-O3, oracle/liboracle_fast.so) of main.rs:36-106: LIFO tile queue of 32x32 "
+                      f"tiles, one StdRng per worker; runs at {', '.join(str(w) for w in workers_list)} workers "
+                      f"(main.rs:27 default 4); value = the faster run; Rust reference unbuildable here",
+            "runs": runs, "host": host_cpu()}
 
 
 def main():
@@ -85,63 +121,63 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
-    ap.add_argument("--cpu-spp", type=int, default=4)
-    ap.add_argument("--cpu-workers", type=int, default=4)
+    ap.add_argument("--cpu-spp", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 2 on several)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the multi-rank path on a one-GPU box (never for measurements): every rank on device
-    # RP_BENCH_DEVICE, collectives over RP_BENCH_BACKEND (gloo)
-    if "RP_BENCH_DEVICE" in os.environ:
-        local = int(os.environ["RP_BENCH_DEVICE"])
-    backend = os.environ.get("RP_BENCH_BACKEND", "nccl")
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")  # bootstrap + barrier + max-time only; frames move over librp's RCCL
 
     from dataclasses import replace
+    from rtpotato import _ffi as F
     from rtpotato import scenes
-    from rtpotato.dist import FrameAssembler, shard_params
+    from rtpotato.dist import bootstrap_comm, shard_params
     from rtpotato.render import DeviceScene
 
+    options = {}
+    for kv in args.opt:
+        k, v = kv.split("=", 1)
+        options[k] = float(v) if k == "cost_traverse" else (v if k == "builder" else int(v))
     scene, params = scenes.config_scene(args.config)
     if args.spp:
         params = replace(params, spp=args.spp)
     t = time.time()
-    ds = DeviceScene(scene, device=local)
+    ds = DeviceScene(scene, device=local, options=options)
     info = ds.info()
     log(f"[rank {rank}] scene ready in {time.time() - t:.2f}s: {info}")
     sp = shard_params(params, rank, world)
-    asm = FrameAssembler(params, world, dev)
-    # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the
-    # end of one frame (its last units leave most of the GPU idle) overlaps the start of the next; the
-    # frame assembly (RCCL all-gather + scatter) runs on the main stream in frame order.  F = 1 is the
-    # plain sequential loop.
-    F = args.inflight if args.inflight > 0 else (1 if world == 1 else 2)
+    comm = bootstrap_comm(rank, world, local)
+    # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
+    # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
+    # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.
+    F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 2)
     main_stream = torch.cuda.current_stream(dev)
-    streams = [main_stream] if F == 1 else [torch.cuda.Stream(dev) for _ in range(F)]
-    wss = [None] + [ds.workspace() for _ in range(F - 1)]
-    bufs = [asm.new_shard_buffer() for _ in range(F)]
-    bgras = [asm.new_bgra_buffer() for _ in range(F)]
-    ctrs = [torch.zeros(8, dtype=torch.int64, device=dev) for _ in range(F)]
-    freed = [None] * F  # event: the assembly of the buffer's previous frame is done
+    streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
+    wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
+    for w in wss:
+        ds.reserve(sp, w)  # batch sums + gather staging: nothing is allocated inside the timed loop
+    from rtpotato.scene import shard_slot_count
+    nslots = shard_slot_count(sp)
+    bufs = [torch.zeros(3 * max(1, nslots), dtype=torch.float64, device=dev) for _ in range(F_)]
+    ctrs = [torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev) for _ in range(F_)]
+    freed = [None] * F_  # event: the gather of the buffer's previous frame is done
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
     def step(k_start=None, k_end=None):
-        i = state["k"] % F
+        i = state["k"] % F_
         state["k"] += 1
         st = streams[i]
         if freed[i] is not None:
@@ -151,12 +187,13 @@ def main():
         ds.render_device(sp, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         if k_end is not None:
             k_end.record(st)
-        ds.to_bgra8(sp, bufs[i], bgras[i], stream=st)  # output stage: to_srgb_u8 bytes in TGA order
         if st is not main_stream:
             done = torch.cuda.Event()
             done.record(st)
             main_stream.wait_event(done)
-        asm.gather_bgra(bgras[i], out=frame)
+        # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks), on the main stream
+        ds.frame_gather(comm, sp, bufs[i], frame_bgra=frame, counters=ctrs[i], stream=main_stream,
+                        workspace=wss[i])
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 
@@ -177,29 +214,45 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps / 1e3
-    if F > 1:
+    if F_ > 1:
         # overlapping frames: a frame's events also span the neighbour frames' work, so the kernel rate is
         # priced on the per-frame throughput time instead
         kernel_s = elapsed / args.steps
-    c = ctrs[0].cpu().tolist()
-    rays_step, samples_step, status = c[0], c[1], c[3]
-    if status != 0:
-        raise RuntimeError(f"render kernel reported status {status}")
-    stats = torch.tensor([float(rays_step), float(samples_step)], dtype=torch.float64, device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    cs = [c.cpu().tolist() for c in ctrs]
+    bad = [c[3] for c in cs if c[3] != 0]
+    if bad:
+        raise RuntimeError(f"render kernel reported status {bad}")
+    rays_step, samples_step = cs[0][0], cs[0][1]  # summed over the ranks by rp_frame_gather
+    tmax = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    total_rays_step, total_samples_step = stats.tolist()
     elapsed_max = float(tmax.item())
-    value = total_rays_step * args.steps / elapsed_max / 1e6
+    value = rays_step * args.steps / elapsed_max / 1e6
 
     if rank == 0:
-        # C4 renders the C3 scene; every other config has its own reference-traversal event counts
-        bpr, fpr, ev = algorithmic_per_ray("C3" if args.config == "C4" else args.config)
-        achieved_gbs = bpr * rays_step / kernel_s / 1e9
-        traffic, traffic_src, traffic_git = pmc_traffic(args.config) if args.spp == 0 else (None, None, None)
-        achieved_tf = fpr * rays_step / kernel_s / 1e12
+        local_rays = rays_step / world  # this rank's launch (shards are balanced by the tile interleave)
+        rec = kernel_record(args.config) if args.spp == 0 else None
+        roof = {"bound": "valu" if args.config != "C5" else "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": None, "traffic": None,
+                "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3)}
+        if rec:
+            traffic = rec["traffic_bytes_per_ray"] * local_rays
+            achieved = traffic / kernel_s / 1e9
+            issue = rec["valu_per_ray"] * local_rays / kernel_s
+            roof.update({
+                "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": round(traffic),
+                "traffic_bytes_per_ray": round(rec["traffic_bytes_per_ray"], 1),
+                "valu_issue": {"achieved": round(issue / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                               "unit": "Gwave-inst/s", "frac": round(issue / VALU_ISSUE_PEAK, 4),
+                               "valu_per_ray": round(rec["valu_per_ray"], 2)},
+                "cycle_budget": rec.get("cycle_budget"),
+                "source": f"{rec['source']} (rocprofv3 PMC, build {rec.get('git')}; per-ray figures x this "
+                          f"launch's rays / its HIP-event duration)"})
+        ref_bpr = reference_equivalent(args.config)
+        roof["reference_equivalent"] = {
+            "bytes_per_ray": round(ref_bpr, 1), "GBps": round(ref_bpr * local_rays / kernel_s / 1e9, 1),
+            "note": "bytes the reference's own traversal (its median-split tree, 1 primitive per leaf, f64 "
+                    "boxes) would fetch per ray at this ray rate; not traffic and not a roofline fraction"}
         out = {
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
@@ -208,30 +261,20 @@ def main():
             "config": {"workload": f"{args.config}: {scenes.CONFIGS[args.config].description}",
                        "width": params.width, "height": params.height, "spp": params.spp,
                        "max_bounce": params.max_bounce, "seed": params.seed,
-                       "parallelism": f"tile-sharded x{world} + RCCL all-gather" if world > 1 else "1 GPU",
-                       "frames_in_flight": F,
+                       "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
+                       "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
-                       "rays_per_frame": int(total_rays_step), "rays_per_sample": total_rays_step / total_samples_step},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src and f"{traffic_src} (rocprofv3 PMC, build {traffic_git})",
-                         "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3),
-                         "bytes_per_ray": round(bpr, 1),
-                         "note": ("achieved = the reference traversal's algorithmic bytes per ray (SURVEY 8d) x rays / "
-                                  "kernel time; the wide SAH tree visits ~9x fewer boxes and the bunny scene is "
-                                  "cache-resident, so it exceeds HBM peak; traffic = measured memory-side bytes; the "
-                                  "kernel is FP64/VALU-issue bound (fp64_vector)") if args.config != "C5" else
-                                 (f"10M-triangle scene ({info['device_bytes'] / 1e9:.2f} GB device data, deep BVH, "
-                                  "beyond the 256 MB Infinity Cache): the memory-bound config")},
-            "fp64_vector": {"achieved": round(achieved_tf, 3), "peak": FP64_VECTOR_PEAK_TF, "unit": "TFLOP/s",
-                            "frac": round(achieved_tf / FP64_VECTOR_PEAK_TF, 4), "flops_per_ray": round(fpr, 1)},
+                       "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
+                       "scene_options": options or "defaults"},
+            "roofline": roof,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
             log("[rank 0] cpu baseline ...")
-            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_spp, args.cpu_workers)
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_spp, CPU_WORKERS)
             out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
         print(json.dumps(out), flush=True)
+    comm.close()
     ds.close()
     if world > 1:
         dist.destroy_process_group()

@@ -19,15 +19,20 @@
  *   - Ownership: the caller owns every buffer it passes.  rp_scene_create deep-copies the scene into
  *     device memory (HBM); the scene is immutable afterwards.
  *   - Determinism (the RNG contract): the samples of pixel (i, j) are drawn in batches of
- *     RP_SAMPLES_PER_STREAM; batch b (samples 32b .. 32b+31) is rendered with its own
- *     StdRng::seed_from_u64(params.seed + b*width*height + j*width + i) (rand 0.8 StdRng = ChaCha12) and
- *     the unchanged per-pixel body of main.rs:70-85 over its samples (make_uv_jitter from a clone of the
- *     batch stream's start).  The pixel value is (S_0 + S_1 + ...) / spp, batch sums added in batch
- *     order (main.rs:80,86).  For spp <= 32 this is one stream per pixel, seed + j*width + i.  Output
- *     depends only on (scene, camera, seed, width, height, spp, max_bounce) -- never on tiling, sharding,
- *     device count or scheduling.  (The reference draws every pixel of a worker's tiles from one
- *     from_entropy() stream, main.rs:52, so its output is not reproducible; a pixel's samples are
- *     sequential in a stream, so batching them is what lets one pixel's work spread over lanes/GPUs.)
+ *     N = params.samples_per_stream (0 -> RP_SAMPLES_PER_STREAM = 32); batch b (samples N*b .. N*b+N-1)
+ *     is rendered with its own StdRng::seed_from_u64(params.seed + b*width*height + j*width + i)
+ *     (rand 0.8 StdRng = ChaCha12) and the unchanged per-pixel body of main.rs:70-85 over its samples
+ *     (make_uv_jitter from a clone of the batch stream's start).  The pixel value is (S_0 + S_1 + ...) /
+ *     spp, batch sums added in batch order (main.rs:80,86).  With N >= spp (e.g. samples_per_stream =
+ *     spp) this is SURVEY.md 8c's one stream per pixel, seed + j*width + i, for any spp.  Output depends
+ *     only on (scene, camera, seed, width, height, spp, max_bounce, samples_per_stream) -- never on
+ *     tiling, sharding, device count, scheduling or the environment.  (The reference draws every pixel of
+ *     a worker's tiles from one from_entropy() stream, main.rs:52, so its output is not reproducible; a
+ *     pixel's samples are sequential in a stream, so batching them is what lets one pixel's work spread
+ *     over lanes/GPUs: the default 32 keeps an 8-GPU shard's longest unit short.)
+ *   - No allocation happens inside the asynchronous calls (rp_render_device*, rp_frame_gather,
+ *     rp_render_gather): device memory they need is reserved up front (rp_workspace_reserve), so they
+ *     can be captured into a hipGraph and never synchronise the device.
  *   - Arithmetic is IEEE binary64 throughout, as the reference (utility.rs:14 `type Real = f64`).
  *   - Image layout: row-major, pixel (i, j) at index j*width + i, row j = 0 is the BOTTOM row
  *     (image.rs:31-33, main.rs:119, tga::save writes bottom-left origin).  RGB are linear f64 averages
@@ -43,10 +48,20 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 3
+#define RP_ABI_VERSION 4
 
-/* Samples per RNG stream (see "Determinism" above). */
+/* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
+
+/* Device counter block of the asynchronous renders: RP_COUNTERS_LEN uint64 {rays, samples, pixels,
+ * status}.  Nothing else is written through the pointer (the unit queue lives in the workspace). */
+#define RP_COUNTERS_LEN 4
+enum { RP_CTR_RAYS = 0, RP_CTR_SAMPLES = 1, RP_CTR_PIXELS = 2, RP_CTR_STATUS = 3 };
+/* status bits */
+#define RP_STATUS_STACK_OVERFLOW 1u
+
+/* Bytes of an RCCL unique id (rp_comm_unique_id). */
+#define RP_COMM_ID_BYTES 128
 
 typedef enum rp_status {
   RP_OK = 0,
@@ -54,7 +69,8 @@ typedef enum rp_status {
   RP_EHIP = -2,      /* HIP runtime error */
   RP_ENOMEM = -3,    /* host or device allocation failed */
   RP_ENODEV = -4,    /* no usable gfx950 device */
-  RP_EINTERNAL = -5  /* kernel reported an internal error (e.g. traversal stack overflow) */
+  RP_EINTERNAL = -5, /* kernel reported an internal error (e.g. traversal stack overflow) */
+  RP_ERCCL = -6      /* RCCL (collective communication) error */
 } rp_status;
 
 /* ---------------------------------------------------------------- scene description ----------- */
@@ -163,7 +179,27 @@ typedef struct rp_render_params {
   uint64_t seed;            /* base seed of the RNG contract */
   uint32_t tile_w, tile_h;  /* 0 -> 32 (main.rs:26) */
   uint32_t shard, num_shards;/* num_shards 0 -> 1 */
+  uint32_t samples_per_stream; /* RNG contract batch size N, 0 -> RP_SAMPLES_PER_STREAM; N >= spp: one
+                                  stream per pixel */
+  uint32_t reserved;        /* 0 */
 } rp_render_params;
+
+/* Scene build and kernel tuning options (rp_scene_create_ex).  None of them changes an image beyond
+ * exact-t ties between primitives (the closest hit does not depend on the tree).
+ * Zero-initialised fields take the defaults; rp_scene_options_init fills them in explicitly. */
+enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2 };
+typedef struct rp_scene_options {
+  uint32_t builder;         /* RP_BUILDER_*: AUTO = host binned SAH below 2^20 hittables, device LBVH above */
+  uint32_t max_leaf;        /* primitives per leaf, 1..8 (0 -> 4) */
+  double cost_traverse;     /* SAH node cost relative to a primitive test (0 -> 0.7) */
+  int32_t always_max;       /* primitives tested before the tree for every ray (-1 -> 4; 0 = none) */
+  uint32_t lds_depth;       /* traversal-stack entries kept in LDS (0 -> automatic; >= 17 forces a split) */
+  uint32_t self_check;      /* 1: structural self-check of a device-built tree (slow; tests) */
+  uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24) */
+  uint32_t tile_order;      /* 0 = cost-ordered tiles (probe launch + sort), 1 = plain shard order */
+  uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
+  uint32_t reserved[4];
+} rp_scene_options;
 
 typedef struct rp_stats {
   uint64_t rays;      /* root scene.hit() calls, primary + secondary (render.rs:105,133) */
@@ -181,8 +217,11 @@ const char* rp_last_error(void);
 int rp_device_count(int* count);
 
 /* Build the acceleration structure and copy the scene to device `device`.  Validates every index the
- * reference would bounds-check (material/mesh/texture ids, triangle offsets, checker recursion). */
+ * reference would bounds-check (material/mesh/texture ids, triangle offsets, checker recursion).
+ * rp_scene_create uses the default options; the library reads no environment variables. */
 int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out);
+int rp_scene_options_init(rp_scene_options* opt);
+int rp_scene_create_ex(const rp_scene_desc* desc, int device, const rp_scene_options* opt, rp_scene** out);
 void rp_scene_destroy(rp_scene* scene);
 /* Acceleration-structure statistics: node count, leaf count, max depth, primitive count. */
 int rp_scene_info(const rp_scene* scene, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth,
@@ -197,32 +236,38 @@ int rp_shard_unpack(const rp_render_params* params, const double* shard_buf, uin
 
 /* Render synchronously into host memory.  out_rgb: width*height*3 doubles (only the shard's pixels are
  * written).  out_foreground (nullable): width*height floats, fraction of samples whose first ray hit
- * geometry (main.rs:81-87).  stats nullable. */
+ * geometry (main.rs:81-87).  stats nullable.  Reserves the scene workspace for params as needed. */
 int rp_render(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
               double* out_rgb, float* out_foreground, rp_stats* stats);
 
 /* Asynchronous device-resident render on `stream` (a hipStream_t, NULL = default stream) of the scene's
  * device.  d_shard_rgb: shard_pixel_count*3 doubles in device memory, compact shard order.
- * d_shard_fg (nullable): shard_pixel_count floats.  d_counters (nullable): 4 uint64 in device memory
- * that receive {rays, samples, pixels, status}; they are zeroed on the stream before the launch.
- * No host synchronisation or copy happens inside.  A frame with spp > RP_SAMPLES_PER_STREAM needs
- * 3 doubles + 1 uint32 per pixel and batch of workspace memory, allocated by the first call that needs
- * it: render once before capturing such calls into a hipGraph. */
+ * d_shard_fg (nullable): shard_pixel_count floats.  d_counters (nullable): RP_COUNTERS_LEN uint64 in
+ * device memory that receive {rays, samples, pixels, status}; they are zeroed on the stream before the
+ * launch.  No host synchronisation, copy or allocation happens inside.  A frame of more than one sample
+ * batch (spp > samples_per_stream) keeps 3 doubles + 1 uint32 per pixel and batch in the workspace:
+ * reserve them first (rp_workspace_reserve), else the call returns RP_EINVAL. */
 int rp_render_device(rp_scene* scene, const rp_camera* camera, const rp_render_params* params,
                      double* d_shard_rgb, float* d_shard_fg, uint64_t* d_counters, void* stream);
 
 /* Frames in flight.  A render's per-frame device state -- the keystream cache of the resident lanes,
- * the unit-queue counters, the cost-probe and tile-order buffers, the multi-batch sums -- lives in a
- * workspace.  The scene owns one, which rp_render and rp_render_device use (their frames must therefore
- * be ordered on one stream).  Frames rendered with different workspaces may run concurrently on
- * different streams: the end of one frame, when its last units leave most of the GPU idle, then
- * overlaps the start of the next.  A workspace serves one frame at a time (the caller orders its reuse
- * on streams); destroy workspaces before their scene.  Same arguments and results as rp_render_device. */
+ * the unit queues, the cost-probe and tile-order buffers, the multi-batch sums, the gather staging of
+ * rp_frame_gather -- lives in a workspace.  The scene owns one, which rp_render and rp_render_device use
+ * (their frames must therefore be ordered on one stream).  Frames rendered with different workspaces may
+ * run concurrently on different streams: the end of one frame, when its last units leave most of the GPU
+ * idle, then overlaps the start of the next.  A workspace serves one frame at a time (the caller orders
+ * its reuse on streams); destroy workspaces before their scene.  Same arguments and results as
+ * rp_render_device. */
 int rp_workspace_create(rp_scene* scene, rp_workspace** out);
 void rp_workspace_destroy(rp_workspace* workspace);
 int rp_render_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
                         const rp_render_params* params, double* d_shard_rgb, float* d_shard_fg,
                         uint64_t* d_counters, void* stream);
+/* Reserve the device memory renders of `params`' shape need in `workspace` (NULL = the scene's own):
+ * the multi-batch sums of the shard and, when params->num_shards > 1, the staging buffers rp_frame_gather
+ * uses for this frame size.  Synchronous (allocates; may free a smaller reservation); idempotent for a
+ * shape it already covers.  rp_render reserves for itself. */
+int rp_workspace_reserve(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params);
 
 /* Output stage on the device: the reference's to_srgb_u8 (utility.rs:212-220, alpha 255) of every slot of
  * a compact shard buffer, bytes in tga::save's pixel order B, G, R, A (image.rs:116-137), so a gathered
@@ -247,6 +292,58 @@ int rp_intersect(rp_scene* scene, const double* rays, uint64_t n, double* out_hi
  * {fetch, new sample, traverse, shade, tail}, wave loop iterations, active lanes at traversal,
  * traversal wave-trips, lane node visits, lane primitive tests.  Synchronises the device. */
 int rp_diagnostics(rp_scene* scene, uint64_t* out, uint32_t n, int reset);
+
+/* ---------------------------------------------------------------- multi-GPU -- */
+/* Image tiles are interleaved across the GPUs (tile t -> rank t % nranks, params.shard = rank), every
+ * GPU holds its own copy of the scene, and one RCCL all-gather over xGMI per frame moves the shards;
+ * each rank then de-interleaves them into frame order on its device.  This replaces the reference's
+ * thread tile queue (main.rs:36-106, num_workers main.rs:27).  The per-pixel RNG contract makes the
+ * gathered frame bitwise identical for any number of GPUs. */
+typedef struct rp_comm rp_comm;     /* opaque: one rank's RCCL communicator (one device) */
+typedef struct rp_multi rp_multi;   /* opaque: a scene on several devices of this process + communicator */
+
+/* One process per GPU (torch.distributed / MPI style): rank 0 makes the id, every rank receives its bytes
+ * out of band and joins.  `device` is the rank's HIP device (the scene's). */
+int rp_comm_unique_id(uint8_t id[RP_COMM_ID_BYTES]);
+int rp_comm_create(const uint8_t id[RP_COMM_ID_BYTES], int nranks, int rank, int device, rp_comm** out);
+void rp_comm_destroy(rp_comm* comm);
+int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
+
+/* Collective over all ranks of `comm`, asynchronous on `stream` (every rank must call it, in the same
+ * order relative to its other collectives on comm).  params: this rank's shard (shard = rank, num_shards
+ * = nranks), the workspace reserved for it (rp_workspace_reserve).  d_shard_rgb: the rank's finished
+ * shard (rp_render_device_ws output).  Outputs (either nullable, on the rank's device, frame order, row 0
+ * = bottom): d_frame_bgra width*height*4 bytes = to_srgb_u8 in tga::save byte order (rp_shard_to_bgra8)
+ * -- the body of output.tga; d_frame_rgb width*height*3 linear f64.  d_counters (nullable): the rank's
+ * RP_COUNTERS_LEN counters, summed over the ranks in place. */
+int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                    const double* d_shard_rgb, uint8_t* d_frame_bgra, double* d_frame_rgb,
+                    uint64_t* d_counters, void* stream);
+/* The frame assembly step alone, for callers that move the shards with their own collective (MPI, a
+ * torch.distributed all-gather): d_gathered holds params->num_shards shard buffers of `stride` slots each
+ * (rp_gather_stride: the largest shard, shard 0), rank r's at slot r * stride, `words_per_slot` 32-bit words
+ * per slot (1 for the BGRA8 bytes of rp_shard_to_bgra8, 6 for f64 RGB); d_frame receives width*height
+ * slots in frame order.  Asynchronous on `stream`, on the current device. */
+int rp_gather_stride(const rp_render_params* params, uint64_t* stride);
+int rp_frame_assemble(const rp_render_params* params, const void* d_gathered, uint32_t words_per_slot,
+                      void* d_frame, void* stream);
+
+/* rp_render_device_ws into the workspace's shard buffer, then rp_frame_gather, on one stream. */
+int rp_render_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
+                     const rp_render_params* params, uint8_t* d_frame_bgra, double* d_frame_rgb,
+                     uint64_t* d_counters, void* stream);
+
+/* One process, several GPUs (the reference's single-process model): a scene copy per device, one
+ * communicator over them (ncclCommInitAll), one stream per device. */
+int rp_multi_create(const rp_scene_desc* desc, const int* devices, int n_devices, const rp_scene_options* opt,
+                    rp_multi** out);
+void rp_multi_destroy(rp_multi* multi);
+/* Synchronous frame on every device of `multi` (params.shard / num_shards are ignored: device k renders
+ * shard k of n_devices).  out_rgb (nullable): width*height*3 doubles on the host, frame order; out_bgra
+ * (nullable): width*height*4 bytes (to_srgb_u8, tga::save order).  stats (nullable): summed counters,
+ * seconds = wall time of the frame. */
+int rp_render_multi(rp_multi* multi, const rp_camera* camera, const rp_render_params* params,
+                    double* out_rgb, uint8_t* out_bgra, rp_stats* stats);
 
 #ifdef __cplusplus
 }

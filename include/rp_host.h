@@ -57,6 +57,12 @@ int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats);
  * rp_intersect) writes n x 3 {node records visited, primitive tests, closest hittable id or 2^64-1}. */
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray);
 
+/* rand 0.8 StdRng (ChaCha12, rand_chacha 0.3 stream: 64-bit block counter, zero nonce) keyed by the 32-byte
+ * seed (StdRng::from_seed; seed_from_u64 seeds come from its PCG32 expansion): n consecutive next_u64
+ * draws starting at draw index `first` (two keystream words each, little-endian).  Host bulk scene
+ * generation (the synthetic C5 mesh: 120 M draws); multi-threaded. */
+int rph_stdrng_u64(const uint8_t seed[32], uint64_t first, uint64_t n, uint64_t* out);
+
 const char* rph_last_error(void);
 
 #ifdef __cplusplus

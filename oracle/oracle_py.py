@@ -12,11 +12,12 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.path.join(HERE, "liboracle.so")            # parity checker (-O2, per-event counters)
+LIB_FAST = os.path.join(HERE, "liboracle_fast.so")  # timed CPU baseline (-O3, no per-event counters)
 N_COUNTERS = 7  # rays, box tests, triangle tests, sphere tests, samples, triangle hits, texel fetches
 COUNTER_NAMES = ["rays", "box_tests", "tri_tests", "sphere_tests", "samples", "tri_hits", "texels"]
 
-_lib = None
+_libs = {}
 
 
 class _Rng(ctypes.Structure):
@@ -29,13 +30,13 @@ def build() -> str:
     return LIB
 
 
-def lib() -> ctypes.CDLL:
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB):
+def lib(fast: bool = False) -> ctypes.CDLL:
+    if fast in _libs:
+        return _libs[fast]
+    path = LIB_FAST if fast else LIB
+    if not os.path.exists(path):
         build()
-    L = ctypes.CDLL(LIB)
+    L = ctypes.CDLL(path)
     vp, u64, u32, i32, dbl = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_double
     L.or_chacha_block.argtypes = [vp, u64, u64, u32, vp]
     L.or_chacha_block.restype = None
@@ -78,7 +79,7 @@ def lib() -> ctypes.CDLL:
     L.or_free.restype = None
     L.or_to_srgb_u8.argtypes = [vp, u64, vp]
     L.or_to_srgb_u8.restype = None
-    _lib = L
+    _libs[fast] = L
     return L
 
 
@@ -141,15 +142,17 @@ def stream_u64(seed: int, n: int) -> np.ndarray:
 class OracleScene:
     """or_scene built from an rp_scene_desc (ctypes struct address, e.g. rtpotato SceneDesc.addr())."""
 
-    def __init__(self, desc_addr: int, keepalive=None):
+    def __init__(self, desc_addr: int, keepalive=None, fast: bool = False):
+        """fast: the -O3 build without per-event counters (the timed CPU baseline)."""
         self._keep = keepalive
-        self.h = lib().or_scene_create(desc_addr)
+        self._lib = lib(fast)
+        self.h = self._lib.or_scene_create(desc_addr)
         if not self.h:
             raise ValueError("or_scene_create failed")
 
     def close(self):
         if self.h:
-            lib().or_scene_destroy(self.h)
+            self._lib.or_scene_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -160,7 +163,7 @@ class OracleScene:
 
     def info(self):
         nn, d = ctypes.c_uint32(), ctypes.c_uint32()
-        lib().or_scene_info(self.h, ctypes.byref(nn), ctypes.byref(d))
+        self._lib.or_scene_info(self.h, ctypes.byref(nn), ctypes.byref(d))
         return {"nodes": nn.value, "depth": d.value}
 
     def intersect(self, rays: np.ndarray):
@@ -168,7 +171,7 @@ class OracleScene:
         hits = np.empty((len(r), 9))
         mats = np.empty(len(r), dtype=np.uint32)
         ctr = np.zeros(N_COUNTERS, dtype=np.uint64)
-        lib().or_intersect(self.h, r.ctypes.data, len(r), hits.ctypes.data, mats.ctypes.data, ctr.ctypes.data)
+        self._lib.or_intersect(self.h, r.ctypes.data, len(r), hits.ctypes.data, mats.ctypes.data, ctr.ctypes.data)
         return hits, mats, dict(zip(COUNTER_NAMES, ctr.tolist()))
 
     def render(self, camera_addr: int, params_addr: int, width: int, height: int, threads: int = 8,
@@ -176,7 +179,7 @@ class OracleScene:
         rgb = np.zeros((height, width, 3))
         fg = np.zeros((height, width), dtype=np.float32) if foreground else None
         ctr = np.zeros(N_COUNTERS, dtype=np.uint64)
-        rc = lib().or_render(self.h, camera_addr, params_addr, rgb.ctypes.data,
+        rc = self._lib.or_render(self.h, camera_addr, params_addr, rgb.ctypes.data,
                              fg.ctypes.data if fg is not None else None, ctr.ctypes.data, threads)
         if rc != 0:
             raise ValueError("or_render failed")
@@ -187,7 +190,7 @@ class OracleScene:
         """The reference driver (main.rs:36-106) timed: (seconds, counters, image or None)."""
         img = np.zeros((height, width, 3)) if want_image else None
         ctr = np.zeros(N_COUNTERS, dtype=np.uint64)
-        secs = lib().or_render_baseline(self.h, camera_addr, width, height, spp, max_bounce, tile, workers, seed,
+        secs = self._lib.or_render_baseline(self.h, camera_addr, width, height, spp, max_bounce, tile, workers, seed,
                                         img.ctypes.data if img is not None else None, ctr.ctypes.data)
         return secs, dict(zip(COUNTER_NAMES, ctr.tolist())), img
 

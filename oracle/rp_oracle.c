@@ -19,6 +19,15 @@
 #include <string.h>
 #include <time.h>
 
+/* Per-event counters (box / triangle / sphere tests, triangle hits, texels) for the algorithmic-bytes
+ * figures (tests/golden/event_counts.json).  The timed CPU baseline (liboracle_fast.so) is built with
+ * -DOR_NO_EVENT_COUNTERS so it runs the reference's work and nothing more; rays and samples are always
+ * counted (the Mrays/s numerator). */
+#ifdef OR_NO_EVENT_COUNTERS
+#define OR_EVENT(C, k) ((void)0)
+#else
+#define OR_EVENT(C, k) ((C)->c[k]++)
+#endif
 
 /* ================================================================ RNG ======================== */
 
@@ -355,38 +364,85 @@ static aabb_t hittable_bbox(const or_scene* s, const rp_hittable* h) {
 
 typedef struct { uint32_t leaf; aabb_t box; } content_t;
 
-static int g_sort_axis;
-/* bvh.rs:58-67 split: sort by centroid along the axis.  Rust's sort_unstable_by orders equal centroids in
- * an implementation-defined way; ties are broken by leaf id here (tree shape is not part of the contract:
- * SURVEY.md 8a A9). */
-static int cmp_centroid(const void* pa, const void* pb) {
-  const content_t* a = (const content_t*)pa;
-  const content_t* b = (const content_t*)pb;
-  double ca = 0.5 * (a->box.min[g_sort_axis] + a->box.max[g_sort_axis]);
-  double cb = 0.5 * (b->box.min[g_sort_axis] + b->box.max[g_sort_axis]);
-  if (ca < cb) return -1;
-  if (ca > cb) return 1;
-  return (a->leaf > b->leaf) - (a->leaf < b->leaf);
+/* bvh.rs:58-67 split: sort by centroid along the axis, split_at_mut(len / 2).  Rust's sort_unstable_by
+ * orders equal centroids in an implementation-defined way; ties are broken by leaf id here (tree shape is
+ * not part of the contract: SURVEY.md 8a A9), which makes the order total.  Under a total order the left
+ * half is exactly the len/2 smallest elements and each half is sorted again on the next axis before it is
+ * split, so the tree only depends on which elements go left, not on their order inside a half: a
+ * selection (quickselect) of the len/2 smallest builds the identical tree in O(n) per level instead of
+ * a full sort. */
+static int less_centroid(const content_t* a, const content_t* b, int axis) {
+  double ca = 0.5 * (a->box.min[axis] + a->box.max[axis]);
+  double cb = 0.5 * (b->box.min[axis] + b->box.max[axis]);
+  if (ca < cb) return 1;
+  if (ca > cb) return 0;
+  return a->leaf < b->leaf;
 }
 
-/* bvh.rs:36-56 make_bvh (post-order node array) */
-static uint32_t make_bvh(content_t* c, uint32_t n, int axis, node_t* nodes, uint32_t* nn, uint32_t depth,
-                         uint32_t* maxdepth) {
-  if (depth > *maxdepth) *maxdepth = depth;
-  if (n == 1) {
-    node_t* nd = &nodes[(*nn)++];
-    nd->is_leaf = 1; nd->box = c[0].box; nd->leaf = c[0].leaf; nd->left = nd->right = 0;
-    return *nn - 1;
+static void swap_content(content_t* a, content_t* b) {
+  content_t t = *a; *a = *b; *b = t;
+}
+
+/* Afterwards c[0..k) are the k smallest of c[0..n) in the total order. */
+static void select_smallest(content_t* c, uint32_t n, uint32_t k, int axis) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 16) {
+    uint32_t m = lo + (hi - lo) / 2, e = hi - 1;
+    /* median of three as the pivot, moved to e */
+    if (less_centroid(&c[m], &c[lo], axis)) swap_content(&c[m], &c[lo]);
+    if (less_centroid(&c[e], &c[lo], axis)) swap_content(&c[e], &c[lo]);
+    if (less_centroid(&c[m], &c[e], axis)) swap_content(&c[m], &c[e]);
+    uint32_t i = lo;
+    for (uint32_t j = lo; j < e; j++)
+      if (less_centroid(&c[j], &c[e], axis)) swap_content(&c[i++], &c[j]);
+    swap_content(&c[i], &c[e]);
+    if (i == k) return;
+    if (k < i) hi = i;
+    else lo = i + 1;
   }
-  g_sort_axis = axis;
-  qsort(c, n, sizeof *c, cmp_centroid);
-  uint32_t h = n / 2;
-  uint32_t l = make_bvh(c, h, (axis + 1) % 3, nodes, nn, depth + 1, maxdepth);
-  uint32_t r = make_bvh(c + h, n - h, (axis + 1) % 3, nodes, nn, depth + 1, maxdepth);
-  node_t* nd = &nodes[(*nn)++];
+  for (uint32_t i = lo + 1; i < hi; i++)  /* insertion sort of the last small range */
+    for (uint32_t j = i; j > lo && less_centroid(&c[j], &c[j - 1], axis); j--) swap_content(&c[j], &c[j - 1]);
+}
+
+/* bvh.rs:36-56 make_bvh (post-order node array): the subtree of n leaves occupies nodes [base, base+2n-1),
+ * left subtree first, then the right, the branch last -- so the two halves can be built concurrently. */
+typedef struct {
+  content_t* c;
+  uint32_t n, base, depth, maxdepth;
+  int axis;
+  node_t* nodes;
+} bvh_job_t;
+
+static void* make_bvh_job(void* arg);
+
+static void make_bvh(bvh_job_t* J) {
+  if (J->depth > J->maxdepth) J->maxdepth = J->depth;
+  node_t* nodes = J->nodes;
+  if (J->n == 1) {
+    node_t* nd = &nodes[J->base];
+    nd->is_leaf = 1; nd->box = J->c[0].box; nd->leaf = J->c[0].leaf; nd->left = nd->right = 0;
+    return;
+  }
+  uint32_t h = J->n / 2;
+  select_smallest(J->c, J->n, h, J->axis);
+  bvh_job_t L = {J->c, h, J->base, J->depth + 1, J->depth + 1, (J->axis + 1) % 3, nodes};
+  bvh_job_t R = {J->c + h, J->n - h, J->base + 2 * h - 1, J->depth + 1, J->depth + 1, (J->axis + 1) % 3, nodes};
+  pthread_t th;
+  int spawned = J->depth < 5 && J->n >= (1u << 16) && pthread_create(&th, NULL, make_bvh_job, &L) == 0;
+  if (!spawned) make_bvh(&L);
+  make_bvh(&R);
+  if (spawned) pthread_join(th, NULL);
+  uint32_t l = L.base + 2 * L.n - 2, r = R.base + 2 * R.n - 2;
+  node_t* nd = &nodes[J->base + 2 * J->n - 2];
   nd->is_leaf = 0; nd->left = l; nd->right = r; nd->leaf = 0;
   nd->box = aabb_union(&nodes[l].box, &nodes[r].box);
-  return *nn - 1;
+  if (L.maxdepth > J->maxdepth) J->maxdepth = L.maxdepth;
+  if (R.maxdepth > J->maxdepth) J->maxdepth = R.maxdepth;
+}
+
+static void* make_bvh_job(void* arg) {
+  make_bvh((bvh_job_t*)arg);
+  return NULL;
 }
 
 static char g_err[256];
@@ -436,10 +492,11 @@ or_scene* or_scene_create(const rp_scene_desc* d) {
     content_t* c = (content_t*)malloc(sizeof(content_t) * s->n_hit);
     for (uint32_t i = 0; i < s->n_hit; i++) { c[i].leaf = i; c[i].box = hittable_bbox(s, &s->hit[i]); }
     s->nodes = (node_t*)malloc(sizeof(node_t) * (2 * s->n_hit));
-    uint32_t nn = 0, md = 0;
-    s->root = make_bvh(c, s->n_hit, 0, s->nodes, &nn, 0, &md);
-    s->n_nodes = nn;
-    s->depth = md;
+    bvh_job_t J = {c, s->n_hit, 0, 0, 0, 0, s->nodes};
+    make_bvh(&J);
+    s->root = 2 * s->n_hit - 2;
+    s->n_nodes = 2 * s->n_hit - 1;
+    s->depth = J.maxdepth;
     free(c);
   }
   return s;
@@ -467,7 +524,7 @@ typedef struct { int valid; hit_t h; uint32_t material; } hitm_t;
 /* hittable.rs:39-63 */
 static hitm_t hit_sphere(const rp_hittable* sp, const ray_t* r, ctr_t* C) {
   hitm_t res; res.valid = 0;
-  C->c[OR_C_SPH]++;
+  OR_EVENT(C, OR_C_SPH);
   v3 center = V(sp->center[0], sp->center[1], sp->center[2]);
   double radius = sp->radius;
   v3 to_center = sub(r->o, center);
@@ -495,7 +552,7 @@ static hitm_t hit_sphere(const rp_hittable* sp, const ray_t* r, ctr_t* C) {
 /* hittable.rs:65-108 (exact expression order) */
 static hitm_t hit_triangle(const or_scene* s, const rp_hittable* tr, const ray_t* r, ctr_t* C) {
   hitm_t res; res.valid = 0;
-  C->c[OR_C_TRI]++;
+  OR_EVENT(C, OR_C_TRI);
   const mesh_t* m = &s->mesh[tr->mesh];
   uint32_t i0 = m->idx[tr->triangle], i1 = m->idx[tr->triangle + 1], i2 = m->idx[tr->triangle + 2];
   v3 a = vpos(m, i0), b = vpos(m, i1), c = vpos(m, i2);
@@ -515,7 +572,7 @@ static hitm_t hit_triangle(const or_scene* s, const rp_hittable* tr, const ray_t
             + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
   double w = 1.0 - u - v;
   if (t < r->tmin || t > r->tmax || u < 0.0 || v < 0.0 || w < 0.0) return res;
-  C->c[OR_C_TRI_HITS]++;
+  OR_EVENT(C, OR_C_TRI_HITS);
   res.valid = 1;
   res.h.t = t;
   res.h.p = ray_at(r, t);
@@ -536,7 +593,7 @@ static hitm_t hittable_hit(const or_scene* s, const rp_hittable* h, const ray_t*
 static hitm_t hit_node(const or_scene* s, const rayx_t* ray, uint32_t node, ctr_t* C) {
   const node_t* nd = &s->nodes[node];
   hitm_t none; none.valid = 0;
-  C->c[OR_C_BOX]++;
+  OR_EVENT(C, OR_C_BOX);
   if (nd->is_leaf) {
     if (aabb_collide(&nd->box, ray)) return hittable_hit(s, &s->hit[nd->leaf], &ray->r, C);
     return none;
@@ -622,7 +679,7 @@ static v3 tex_sample(const or_scene* s, uint32_t tid, const hit_t* h, ctr_t* C) 
       if (y > hh - 1.0) y = hh - 1.0;
       uint32_t i = sat_u32(x), j = sat_u32(y);
       const uint8_t* px = t->rgba + 4 * ((size_t)i + (size_t)j * t->w);
-      C->c[OR_C_TEXELS]++;
+      OR_EVENT(C, OR_C_TEXELS);
       return V((double)px[0] / 255.0, (double)px[1] / 255.0, (double)px[2] / 255.0);
     }
     case RP_TEXTURE_CHECKER: {  /* texture.rs:51-60 */
@@ -827,18 +884,20 @@ static void* render_worker(void* arg) {
     for (uint32_t tj = 0; tj < h; tj++)
       for (uint32_t ti = 0; ti < w; ti++) {
         uint32_t i = ox + ti, j = oy + tj;
-        /* RNG contract: batch b (samples 32b .. 32b+31) of pixel (i, j) has its own stream
-         * seed_from_u64(seed + b*W*H + j*W + i) and runs the unchanged per-pixel body over its samples;
-         * the batch sums are added in batch order, then divided by spp (main.rs:86-87). */
+        /* RNG contract (include/rp.h): batch b (samples N*b .. N*b+N-1, N = samples_per_stream, 0 -> 32) of
+         * pixel (i, j) has its own stream seed_from_u64(seed + b*W*H + j*W + i) and runs the unchanged
+         * per-pixel body over its samples; the batch sums are added in batch order, then divided by spp
+         * (main.rs:86-87).  N >= spp: one stream per pixel. */
         const uint64_t WH = (uint64_t)J->p->width * J->p->height;
+        const uint64_t N = J->p->samples_per_stream ? J->p->samples_per_stream : OR_SAMPLES_PER_STREAM;
         double c[3] = {0.0, 0.0, 0.0}, fg = 0.0;
-        for (uint32_t b = 0; b * OR_SAMPLES_PER_STREAM < J->p->spp; b++) {
-          uint32_t n = J->p->spp - b * OR_SAMPLES_PER_STREAM;
-          if (n > OR_SAMPLES_PER_STREAM) n = OR_SAMPLES_PER_STREAM;
+        for (uint64_t b = 0; b * N < J->p->spp; b++) {
+          uint64_t n = J->p->spp - b * N;
+          if (n > N) n = N;
           or_rng rng;
           or_rng_seed_from_u64(&rng, J->p->seed + b * WH + (uint64_t)j * J->p->width + i);
           double cb[3], fb;
-          render_pixel(J->s, J->cam, i, j, J->p->width, J->p->height, n, J->p->max_bounce, &rng, &C, cb, &fb);
+          render_pixel(J->s, J->cam, i, j, J->p->width, J->p->height, (uint32_t)n, J->p->max_bounce, &rng, &C, cb, &fb);
           c[0] = c[0] + cb[0]; c[1] = c[1] + cb[1]; c[2] = c[2] + cb[2];
           fg += fb;
         }

@@ -1,11 +1,15 @@
 // rp_api.cpp -- implementation of the C-ABI in include/rp.h (librp.so).
 //
 // Host side of the drop-in: validates the reference-shaped scene (rp_scene_desc mirrors hittable.rs,
-// mesh.rs, material.rs, texture.rs), builds the acceleration structure (rp_bvh.cpp), copies it to HBM
-// once, and launches the persistent render kernel (rp_kernel.hip) per frame / shard.
+// mesh.rs, material.rs, texture.rs), builds the acceleration structure (rp_bvh.cpp / rp_bvh_gpu.hip),
+// copies it to HBM once, launches the persistent render kernel (rp_kernel.hip) per frame / shard, and
+// assembles multi-GPU frames with one RCCL all-gather over xGMI.  The library reads no
+// environment variables: every knob is an argument (rp_scene_options, rp_render_params).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +20,12 @@
 #include "../../include/rp.h"
 #include "rp_bvh.h"
 #include "rp_kernel.h"
+
+static_assert(rpk::CTR_N == RP_COUNTERS_LEN, "kernel counter block = the ABI's");
+static_assert(rpk::CTR_RAYS == RP_CTR_RAYS && rpk::CTR_STATUS == RP_CTR_STATUS, "counter order");
+static_assert(rpk::STATUS_STACK_OVERFLOW == RP_STATUS_STACK_OVERFLOW, "status bits");
+static_assert(sizeof(ncclUniqueId) == RP_COMM_ID_BYTES, "RCCL unique id size");
+static_assert(sizeof(rp_render_params) == 48, "rp_render_params layout (bindings mirror it)");
 
 namespace {
 
@@ -30,6 +40,12 @@ int fail(int code, const std::string& msg) {
   do {                                                                                      \
     hipError_t e_ = (call);                                                                 \
     if (e_ != hipSuccess) return fail(RP_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define RP_NCCL(call)                                                                           \
+  do {                                                                                          \
+    ncclResult_t r_ = (call);                                                                   \
+    if (r_ != ncclSuccess) return fail(RP_ERCCL, std::string(#call) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
 struct DeviceGuard {
@@ -55,26 +71,50 @@ int upload(const std::vector<T>& v, T** out) {
   return RP_OK;
 }
 
+template <class T>
+bool dalloc(T** p, uint64_t n) {
+  return hipMalloc(reinterpret_cast<void**>(p), sizeof(T) * (n ? n : 1)) == hipSuccess;
+}
+
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+// Defaults of rp_scene_options (the measured best).
+constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
+constexpr double DEF_COST_TRAVERSE = 0.7;
+// Above this many hittables the single-threaded host SAH build dominates setup: the device LBVH builds.
+constexpr uint32_t GPU_BUILD_MIN_PRIMS = 1u << 20;
+
 }  // namespace
 
 // Per-frame device state of a render (include/rp.h rp_workspace): frames with different workspaces may
 // run concurrently on different streams.
 struct rp_workspace {
   rp_scene* scene = nullptr;
-  uint64_t* d_ctr = nullptr;         // default counter block (CTR_N x u64)
-  uint64_t* d_probe_ctr = nullptr;   // counter block of the probe launch
+  uint64_t* d_ctr = nullptr;         // counters when the caller passes none (CTR_N x u64)
+  uint64_t* d_probe_ctr = nullptr;   // counters of the probe launch
+  uint32_t* d_queue = nullptr;       // unit queues: [0] the frame, [1] the probe
   uint32_t* d_tile_cost = nullptr;   // cost probe output, 2 x rpk::TILE_SORT_MAX entries
   uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
   uint32_t* d_slab = nullptr;        // keystream cache, one slab per resident render lane
   uint32_t* d_spill = nullptr;       // traversal-stack overflow entries of every resident lane (deep trees)
-  double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames (grown on demand)
+  // reserved by rp_workspace_reserve:
+  double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames
   uint32_t* d_partial_hits = nullptr;
   uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
+  double* d_gs_rgb = nullptr;        // gather staging: this rank's shard, padded to the stride (3 f64 / slot)
+  uint32_t* d_gs_bgra = nullptr;     //   ... its to_srgb_u8 bytes (1 word / slot)
+  double* d_gather_rgb = nullptr;    //   all ranks' shards (nranks x stride x 3 f64)
+  uint32_t* d_gather_bgra = nullptr; //   all ranks' bytes (nranks x stride words)
+  uint64_t gs_slots = 0;             // capacity of d_gs_* in slots
+  uint64_t gather_slots = 0;         // capacity of d_gather_* in slots (over all ranks)
 };
 
 struct rp_scene {
   int device = 0;
   rpk::KScene ks{};
+  rp_scene_options opt{};
   rpl::Node4* d_nodes = nullptr;
   rpl::Prim* d_prims = nullptr;
   rpl::PrimRef* d_prim_refs = nullptr;
@@ -90,30 +130,46 @@ struct rp_scene {
   uint32_t max_depth = 0;
   int num_cu = 0;
   int blocks_per_cu = 0;
+  uint64_t lanes() const { return (uint64_t)num_cu * (uint64_t)blocks_per_cu * rpk::RENDER_BLOCK; }
+};
+
+struct rp_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+};
+
+struct rp_multi {
+  std::vector<int> devices;
+  std::vector<rp_scene*> scenes;
+  std::vector<ncclComm_t> comms;
+  std::vector<hipStream_t> streams;
+  std::vector<uint64_t*> d_ctr;  // per device, CTR_N
+  double* d_frame_rgb = nullptr;  // device 0: the assembled frame
+  uint32_t* d_frame_bgra = nullptr;
+  uint64_t frame_px = 0;
 };
 
 namespace {
 
 void ws_release(rp_workspace* w) {
-  for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_tile_cost, (void*)w->d_tile_order,
-                  (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial, (void*)w->d_partial_hits})
-    if (p) (void)hipFree(p);
+  for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
+                  (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
+                  (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
+                  (void*)w->d_gather_bgra})
+    dfree(p);
   *w = rp_workspace{};
 }
 
-// Allocate a workspace for scene s (current device = the scene's): counters, probe/sort buffers and a
-// keystream slab for every lane the render grid can hold resident.
+// Allocate a workspace for scene s (current device = the scene's): counters, queues, probe/sort buffers
+// and a keystream slab for every lane the render grid can hold resident.
 int ws_alloc(rp_scene* s, rp_workspace* w) {
   *w = rp_workspace{};
   w->scene = s;
-  const uint64_t lanes = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu * rpk::RENDER_BLOCK;
-  if (hipMalloc(reinterpret_cast<void**>(&w->d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_probe_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_tile_cost), sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_tile_order), sizeof(uint32_t) * rpk::TILE_SORT_MAX) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) != hipSuccess ||
-      hipMalloc(reinterpret_cast<void**>(&w->d_spill),
-                lanes * sizeof(uint32_t) * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth)) != hipSuccess) {
+  const uint64_t lanes = s->lanes();
+  if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, 2) ||
+      !dalloc(&w->d_tile_cost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_tile_order, rpk::TILE_SORT_MAX) ||
+      !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
+      !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
   }
@@ -123,6 +179,7 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
 struct Tiling {
   uint32_t tw, th, shards, shard, tiles_x, tiles_y, n_tiles, n_shard_tiles;
   uint64_t n_slots;
+  uint32_t sps, nbatch;  // RNG contract: samples per stream, batches per pixel
 };
 
 int make_tiling(const rp_render_params* p, Tiling& t) {
@@ -131,6 +188,7 @@ int make_tiling(const rp_render_params* p, Tiling& t) {
   if (p->width > 65535 || p->height > 65535) return fail(RP_EINVAL, "width and height must be <= 65535");
   t.tw = p->tile_w ? p->tile_w : 32;
   t.th = p->tile_h ? p->tile_h : 32;
+  if (t.tw > 65535 || t.th > 65535) return fail(RP_EINVAL, "tile_w and tile_h must be <= 65535");
   t.shards = p->num_shards ? p->num_shards : 1;
   t.shard = p->shard;
   if (t.shard >= t.shards) return fail(RP_EINVAL, "shard must be < num_shards");
@@ -140,41 +198,9 @@ int make_tiling(const rp_render_params* p, Tiling& t) {
   t.n_shard_tiles = t.n_tiles > t.shard ? (t.n_tiles - t.shard + t.shards - 1) / t.shards : 0;
   t.n_slots = (uint64_t)t.n_shard_tiles * t.tw * t.th;
   if (t.n_slots >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel slots)");
+  t.sps = p->samples_per_stream ? p->samples_per_stream : RP_SAMPLES_PER_STREAM;
+  t.nbatch = p->spp ? (uint32_t)(((uint64_t)p->spp + t.sps - 1) / t.sps) : 0;
   return RP_OK;
-}
-
-// Lanes of a wave keep stepping traversal while at least this many are still traversing; below it,
-// the finished lanes shade and take new rays (1 = wait for every lane, 64 = shade eagerly).
-// Override with RP_TRAV_THRESHOLD for tuning.
-uint32_t trav_threshold() {
-  static const uint32_t v = [] {
-    const char* e = std::getenv("RP_TRAV_THRESHOLD");
-    long x = e ? std::strtol(e, nullptr, 10) : 24;
-    return (uint32_t)(x < 1 ? 1 : (x > 64 ? 64 : x));
-  }();
-  return v;
-}
-
-// Acceleration-structure builder: the host binned SAH (rp_bvh.cpp, the better tree) unless the scene is
-// large enough for its single-threaded build to dominate setup, then the device LBVH (rp_bvh_gpu.hip).
-// RP_BVH_BUILDER=host|gpu forces one (read per scene).
-enum : uint32_t { GPU_BUILD_MIN_PRIMS = 1u << 20 };
-bool use_gpu_builder(uint32_t n_hittables) {
-  if (n_hittables < 2) return false;
-  if (const char* e = std::getenv("RP_BVH_BUILDER")) {
-    if (std::strcmp(e, "gpu") == 0) return true;
-    if (std::strcmp(e, "host") == 0) return false;
-  }
-  return n_hittables >= GPU_BUILD_MIN_PRIMS;
-}
-
-// Cost-ordered tile scheduling (rp_kernel.h); RP_TILE_ORDER=0 restores plain shard order (for A/B timing).
-bool tile_order_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("RP_TILE_ORDER");
-    return !(e && std::strtol(e, nullptr, 10) == 0);
-  }();
-  return v;
 }
 
 // to_srgb_u8's byte for one channel (utility.rs:212-216), in the host libm: the reference's arithmetic
@@ -206,6 +232,354 @@ const rpk::SrgbTable& srgb_table() {
     return t;
   }();
   return tab;
+}
+
+rp_scene_options default_options() {
+  rp_scene_options o{};
+  o.builder = RP_BUILDER_AUTO;
+  o.max_leaf = DEF_MAX_LEAF;
+  o.cost_traverse = DEF_COST_TRAVERSE;
+  o.always_max = (int32_t)DEF_ALWAYS_MAX;
+  o.lds_depth = 0;
+  o.self_check = 0;
+  o.trav_threshold = DEF_TRAV_THRESHOLD;
+  o.tile_order = 0;
+  o.probe_n = rpk::PROBE_LATTICE_N;
+  return o;
+}
+
+// Zero fields -> defaults; range checks.
+int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
+  const rp_scene_options d = default_options();
+  o = in ? *in : d;
+  if (o.builder > RP_BUILDER_DEVICE) return fail(RP_EINVAL, "options.builder must be RP_BUILDER_*");
+  if (o.max_leaf == 0) o.max_leaf = d.max_leaf;
+  if (o.max_leaf > rpl::LEAF_MAX) return fail(RP_EINVAL, "options.max_leaf must be 1..8");
+  if (o.cost_traverse == 0.0) o.cost_traverse = d.cost_traverse;
+  if (!(o.cost_traverse > 0.0) || !std::isfinite(o.cost_traverse)) return fail(RP_EINVAL, "options.cost_traverse must be > 0");
+  if (o.always_max < 0) o.always_max = d.always_max;
+  if (o.lds_depth != 0 && o.lds_depth < 17) return fail(RP_EINVAL, "options.lds_depth must be 0 or >= 17");
+  if (o.trav_threshold == 0) o.trav_threshold = d.trav_threshold;
+  if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
+  if (o.tile_order > 1) return fail(RP_EINVAL, "options.tile_order must be 0 or 1");
+  if (o.probe_n == 0) o.probe_n = d.probe_n;
+  return RP_OK;
+}
+
+// Slots per rank buffer of a gathered frame: shard 0 holds the most tiles (one rank: the whole frame).
+uint64_t stage_slots(const Tiling& t) {
+  const uint32_t n0 = t.n_tiles ? (t.n_tiles + t.shards - 1) / t.shards : 0;
+  return (uint64_t)n0 * t.tw * t.th;
+}
+
+// Grow a pair of device buffers (a, b) of na, nb elements per unit to `units` units (synchronous).
+template <class A, class B>
+int grow(A*& a, B*& b, uint64_t& cap, uint64_t units, uint64_t na, uint64_t nb, const char* what) {
+  if (units <= cap) return RP_OK;
+  dfree(a);
+  dfree(b);
+  a = nullptr;
+  b = nullptr;
+  cap = 0;
+  if (!dalloc(&a, na * units) || !dalloc(&b, nb * units)) return fail(RP_ENOMEM, std::string("hipMalloc ") + what);
+  cap = units;
+  return RP_OK;
+}
+
+// Grow the workspace's reservation for renders of params' shape (synchronous): the multi-batch sums and,
+// with `gather`, the staging and receive buffers of rp_frame_gather.
+int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gather) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  DeviceGuard g(s->device);
+  const uint64_t units = t.nbatch > 1 ? t.n_slots * t.nbatch : 0;
+  if ((rc = grow(w->d_partial, w->d_partial_hits, w->partial_units, units, 3, 1, "sample-batch workspace"))) return rc;
+  if (gather) {
+    const uint64_t stride = stage_slots(t);
+    if ((rc = grow(w->d_gs_rgb, w->d_gs_bgra, w->gs_slots, stride, 3, 1, "gather staging"))) return rc;
+    if ((rc = grow(w->d_gather_rgb, w->d_gather_bgra, w->gather_slots, stride * t.shards, 3, 1, "gather buffers")))
+      return rc;
+  }
+  return RP_OK;
+}
+
+int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* opt_in, rp_scene** out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  *out = nullptr;
+  rp_scene_options opt;
+  int rc = resolve_options(opt_in, opt);
+  if (rc) return rc;
+  std::string err;
+  rc = rpb::validate(desc, err);
+  if (rc != RP_OK) return fail(rc, err);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RP_ENODEV, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RP_EINVAL, "device index out of range");
+  hipDeviceProp_t prop;
+  RP_HIP(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(RP_ENODEV, std::string("librp.so is built for gfx950, device is ") + prop.gcnArchName);
+
+  rpb::PackedScene ps;
+  rpb::BuildOptions bo;
+  const bool gpu_build = opt.builder == RP_BUILDER_DEVICE ||
+                         (opt.builder == RP_BUILDER_AUTO && desc->n_hittables >= GPU_BUILD_MIN_PRIMS);
+  const bool use_gpu = gpu_build && desc->n_hittables >= 2;  // the LBVH needs two primitives
+  bo.tables_only = use_gpu;
+  bo.max_leaf = opt.max_leaf;
+  bo.cost_traverse = opt.cost_traverse;
+  bo.always_max = (uint32_t)opt.always_max;
+  rc = rpb::build(desc, bo, ps, err);
+  if (rc != RP_OK) return fail(rc, err);
+
+  DeviceGuard g(device);
+  rp_scene* s = new rp_scene();
+  s->device = device;
+  s->opt = opt;
+  s->num_cu = prop.multiProcessorCount;
+  auto bail = [&](int code) { rp_scene_destroy(s); return code; };
+  uint64_t n_tree_nodes = ps.nodes.size(), n_tree_prims = ps.prims.size();
+  if (use_gpu) {
+    rpb::PrimInput pin;
+    if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
+    rpg::GpuTree gt;
+    if ((rc = rpg::build_gpu(pin, opt.max_leaf, gt, err))) return bail(fail(rc, err));
+    s->d_nodes = gt.d_nodes;
+    s->d_prims = gt.d_prims;
+    s->d_prim_refs = gt.d_prim_refs;
+    ps.root = 0;
+    ps.max_depth = gt.max_depth;
+    ps.n_leaves = gt.n_leaves;
+    n_tree_nodes = gt.n_nodes;
+    n_tree_prims = pin.prims.size();
+    if (opt.self_check) {
+      // the structural self-check of the host builder on the device-built tree (tests)
+      rpb::PackedScene chk;
+      chk.nodes.resize(n_tree_nodes);
+      chk.prims.resize(n_tree_prims);
+      chk.prim_refs.resize(n_tree_prims);
+      RP_HIP(hipMemcpy(chk.nodes.data(), s->d_nodes, sizeof(rpl::Node4) * n_tree_nodes, hipMemcpyDeviceToHost));
+      RP_HIP(hipMemcpy(chk.prims.data(), s->d_prims, sizeof(rpl::Prim) * n_tree_prims, hipMemcpyDeviceToHost));
+      RP_HIP(hipMemcpy(chk.prim_refs.data(), s->d_prim_refs, sizeof(rpl::PrimRef) * n_tree_prims, hipMemcpyDeviceToHost));
+      chk.root = 0;
+      chk.max_depth = gt.max_depth;
+      chk.n_leaves = gt.n_leaves;
+      if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
+    }
+  } else if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
+             (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
+    return bail(rc);
+  }
+  if ((rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
+      (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
+      (rc = upload(ps.texels, &s->d_texels)))
+    return bail(rc);
+  if (!dalloc(&s->d_diag, rpk::DIAG_N) || hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
+    return bail(fail(RP_ENOMEM, "hipMalloc diagnostics"));
+  s->ks.diag = s->d_diag;
+  s->ks.nodes = s->d_nodes;
+  s->ks.prims = s->d_prims;
+  s->ks.prim_refs = s->d_prim_refs;
+  s->ks.vnrm = s->d_vnrm;
+  s->ks.vuv = s->d_vuv;
+  s->ks.mats = s->d_mats;
+  s->ks.texs = s->d_texs;
+  s->ks.texels = s->d_texels;
+  s->ks.background = ps.background;
+  s->ks.root = ps.root;
+  s->ks.always_first = ps.always_first;  // 0 / 0 for a device-built tree
+  s->ks.n_always = ps.n_always;
+  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
+  // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
+  s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
+  // floor of 17 entries: the spill split below never keeps fewer in LDS (options.lds_depth tests force 17)
+  if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
+  s->n_nodes = n_tree_nodes;
+  s->n_leaves = ps.n_leaves;
+  s->n_prims = desc->n_hittables;
+  s->max_depth = ps.max_depth;
+  s->device_bytes = sizeof(rpl::Node4) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
+                    sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
+                    sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
+  // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
+  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
+  // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  options.lds_depth
+  // forces a depth (>= 17) for tests and tuning.
+  s->ks.lds_depth = s->ks.stack_depth;
+  int bpc = 0;
+  if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, &bpc) != 0 || bpc < 1) bpc = 1;
+  int bpc_spill = 0;
+  if (rpk::render_blocks_per_cu(17, true, &bpc_spill) == 0 && bpc_spill > bpc) {
+    uint32_t L = s->ks.stack_depth - 1;
+    int b = 0;
+    while (L > 17 && (rpk::render_blocks_per_cu(L, true, &b) != 0 || b < bpc_spill)) L--;
+    s->ks.lds_depth = L;
+    bpc = bpc_spill;
+  }
+  if (opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
+    s->ks.lds_depth = opt.lds_depth;
+    if (rpk::render_blocks_per_cu(opt.lds_depth, true, &bpc) != 0 || bpc < 1) bpc = 1;
+  }
+  s->blocks_per_cu = bpc;
+  if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);
+  *out = s;
+  return RP_OK;
+}
+
+// The render of one shard on `stream` (rp_render_device_ws's body).
+int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
+                 float* d_fg, uint64_t* d_counters, void* stream) {
+  if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
+  if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (p->max_bounce < 1) return fail(RP_EINVAL, "max_bounce must be >= 1 (render.rs:97 assert!(depth >= 1))");
+  DeviceGuard g(s->device);
+  uint64_t* ctr = d_counters ? d_counters : w->d_ctr;
+  hipStream_t st = (hipStream_t)stream;
+  RP_HIP(hipMemsetAsync(ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+  if (t.n_slots == 0) return RP_OK;
+  if (p->spp == 0) {
+    // main.rs:86-87 with num_samples = 0: (0,0,0) / 0 and 0 / 0 are NaN; all-ones bits are a NaN.
+    RP_HIP(hipMemsetAsync(d_rgb, 0xff, sizeof(double) * 3 * t.n_slots, st));
+    if (d_fg) RP_HIP(hipMemsetAsync(d_fg, 0xff, sizeof(float) * t.n_slots, st));
+    return RP_OK;
+  }
+  rpk::KParams kp{};
+  std::memcpy(kp.orient, cam->orientation, sizeof kp.orient);
+  std::memcpy(kp.pos, cam->position, sizeof kp.pos);
+  kp.aspect = cam->aspect_ratio;
+  kp.tan_fov = std::tan(0.5 * cam->fov);  // render.rs:33, hoisted: a per-camera constant
+  kp.focal = cam->focal_dist;
+  kp.lens = cam->lens_radius;
+  kp.seed = p->seed;
+  kp.W = p->width;
+  kp.H = p->height;
+  kp.spp = p->spp;
+  kp.max_bounce = p->max_bounce;
+  kp.tw = t.tw;
+  kp.th = t.th;
+  kp.shard = t.shard;
+  kp.nshards = t.shards;
+  kp.tiles_x = t.tiles_x;
+  kp.n_shard_tiles = t.n_shard_tiles;
+  kp.n_slots = t.n_slots;
+  kp.trav_threshold = s->opt.trav_threshold;
+  kp.spp_batch = t.sps;  // the RNG contract's samples per stream (rp_render_params.samples_per_stream)
+  kp.nbatch = t.nbatch;
+  kp.n_queue = t.n_slots * kp.nbatch;
+  // the 32-bit queue word also takes one failed fetch per resident lane after the last unit
+  if (kp.n_queue + s->lanes() >= 0xffffffffull)
+    return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units with the resident lanes)");
+  if (kp.nbatch > 1) {
+    if (kp.n_queue > w->partial_units)
+      return fail(RP_EINVAL, "workspace not reserved for this frame's sample batches: call rp_workspace_reserve");
+    kp.partial = w->d_partial;
+    kp.partial_hits = w->d_partial_hits;
+  }
+  const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
+  rpk::KScene ks = s->ks;
+  ks.rng_slab = w->d_slab;
+  ks.spill = w->d_spill;
+  auto grid_for = [&](uint64_t slots) {
+    const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
+    return (int)std::max<uint64_t>(1, std::min(want, resident));
+  };
+  RP_HIP(hipMemsetAsync(w->d_queue, 0, sizeof(uint32_t) * 2, st));
+  if (s->opt.tile_order == 0 && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
+    // probe sample 0 of an n x n lattice of pixels per tile, then sort the tiles by cost (same stream,
+    // no host sync)
+    rpk::KParams pk = kp;
+    pk.probe = 1;
+    pk.spp = 1;
+    pk.probe_n = std::min(s->opt.probe_n, std::min(t.tw, t.th));
+    pk.probe_px = pk.probe_n * pk.probe_n;
+    pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
+    pk.nbatch = 1;
+    pk.spp_batch = 1;
+    pk.n_queue = pk.n_slots;
+    pk.tile_cost = w->d_tile_cost;
+    RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+    RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
+    int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + 1, grid_for(pk.n_slots), stream);
+    if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
+    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, w->d_tile_order, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
+    kp.tile_order = w->d_tile_order;
+  }
+  int e = rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
+  if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+  if (kp.nbatch > 1) {
+    e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  return RP_OK;
+}
+
+// ---- multi-GPU frame assembly, in three phases so one thread can drive several devices (rp_multi):
+// (1) stage the rank's shard (to_srgb_u8 bytes and/or a padded f64 copy), (2) the RCCL collectives,
+// (3) de-interleave the gathered shards into frame order.
+
+struct GatherPlan {
+  Tiling t;
+  uint64_t stride;  // slots per rank buffer
+  rpk::FrameGeom geom;
+};
+
+int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_render_params* p, GatherPlan& gp) {
+  if (!s || !w || w->scene != s) return fail(RP_EINVAL, "scene / workspace mismatch");
+  int rc = make_tiling(p, gp.t);
+  if (rc) return rc;
+  if ((int)gp.t.shards != nranks || (int)gp.t.shard != rank)
+    return fail(RP_EINVAL, "params.shard / num_shards must be the communicator's rank / size");
+  gp.stride = stage_slots(gp.t);
+  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots)
+    return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
+  gp.geom.W = p->width;
+  gp.geom.H = p->height;
+  gp.geom.tw = gp.t.tw;
+  gp.geom.th = gp.t.th;
+  gp.geom.tiles_x = gp.t.tiles_x;
+  gp.geom.nranks = (uint32_t)nranks;
+  gp.geom.stride = gp.stride;
+  return RP_OK;
+}
+
+int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const double* d_shard_rgb, bool bgra, bool rgb,
+                 hipStream_t st) {
+  DeviceGuard g(s->device);
+  if (bgra && gp.t.n_slots) {
+    int e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_gs_bgra), st);
+    if (e != 0) return fail(RP_EHIP, std::string("output stage launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  if (rgb && gp.t.n_slots && d_shard_rgb != w->d_gs_rgb)
+    RP_HIP(hipMemcpyAsync(w->d_gs_rgb, d_shard_rgb, sizeof(double) * 3 * gp.t.n_slots, hipMemcpyDeviceToDevice, st));
+  return RP_OK;
+}
+
+int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb,
+                       uint64_t* d_counters, hipStream_t st) {
+  if (bgra) RP_NCCL(ncclAllGather(w->d_gs_bgra, w->d_gather_bgra, gp.stride, ncclUint32, comm, st));
+  if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
+  if (d_counters) RP_NCCL(ncclAllReduce(d_counters, d_counters, RP_COUNTERS_LEN, ncclUint64, ncclSum, comm, st));
+  return RP_OK;
+}
+
+int gather_assemble(rp_scene* s, rp_workspace* w, const GatherPlan& gp, uint8_t* d_frame_bgra, double* d_frame_rgb,
+                    hipStream_t st) {
+  DeviceGuard g(s->device);
+  if (d_frame_bgra) {
+    int e = rpk::launch_frame_assemble(gp.geom, w->d_gather_bgra, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
+    if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  if (d_frame_rgb) {
+    int e = rpk::launch_frame_assemble(gp.geom, reinterpret_cast<const uint32_t*>(w->d_gather_rgb), 6,
+                                       reinterpret_cast<uint32_t*>(d_frame_rgb), st);
+    if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  return RP_OK;
 }
 
 }  // namespace
@@ -251,132 +625,24 @@ void rp_scene_destroy(rp_scene* s) {
   if (!s) return;
   DeviceGuard g(s->device);
   ws_release(&s->ws0);
-  for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_prim_refs, (void*)s->d_vnrm, (void*)s->d_vuv, (void*)s->d_mats,
-                  (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_diag})
-    if (p) (void)hipFree(p);
+  for (void* p : {(void*)s->d_nodes, (void*)s->d_prims, (void*)s->d_prim_refs, (void*)s->d_vnrm, (void*)s->d_vuv,
+                  (void*)s->d_mats, (void*)s->d_texs, (void*)s->d_texels, (void*)s->d_diag})
+    dfree(p);
   delete s;
 }
 
-int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
-  if (!out) return fail(RP_EINVAL, "out is NULL");
-  *out = nullptr;
-  std::string err;
-  int rc = rpb::validate(desc, err);
-  if (rc != RP_OK) return fail(rc, err);
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RP_ENODEV, "no HIP device");
-  if (device < 0 || device >= ndev) return fail(RP_EINVAL, "device index out of range");
-  hipDeviceProp_t prop;
-  RP_HIP(hipGetDeviceProperties(&prop, device));
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-    return fail(RP_ENODEV, std::string("librp.so is built for gfx950, device is ") + prop.gcnArchName);
-
-  rpb::PackedScene ps;
-  rpb::BuildOptions opt;
-  const bool gpu_build = use_gpu_builder(desc->n_hittables);
-  opt.tables_only = gpu_build;
-  // tuning knobs for experiments (the defaults are the measured best): leaf size and SAH cost ratio
-  if (const char* e = std::getenv("RP_BVH_MAX_LEAF")) opt.max_leaf = (uint32_t)std::strtoul(e, nullptr, 10);
-  if (const char* e = std::getenv("RP_BVH_COST_TRAVERSE")) opt.cost_traverse = std::strtod(e, nullptr);
-  if (const char* e = std::getenv("RP_ALWAYS_MAX")) opt.always_max = (uint32_t)std::strtoul(e, nullptr, 10);
-  rc = rpb::build(desc, opt, ps, err);
-  if (rc != RP_OK) return fail(rc, err);
-
-  DeviceGuard g(device);
-  rp_scene* s = new rp_scene();
-  s->device = device;
-  s->num_cu = prop.multiProcessorCount;
-  auto bail = [&](int code) { rp_scene_destroy(s); return code; };
-  uint64_t n_tree_nodes = ps.nodes.size(), n_tree_prims = ps.prims.size();
-  if (gpu_build) {
-    rpb::PrimInput pin;
-    if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
-    rpg::GpuTree gt;
-    if ((rc = rpg::build_gpu(pin, opt.max_leaf, gt, err))) return bail(fail(rc, err));
-    s->d_nodes = gt.d_nodes;
-    s->d_prims = gt.d_prims;
-    s->d_prim_refs = gt.d_prim_refs;
-    ps.root = 0;
-    ps.max_depth = gt.max_depth;
-    ps.n_leaves = gt.n_leaves;
-    n_tree_nodes = gt.n_nodes;
-    n_tree_prims = pin.prims.size();
-    if (const char* e = std::getenv("RP_BVH_CHECK"); e && std::strcmp(e, "1") == 0) {
-      // test hook: the structural self-check of the host builder on the device-built tree
-      rpb::PackedScene chk;
-      chk.nodes.resize(n_tree_nodes);
-      chk.prims.resize(n_tree_prims);
-      chk.prim_refs.resize(n_tree_prims);
-      RP_HIP(hipMemcpy(chk.nodes.data(), s->d_nodes, sizeof(rpl::Node4) * n_tree_nodes, hipMemcpyDeviceToHost));
-      RP_HIP(hipMemcpy(chk.prims.data(), s->d_prims, sizeof(rpl::Prim) * n_tree_prims, hipMemcpyDeviceToHost));
-      RP_HIP(hipMemcpy(chk.prim_refs.data(), s->d_prim_refs, sizeof(rpl::PrimRef) * n_tree_prims, hipMemcpyDeviceToHost));
-      chk.root = 0;
-      chk.max_depth = gt.max_depth;
-      chk.n_leaves = gt.n_leaves;
-      if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
-    }
-  } else if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
-             (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
-    return bail(rc);
-  }
-  if ((rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
-      (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
-      (rc = upload(ps.texels, &s->d_texels)))
-    return bail(rc);
-  if (hipMalloc(reinterpret_cast<void**>(&s->d_diag), sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess ||
-      hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
-    return bail(fail(RP_ENOMEM, "hipMalloc workspace"));
-  s->ks.diag = s->d_diag;
-  s->ks.nodes = s->d_nodes;
-  s->ks.prims = s->d_prims;
-  s->ks.prim_refs = s->d_prim_refs;
-  s->ks.vnrm = s->d_vnrm;
-  s->ks.vuv = s->d_vuv;
-  s->ks.mats = s->d_mats;
-  s->ks.texs = s->d_texs;
-  s->ks.texels = s->d_texels;
-  s->ks.background = ps.background;
-  s->ks.root = ps.root;
-  s->ks.always_first = ps.always_first;  // 0 / 0 for a device-built tree
-  s->ks.n_always = ps.n_always;
-  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
-  // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
-  s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
-  // floor of 17 entries: the spill split below never keeps fewer in LDS (RP_LDS_DEPTH tests force 17)
-  if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
-  s->n_nodes = n_tree_nodes;
-  s->n_leaves = ps.n_leaves;
-  s->n_prims = desc->n_hittables;
-  s->max_depth = ps.max_depth;
-  s->device_bytes = sizeof(rpl::Node4) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
-                    sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
-                    sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
-  // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
-  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
-  // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  RP_LDS_DEPTH forces a
-  // depth (>= 17) for tests and tuning.
-  s->ks.lds_depth = s->ks.stack_depth;
-  int bpc = 0;
-  if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, &bpc) != 0 || bpc < 1) bpc = 1;
-  int bpc_spill = 0;
-  if (rpk::render_blocks_per_cu(17, true, &bpc_spill) == 0 && bpc_spill > bpc) {
-    uint32_t L = s->ks.stack_depth - 1;
-    int b = 0;
-    while (L > 17 && (rpk::render_blocks_per_cu(L, true, &b) != 0 || b < bpc_spill)) L--;
-    s->ks.lds_depth = L;
-    bpc = bpc_spill;
-  }
-  if (const char* e = std::getenv("RP_LDS_DEPTH")) {
-    const uint32_t L = (uint32_t)std::strtoul(e, nullptr, 10);
-    if (L >= 17 && L < s->ks.stack_depth) {
-      s->ks.lds_depth = L;
-      if (rpk::render_blocks_per_cu(L, true, &bpc) != 0 || bpc < 1) bpc = 1;
-    }
-  }
-  s->blocks_per_cu = bpc;
-  if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);
-  *out = s;
+int rp_scene_options_init(rp_scene_options* opt) {
+  if (!opt) return fail(RP_EINVAL, "opt is NULL");
+  *opt = default_options();
   return RP_OK;
+}
+
+int rp_scene_create_ex(const rp_scene_desc* desc, int device, const rp_scene_options* opt, rp_scene** out) {
+  return scene_create(desc, device, opt, out);
+}
+
+int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
+  return scene_create(desc, device, nullptr, out);
 }
 
 int rp_scene_info(const rp_scene* s, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth, uint64_t* n_prims,
@@ -448,112 +714,22 @@ void rp_workspace_destroy(rp_workspace* w) {
   delete w;
 }
 
+int rp_workspace_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  return ws_reserve(s, w, p, true);
+}
+
 int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* d_rgb, float* d_fg,
                      uint64_t* d_counters, void* stream) {
   if (!s) return fail(RP_EINVAL, "scene is NULL");
-  return rp_render_device_ws(s, &s->ws0, cam, p, d_rgb, d_fg, d_counters, stream);
+  return render_shard(s, &s->ws0, cam, p, d_rgb, d_fg, d_counters, stream);
 }
 
 int rp_render_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
                         float* d_fg, uint64_t* d_counters, void* stream) {
-  if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
-  if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
-  Tiling t;
-  int rc = make_tiling(p, t);
-  if (rc) return rc;
-  if (p->max_bounce < 1) return fail(RP_EINVAL, "max_bounce must be >= 1 (render.rs:97 assert!(depth >= 1))");
-  DeviceGuard g(s->device);
-  uint64_t* ctr = d_counters ? d_counters : w->d_ctr;
-  hipStream_t st = (hipStream_t)stream;
-  RP_HIP(hipMemsetAsync(ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
-  if (t.n_slots == 0) return RP_OK;
-  if (p->spp == 0) {
-    // main.rs:86-87 with num_samples = 0: (0,0,0) / 0 and 0 / 0 are NaN; all-ones bits are a NaN.
-    RP_HIP(hipMemsetAsync(d_rgb, 0xff, sizeof(double) * 3 * t.n_slots, st));
-    if (d_fg) RP_HIP(hipMemsetAsync(d_fg, 0xff, sizeof(float) * t.n_slots, st));
-    return RP_OK;
-  }
-  rpk::KParams kp{};
-  std::memcpy(kp.orient, cam->orientation, sizeof kp.orient);
-  std::memcpy(kp.pos, cam->position, sizeof kp.pos);
-  kp.aspect = cam->aspect_ratio;
-  kp.tan_fov = std::tan(0.5 * cam->fov);  // render.rs:33, hoisted: a per-camera constant
-  kp.focal = cam->focal_dist;
-  kp.lens = cam->lens_radius;
-  kp.seed = p->seed;
-  kp.W = p->width;
-  kp.H = p->height;
-  kp.spp = p->spp;
-  kp.max_bounce = p->max_bounce;
-  kp.tw = t.tw;
-  kp.th = t.th;
-  kp.shard = t.shard;
-  kp.nshards = t.shards;
-  kp.tiles_x = t.tiles_x;
-  kp.n_shard_tiles = t.n_shard_tiles;
-  kp.n_slots = t.n_slots;
-  kp.trav_threshold = trav_threshold();
-  // RP_SPP_BATCH overrides the contract's batch size for timing studies only (it changes every
-  // multi-batch image: never set it for parity runs)
-  kp.spp_batch = rpk::SPP_BATCH;
-  if (const char* e = std::getenv("RP_SPP_BATCH")) kp.spp_batch = std::max(1u, (uint32_t)std::strtoul(e, nullptr, 10));
-  kp.nbatch = (p->spp + kp.spp_batch - 1) / kp.spp_batch;
-  kp.n_queue = t.n_slots * kp.nbatch;
-  if (kp.n_queue >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units)");
-  if (kp.nbatch > 1) {
-    if (kp.n_queue > w->partial_units) {  // workspace-owned, grown on the first call that needs it
-      if (w->d_partial) (void)hipFree(w->d_partial);
-      if (w->d_partial_hits) (void)hipFree(w->d_partial_hits);
-      w->d_partial = nullptr;
-      w->d_partial_hits = nullptr;
-      w->partial_units = 0;
-      if (hipMalloc(reinterpret_cast<void**>(&w->d_partial), sizeof(double) * 3 * kp.n_queue) != hipSuccess ||
-          hipMalloc(reinterpret_cast<void**>(&w->d_partial_hits), sizeof(uint32_t) * kp.n_queue) != hipSuccess)
-        return fail(RP_ENOMEM, "hipMalloc sample-batch workspace");
-      w->partial_units = kp.n_queue;
-    }
-    kp.partial = w->d_partial;
-    kp.partial_hits = w->d_partial_hits;
-  }
-  const uint64_t resident = (uint64_t)s->num_cu * (uint64_t)s->blocks_per_cu;
-  rpk::KScene ks = s->ks;
-  ks.rng_slab = w->d_slab;
-  ks.spill = w->d_spill;
-  auto grid_for = [&](uint64_t slots) {
-    const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
-    return (int)std::max<uint64_t>(1, std::min(want, resident));
-  };
-  if (tile_order_enabled() && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
-    // probe sample 0 of PROBE_PX pixels per tile, then sort the tiles by cost (same stream, no host sync)
-    rpk::KParams pk = kp;
-    pk.probe = 1;
-    pk.spp = 1;
-    // every pixel's sample 0 once spp is large enough to amortise it (a 1/spp extra), else a lattice
-    // an n x n lattice of pixels per tile (RP_PROBE_N overrides n for tuning; 0 = every pixel)
-    pk.probe_n = rpk::PROBE_LATTICE_N;
-    if (const char* e = std::getenv("RP_PROBE_N")) pk.probe_n = (uint32_t)std::strtoul(e, nullptr, 10);
-    pk.probe_n = std::min(pk.probe_n, std::min(t.tw, t.th));
-    pk.probe_px = pk.probe_n ? pk.probe_n * pk.probe_n : t.tw * t.th;
-    pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
-    pk.nbatch = 1;
-    pk.spp_batch = 1;
-    pk.n_queue = pk.n_slots;
-    pk.tile_cost = w->d_tile_cost;
-    RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
-    RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
-    int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, grid_for(pk.n_slots), stream);
-    if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
-    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, w->d_tile_order, stream);
-    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
-    kp.tile_order = w->d_tile_order;
-  }
-  int e = rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, grid_for(kp.n_queue), stream);
-  if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
-  if (kp.nbatch > 1) {
-    e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);
-    if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
-  }
-  return RP_OK;
+  return render_shard(s, w, cam, p, d_rgb, d_fg, d_counters, stream);
 }
 
 int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* out_rgb, float* out_fg,
@@ -562,6 +738,7 @@ int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, doub
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
+  if ((rc = ws_reserve(s, &s->ws0, p, false))) return rc;
   DeviceGuard g(s->device);
   double* d_rgb = nullptr;
   float* d_fg = nullptr;
@@ -575,15 +752,13 @@ int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, doub
   float ms = 0.f;
   do {
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) { result = fail(RP_EHIP, "stream"); break; }
-    if (hipMalloc(reinterpret_cast<void**>(&d_rgb), sizeof(double) * shard.size()) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess ||
-        (out_fg && hipMalloc(reinterpret_cast<void**>(&d_fg), sizeof(float) * shard_fg.size()) != hipSuccess)) {
+    if (!dalloc(&d_rgb, shard.size()) || !dalloc(&d_ctr, rpk::CTR_N) || (out_fg && !dalloc(&d_fg, shard_fg.size()))) {
       result = fail(RP_ENOMEM, "hipMalloc output");
       break;
     }
     if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) { result = fail(RP_EHIP, "event"); break; }
     (void)hipEventRecord(e0, st);
-    result = rp_render_device(s, cam, p, d_rgb, d_fg, d_ctr, st);
+    result = render_shard(s, &s->ws0, cam, p, d_rgb, d_fg, d_ctr, st);
     if (result) break;
     (void)hipEventRecord(e1, st);
     hipError_t e = hipStreamSynchronize(st);
@@ -596,9 +771,9 @@ int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, doub
       break;
     }
   } while (0);
-  if (d_rgb) (void)hipFree(d_rgb);
-  if (d_fg) (void)hipFree(d_fg);
-  if (d_ctr) (void)hipFree(d_ctr);
+  dfree(d_rgb);
+  dfree(d_fg);
+  dfree(d_ctr);
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
   if (st) (void)hipStreamDestroy(st);
@@ -647,10 +822,7 @@ int rp_intersect(rp_scene* s, const double* rays, uint64_t n, double* out_hit, u
   int result = RP_OK;
   uint64_t ctr[rpk::CTR_N] = {0};
   do {
-    if (hipMalloc(reinterpret_cast<void**>(&d_rays), sizeof(double) * 8 * n) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_hit), sizeof(double) * 9 * n) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_mat), sizeof(uint32_t) * n) != hipSuccess ||
-        hipMalloc(reinterpret_cast<void**>(&d_ctr), sizeof(uint64_t) * rpk::CTR_N) != hipSuccess) {
+    if (!dalloc(&d_rays, 8 * n) || !dalloc(&d_hit, 9 * n) || !dalloc(&d_mat, n) || !dalloc(&d_ctr, rpk::CTR_N)) {
       result = fail(RP_ENOMEM, "hipMalloc");
       break;
     }
@@ -670,10 +842,231 @@ int rp_intersect(rp_scene* s, const double* rays, uint64_t n, double* out_hit, u
       break;
     }
   } while (0);
-  for (void* p : {(void*)d_rays, (void*)d_hit, (void*)d_mat, (void*)d_ctr})
-    if (p) (void)hipFree(p);
+  for (void* p : {(void*)d_rays, (void*)d_hit, (void*)d_mat, (void*)d_ctr}) dfree(p);
   if (result) return result;
   if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
+  return RP_OK;
+}
+
+// ---------------------------------------------------------------- multi-GPU ------------------------
+
+int rp_gather_stride(const rp_render_params* p, uint64_t* stride) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!stride) return fail(RP_EINVAL, "stride is NULL");
+  *stride = stage_slots(t);
+  return RP_OK;
+}
+
+int rp_frame_assemble(const rp_render_params* p, const void* d_gathered, uint32_t words, void* d_frame, void* stream) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!d_gathered || !d_frame || words == 0) return fail(RP_EINVAL, "NULL buffer or zero words per slot");
+  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t)};
+  int e = rpk::launch_frame_assemble(g, static_cast<const uint32_t*>(d_gathered), words, static_cast<uint32_t*>(d_frame),
+                                     stream);
+  if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
+  return RP_OK;
+}
+
+int rp_comm_unique_id(uint8_t id[RP_COMM_ID_BYTES]) {
+  if (!id) return fail(RP_EINVAL, "id is NULL");
+  ncclUniqueId u;
+  RP_NCCL(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof u);
+  return RP_OK;
+}
+
+int rp_comm_create(const uint8_t id[RP_COMM_ID_BYTES], int nranks, int rank, int device, rp_comm** out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(RP_EINVAL, "bad id / nranks / rank");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return fail(RP_EINVAL, "device index out of range");
+  DeviceGuard g(device);
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  rp_comm* c = new rp_comm();
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(RP_ERCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  *out = c;
+  return RP_OK;
+}
+
+void rp_comm_destroy(rp_comm* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  delete c;
+}
+
+int rp_comm_info(const rp_comm* c, int* nranks, int* rank, int* device) {
+  if (!c) return fail(RP_EINVAL, "comm is NULL");
+  if (nranks) *nranks = c->nranks;
+  if (rank) *rank = c->rank;
+  if (device) *device = c->device;
+  return RP_OK;
+}
+
+int rp_frame_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_params* p, const double* d_shard_rgb,
+                    uint8_t* d_frame_bgra, double* d_frame_rgb, uint64_t* d_counters, void* stream) {
+  if (!c || !s || !d_shard_rgb) return fail(RP_EINVAL, "comm, scene and shard must be non-NULL");
+  if (!w) w = &s->ws0;
+  if (c->device != s->device) return fail(RP_EINVAL, "the communicator's device is not the scene's");
+  if (reinterpret_cast<uintptr_t>(d_frame_bgra) % 4 != 0) return fail(RP_EINVAL, "d_frame_bgra must be 4-byte aligned");
+  GatherPlan gp;
+  int rc = gather_plan(s, w, c->nranks, c->rank, p, gp);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bgra = d_frame_bgra != nullptr, rgb = d_frame_rgb != nullptr;
+  DeviceGuard g(s->device);
+  if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, rgb, st))) return rc;
+  if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, d_counters, st))) return rc;
+  return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, st);
+}
+
+int rp_render_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,
+                     uint8_t* d_frame_bgra, double* d_frame_rgb, uint64_t* d_counters, void* stream) {
+  if (!c || !s) return fail(RP_EINVAL, "comm and scene must be non-NULL");
+  if (!w) w = &s->ws0;
+  GatherPlan gp;
+  int rc = gather_plan(s, w, c->nranks, c->rank, p, gp);
+  if (rc) return rc;
+  if ((rc = render_shard(s, w, cam, p, w->d_gs_rgb, nullptr, d_counters, stream))) return rc;
+  return rp_frame_gather(c, s, w, p, w->d_gs_rgb, d_frame_bgra, d_frame_rgb, d_counters, stream);
+}
+
+void rp_multi_destroy(rp_multi* m) {
+  if (!m) return;
+  for (size_t k = 0; k < m->devices.size(); k++) {
+    DeviceGuard g(m->devices[k]);
+    if (k < m->comms.size() && m->comms[k]) (void)ncclCommDestroy(m->comms[k]);
+    if (k < m->streams.size() && m->streams[k]) (void)hipStreamDestroy(m->streams[k]);
+    if (k < m->d_ctr.size()) dfree(m->d_ctr[k]);
+    if (k == 0) {
+      dfree(m->d_frame_rgb);
+      dfree(m->d_frame_bgra);
+    }
+  }
+  for (rp_scene* s : m->scenes) rp_scene_destroy(s);
+  delete m;
+}
+
+int rp_multi_create(const rp_scene_desc* desc, const int* devices, int n, const rp_scene_options* opt, rp_multi** out) {
+  if (!out) return fail(RP_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (!devices || n < 1) return fail(RP_EINVAL, "devices must list >= 1 device");
+  for (int a = 0; a < n; a++)
+    for (int b = a + 1; b < n; b++)
+      if (devices[a] == devices[b]) return fail(RP_EINVAL, "devices must be distinct");
+  rp_multi* m = new rp_multi();
+  m->devices.assign(devices, devices + n);
+  int rc = RP_OK;
+  for (int k = 0; k < n && rc == RP_OK; k++) {
+    rp_scene* s = nullptr;
+    rc = scene_create(desc, devices[k], opt, &s);
+    if (rc == RP_OK) m->scenes.push_back(s);
+  }
+  if (rc) {
+    std::string e = g_err;
+    rp_multi_destroy(m);
+    return fail(rc, e);
+  }
+  m->comms.assign(n, nullptr);
+  ncclResult_t r = ncclCommInitAll(m->comms.data(), n, devices);
+  if (r != ncclSuccess) {
+    m->comms.assign(n, nullptr);
+    rp_multi_destroy(m);
+    return fail(RP_ERCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+  }
+  m->streams.assign(n, nullptr);
+  m->d_ctr.assign(n, nullptr);
+  for (int k = 0; k < n; k++) {
+    DeviceGuard g(devices[k]);
+    if (hipStreamCreateWithFlags(&m->streams[k], hipStreamNonBlocking) != hipSuccess || !dalloc(&m->d_ctr[k], rpk::CTR_N)) {
+      rp_multi_destroy(m);
+      return fail(RP_EHIP, "stream / counter allocation");
+    }
+  }
+  *out = m;
+  return RP_OK;
+}
+
+int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p_in, double* out_rgb, uint8_t* out_bgra,
+                    rp_stats* stats) {
+  if (!m || !cam || !p_in) return fail(RP_EINVAL, "multi, camera and params must be non-NULL");
+  const int n = (int)m->devices.size();
+  const bool bgra = out_bgra != nullptr, rgb = out_rgb != nullptr;
+  std::vector<rp_render_params> ps(n, *p_in);
+  std::vector<GatherPlan> plans(n);
+  for (int k = 0; k < n; k++) {
+    ps[k].shard = (uint32_t)k;
+    ps[k].num_shards = (uint32_t)n;
+    int rc = ws_reserve(m->scenes[k], &m->scenes[k]->ws0, &ps[k], true);
+    if (rc) return rc;
+    if ((rc = gather_plan(m->scenes[k], &m->scenes[k]->ws0, n, k, &ps[k], plans[k]))) return rc;
+  }
+  const uint64_t frame_px = (uint64_t)p_in->width * p_in->height;
+  if (frame_px > m->frame_px) {
+    DeviceGuard g(m->devices[0]);
+    dfree(m->d_frame_rgb);
+    dfree(m->d_frame_bgra);
+    m->d_frame_rgb = nullptr;
+    m->d_frame_bgra = nullptr;
+    m->frame_px = 0;
+    if (!dalloc(&m->d_frame_rgb, 3 * frame_px) || !dalloc(&m->d_frame_bgra, frame_px))
+      return fail(RP_ENOMEM, "hipMalloc frame");
+    m->frame_px = frame_px;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0; k < n; k++) {  // every device renders its shard into its staging buffer
+    rp_scene* s = m->scenes[k];
+    int rc = render_shard(s, &s->ws0, cam, &ps[k], s->ws0.d_gs_rgb, nullptr, m->d_ctr[k], m->streams[k]);
+    if (rc) return rc;
+    if ((rc = gather_stage(s, &s->ws0, plans[k], s->ws0.d_gs_rgb, bgra, rgb, m->streams[k]))) return rc;
+  }
+  // one thread drives every device: the collectives of all ranks form one group
+  RP_NCCL(ncclGroupStart());
+  for (int k = 0; k < n; k++) {
+    DeviceGuard g(m->devices[k]);
+    int rc = gather_collectives(m->comms[k], &m->scenes[k]->ws0, plans[k], bgra, rgb, m->d_ctr[k], m->streams[k]);
+    if (rc) {
+      (void)ncclGroupEnd();
+      return rc;
+    }
+  }
+  RP_NCCL(ncclGroupEnd());
+  rp_scene* s0 = m->scenes[0];
+  int rc = gather_assemble(s0, &s0->ws0, plans[0], bgra ? reinterpret_cast<uint8_t*>(m->d_frame_bgra) : nullptr,
+                           rgb ? m->d_frame_rgb : nullptr, m->streams[0]);
+  if (rc) return rc;
+  for (int k = 0; k < n; k++) {
+    DeviceGuard g(m->devices[k]);
+    hipError_t e = hipStreamSynchronize(m->streams[k]);
+    if (e != hipSuccess) return fail(RP_EHIP, std::string("render: ") + hipGetErrorString(e));
+  }
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  DeviceGuard g(m->devices[0]);
+  uint64_t ctr[rpk::CTR_N];
+  RP_HIP(hipMemcpy(ctr, m->d_ctr[0], sizeof ctr, hipMemcpyDeviceToHost));
+  if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
+  if (rgb) RP_HIP(hipMemcpy(out_rgb, m->d_frame_rgb, sizeof(double) * 3 * frame_px, hipMemcpyDeviceToHost));
+  if (bgra) RP_HIP(hipMemcpy(out_bgra, m->d_frame_bgra, 4 * frame_px, hipMemcpyDeviceToHost));
+  if (stats) {
+    stats->rays = ctr[rpk::CTR_RAYS];
+    stats->samples = ctr[rpk::CTR_SAMPLES];
+    stats->pixels = ctr[rpk::CTR_PIXELS];
+    stats->seconds = secs;
+  }
   return RP_OK;
 }
 

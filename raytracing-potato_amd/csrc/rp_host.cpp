@@ -1,12 +1,14 @@
 // rp_host.cpp -- librp_host.so: host-side loaders and helpers (include/rp_host.h).
 #include "../../include/rp_host.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -541,6 +543,61 @@ int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats) {
     stats[2] = ps.max_depth;
     stats[3] = desc->n_hittables;
   }
+  return RP_OK;
+}
+
+namespace {
+inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+// ChaCha12 block `ctr` of `key` (randomness.rs:5 StdRng = rand_chacha 0.3 ChaCha12Rng).
+void chacha12_block(const uint32_t key[8], uint64_t ctr, uint32_t out[16]) {
+  uint32_t x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                    key[4],      key[5],      key[6],      key[7],      (uint32_t)ctr, (uint32_t)(ctr >> 32), 0u, 0u};
+  uint32_t s[16];
+  std::memcpy(s, x, sizeof s);
+  auto qr = [&](int a, int b, int c, int d) {
+    x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 16);
+    x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 12);
+    x[a] += x[b]; x[d] ^= x[a]; x[d] = rotl32(x[d], 8);
+    x[c] += x[d]; x[b] ^= x[c]; x[b] = rotl32(x[b], 7);
+  };
+  for (int r = 0; r < 6; r++) {
+    qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+    qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+  }
+  for (int i = 0; i < 16; i++) out[i] = x[i] + s[i];
+}
+}  // namespace
+
+int rph_stdrng_u64(const uint8_t seed[32], uint64_t first, uint64_t n, uint64_t* out) {
+  if (!seed || (n && !out)) return fail("NULL argument");
+  uint32_t key[8];
+  for (int i = 0; i < 8; i++)
+    key[i] = (uint32_t)seed[4 * i] | (uint32_t)seed[4 * i + 1] << 8 | (uint32_t)seed[4 * i + 2] << 16 |
+             (uint32_t)seed[4 * i + 3] << 24;
+  // draw k = words 2k, 2k+1 of the keystream = block k / 8, u64 k % 8 of it
+  auto work = [&](uint64_t a, uint64_t b) {
+    uint32_t w[16];
+    uint64_t blk = ~0ull;
+    for (uint64_t k = a; k < b; k++) {
+      const uint64_t d = first + k;
+      if (d / 8 != blk) {
+        blk = d / 8;
+        chacha12_block(key, blk, w);
+      }
+      const uint32_t q = (uint32_t)(d % 8);
+      out[k] = (uint64_t)w[2 * q] | (uint64_t)w[2 * q + 1] << 32;
+    }
+  };
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned nt = n < (1u << 20) ? 1u : hw;
+  std::vector<std::thread> th;
+  const uint64_t per = (n + nt - 1) / nt;
+  for (unsigned t = 1; t < nt; t++) {
+    const uint64_t a = std::min<uint64_t>(n, t * per), b = std::min<uint64_t>(n, a + per);
+    if (a < b) th.emplace_back(work, a, b);
+  }
+  work(0, std::min<uint64_t>(n, per));
+  for (auto& t : th) t.join();
   return RP_OK;
 }
 

@@ -87,14 +87,14 @@ enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
 // efficiency).
 enum { SPP_BATCH = 32 };
 
-// Counter block layout (8 x uint64 in device memory), see rp.h rp_render_device.
-enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_QUEUE = 4, CTR_N = 8 };
+// Counter block layout (RP_COUNTERS_LEN x uint64 in device memory), see rp.h rp_render_device.
+enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_N = 4 };
 enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
 
-// Launch the persistent render kernel on `stream` (hipStream_t).  `counters` must have been zeroed on
-// the same stream.  Returns a hipError_t as int.
+// Launch the persistent render kernel on `stream` (hipStream_t).  `counters` and the unit-queue word
+// `queue` (workspace-owned) must have been zeroed on the same stream.  Returns a hipError_t as int.
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
-                  int grid, void* stream);
+                  uint32_t* queue, int grid, void* stream);
 
 // Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (longest sample, mean rays per probed
 // pixel), ties by tile index, into order[] (shard tile indices).  One block.
@@ -109,6 +109,17 @@ struct SrgbTable {
   double thr[256];
 };
 int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_t* bgra, void* stream);
+
+// Frame assembly of a multi-GPU frame: `gathered` holds nranks shard buffers of `stride` slots each (rank r
+// at r * stride, `words` 32-bit words per slot: 1 for BGRA8, 6 for f64 RGB); every frame pixel (i, j)
+// takes its slot from the rank that owns its tile (tile t -> rank t % nranks, shard slot k * tw * th +
+// row-major offset inside the tile, k = t / nranks: rp_shard_unpack's order).  One thread per pixel.
+struct FrameGeom {
+  uint32_t W, H, tw, th, tiles_x, nranks;
+  uint64_t stride;
+};
+int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t words, uint32_t* frame,
+                          void* stream);
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);

@@ -18,6 +18,14 @@
 
 #pragma clang fp contract(off)
 
+// Every compile-time knob below changes timing only.  Experiments that change results (timing ablations
+// with wrong streams or colours) are not kept in this file, and a build asking for one is refused so a
+// library that writes wrong frames can never be produced from it.
+#if defined(RPK_ABLATE_RNG) || defined(RPK_ABLATE_UV) || defined(RPK_ABLATE_TEX) || defined(RPK_ABLATE_METAL) || \
+    defined(RPK_BATCH_LEAF)
+#error "result-changing experiment macros are not part of the product kernel"
+#endif
+
 namespace rpk {
 
 #define RPK_INLINE __device__ __forceinline__
@@ -72,10 +80,6 @@ RPK_INLINE uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n));
 
 // ChaCha12 block (rand_chacha 0.3: 64-bit block counter in words 12-13, zero nonce).
 RPK_INLINE void chacha12(const uint32_t k[8], uint32_t ctr, uint32_t o[16]) {
-#ifdef RPK_ABLATE_RNG  // timing ablation only (wrong stream): a cheap mix instead of 12 rounds
-  for (int i = 0; i < 16; i++) { uint32_t x = k[i & 7] ^ (ctr * 0x9E3779B9u + i * 0x85EBCA6Bu); x ^= x >> 15; x *= 0x2C1B3C6Du; o[i] = x ^ (x >> 13); }
-  return;
-#endif
   uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
   uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
   uint32_t x12 = ctr, x13 = 0, x14 = 0, x15 = 0;
@@ -161,10 +165,7 @@ static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
 #ifndef RPK_PRIM_BREAK
 #define RPK_PRIM_BREAK 0
 #endif
-#ifndef RPK_BATCH_BELOW
-#define RPK_BATCH_BELOW 64
-#endif    // a lane holding <= this many blocks forces a refill pass
-static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // ... as do this many lanes with room
+static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // this many lanes with room force a refill pass
 
 struct Rng {
   uint4* slab;     // global: this lane's slab
@@ -534,7 +535,7 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const uint32_t* stk, uint32_t strid
 
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
-template <bool SPILL, bool BATCH = false>
+template <bool SPILL>
 RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
@@ -666,69 +667,6 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
       // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
       if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
       break;
-    }
-    // batched variant: the sequential loop runs while many lanes test; the stragglers' runs are batched
-    if (BATCH && (uint32_t)__popcll(__ballot(leaf != 0u)) <= RPK_BATCH_BELOW) break;
-  }
-  if (BATCH) {
-    // Batched leaf tests (experiment, RPK_BATCH_LEAF; all 64 lanes of the wave call this, lanes without a
-    // leaf as helpers): every lane's current run [k, kend) becomes jobs P..P+n-1 (P = exclusive prefix of
-    // the runs' sizes over the lanes), lane L takes job base + L, finds the owner (largest lane with
-    // P <= job) by a 6-step ds_bpermute search, tests the owner's ray against the owner's best, and each
-    // owner reduces its results in job order (min t, a later primitive wins a tie: the sequential order).
-    const uint32_t lane = __lane_id();
-    while (__ballot(leaf != 0u)) {
-      const uint32_t n = leaf != 0u ? kend - k : 0u;  // 1..8
-      uint32_t P = 0, T = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const uint64_t m = __ballot((n >> b) & 1u);
-        P += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
-        T += (uint32_t)__popcll(m) << b;
-      }
-      for (uint32_t base = 0; base < T; base += 64u) {
-        DIAG(if (td) td->tests++;)
-        DREG(DREG_PRIM)
-        const uint32_t j = base + lane;
-        uint32_t own = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-          const uint32_t cand = own + step;
-          if ((uint32_t)__shfl((int)P, (int)cand) <= j) own = cand;
-        }
-        const uint32_t Po = (uint32_t)__shfl((int)P, (int)own), ko = (uint32_t)__shfl((int)k, (int)own);
-        const V3 oo = v3(__shfl(o.x, (int)own), __shfl(o.y, (int)own), __shfl(o.z, (int)own));
-        const V3 dd = v3(__shfl(d.x, (int)own), __shfl(d.y, (int)own), __shfl(d.z, (int)own));
-        double bt = __shfl(best, (int)own);
-        TravState tmp;
-        tmp.bestp = -1;
-        tmp.bu = 0.0;
-        tmp.bv = 0.0;
-        if (j < T) prim_test(S, ko + (j - Po), oo, dd, tmin, bt, tmp);
-        const double tres = tmp.bestp >= 0 ? bt : __builtin_nan("");
-        // owners: results of jobs P + i in this round, in order
-        int win = -1;
-        for (uint32_t i = 0; __ballot(i < n); i++) {
-          const uint32_t jj = P + i;
-          const bool mine = i < n && jj >= base && jj < base + 64u;
-          const double ti = __shfl(tres, (int)((jj - base) & 63u));
-          if (mine && ti <= best) { best = ti; win = (int)(jj - base); }
-        }
-        const double uw = __shfl(tmp.bu, win & 63), vw = __shfl(tmp.bv, win & 63);
-        const int pw = __shfl(tmp.bestp, win & 63);
-        if (win >= 0) { ts.bestp = pw; ts.bu = uw; ts.bv = vw; }
-      }
-      // every run is done: the next leaf of each lane, as the sequential loop chains them
-      if (leaf != 0u) {
-        if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
-          leaf = cur;
-          cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
-          k = leaf & rpl::LEAF_FIRST_MASK;
-          kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
-        } else {
-          leaf = 0u;
-        }
-      }
     }
   }
   ts.cur = cur;
@@ -996,6 +934,7 @@ struct KArgs {
   double* out;
   float* out_fg;
   unsigned long long* ctr;
+  unsigned int* queue;       // the unit queue's next index (workspace-owned, zeroed before the launch)
   unsigned long long* diag;  // RPK_DIAG builds only (DIAG_N counters)
 };
 typedef const __attribute__((address_space(4))) KArgs* KArgsPtr;
@@ -1041,7 +980,7 @@ RPK_INLINE KArgsPtr kargs() {
 template <bool PROBE>
 RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t& batch) {
   KArgsPtr A = kargs();
-  unsigned int* queue = reinterpret_cast<unsigned int*>(A->ctr + CTR_QUEUE);
+  unsigned int* queue = A->queue;
   const uint32_t tw = A->P.tw, th = A->P.th;
   if (PROBE && A->P.probe_n) {  // cost probe: an n x n lattice per tile (cell centres), clamped into the frame
     slot = atomicAdd(queue, 1u);
@@ -1199,7 +1138,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   hits = 0;
   sum_x = sum_y = sum_z = 0.0;
   TravState ts;
-  ts.cur = rpl::ENTRY_EMPTY;  // no ray: done (RPK_BATCH_LEAF steps every lane)
+  ts.cur = rpl::ENTRY_EMPTY;  // no ray: done
   ts.leaf = 0u;
   ts.sp = 0u;
   ts.best = 0.0;
@@ -1258,14 +1197,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       Ray32 r;
       setup_ray32(o, d, RAY_EPSILON, r);
       for (;;) {
-#ifdef RPK_BATCH_LEAF
-        // every lane steps (idle lanes hold cur = EMPTY, no leaf: they only help with the leaf tests)
-        {
-          DREG(DREG_STEP)
-          trav_step<SPILL, true>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
-          if (alive) tdone = trav_done(ts);
-        }
-#else
         if (alive && !tdone) {
           DREG(DREG_STEP)
 #ifdef RPK_DIAG
@@ -1275,7 +1206,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 #endif
           tdone = trav_done(ts);
         }
-#endif
         const uint64_t act = __ballot(alive && !tdone);
         const uint64_t waiting = __ballot(alive && tdone);
         if (act == 0 || (waiting != 0 && (uint32_t)__popcll(act) < thr)) break;
@@ -1320,9 +1250,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           h.material = 0;
           sph_uv = S.background.needs_uv != 0;
         }
-#ifdef RPK_ABLATE_UV  // timing ablation only (colours change, rays do not)
-        sph_uv = false;
-#endif
         if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
           DREG(DREG_SPHUV)
           const V3 q = hit ? h.n : d;
@@ -1334,10 +1261,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         // the load latency overlaps it.  A hit reading both takes the second in a rare extra pass.
         const uint32_t emit_kind = hit ? m->emit_kind : S.background.kind;
         const uint32_t emit_tex = hit ? m->emit_tex : S.background.tex;
-        bool ta = hit && m->absorb_kind == 3, te = emit_kind == 4;
-#ifdef RPK_ABLATE_TEX  // timing ablation only (colours change, rays do not)
-        ta = te = false;
-#endif
+        const bool ta = hit && m->absorb_kind == 3, te = emit_kind == 4;
         const bool t1 = ta || te;
         uint32_t tid1 = 0, px1 = 0;
         // a miss under an Image sky sphere: size and offset are kernel arguments (scalar registers), so the
@@ -1518,8 +1442,8 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
   if (overflow) atomicOr(&ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
 }
 
-int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters, int grid,
-                  void* stream) {
+int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
+                  uint32_t* queue, int grid, void* stream) {
   const size_t lds = (size_t)s.lds_depth * BLOCK * sizeof(uint32_t);
   const bool spill = s.lds_depth < s.stack_depth;
   KArgs a;
@@ -1528,6 +1452,7 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.out = out_rgb;
   a.out_fg = out_fg;
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
+  a.queue = queue;
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
   if (p.probe && spill) hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
   else if (p.probe) hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
@@ -1600,6 +1525,31 @@ int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_
   const uint64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
   hipLaunchKernelGGL(srgb_bgra_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, tab, rgb, n,
                      reinterpret_cast<uint32_t*>(bgra));
+  return (int)hipGetLastError();
+}
+
+// Multi-GPU frame assembly (rp_frame_gather): frame pixel (i, j) <- the slot of the rank owning its tile.
+// Consecutive threads take consecutive pixels of a row, so the frame writes are coalesced; the reads are
+// runs of tw slots.
+__global__ void __launch_bounds__(256) frame_assemble_kernel(const FrameGeom g, const uint32_t* __restrict__ src,
+                                                            uint32_t words, uint32_t* __restrict__ frame) {
+  const uint64_t n = (uint64_t)g.W * g.H;
+  for (uint64_t px = (uint64_t)blockIdx.x * 256 + threadIdx.x; px < n; px += (uint64_t)gridDim.x * 256) {
+    const uint32_t j = (uint32_t)(px / g.W), i = (uint32_t)(px - (uint64_t)j * g.W);
+    const uint32_t t = (j / g.th) * g.tiles_x + i / g.tw;
+    const uint32_t r = t % g.nranks, k = t / g.nranks;
+    const uint64_t slot = (uint64_t)k * g.tw * g.th + (uint64_t)(j % g.th) * g.tw + i % g.tw;
+    const uint32_t* s = src + ((uint64_t)r * g.stride + slot) * words;
+    for (uint32_t w = 0; w < words; w++) frame[px * words + w] = s[w];
+  }
+}
+
+int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t words, uint32_t* frame, void* stream) {
+  const uint64_t n = (uint64_t)g.W * g.H;
+  if (n == 0) return 0;
+  const uint64_t blocks = (n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536;
+  hipLaunchKernelGGL(frame_assemble_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, g, gathered,
+                     words, frame);
   return (int)hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int, c_in
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 
-RP_OK, RP_EINVAL, RP_EHIP, RP_ENOMEM, RP_ENODEV, RP_EINTERNAL = 0, -1, -2, -3, -4, -5
+RP_OK, RP_EINVAL, RP_EHIP, RP_ENOMEM, RP_ENODEV, RP_EINTERNAL, RP_ERCCL = 0, -1, -2, -3, -4, -5, -6
 RP_HITTABLE_SPHERE, RP_HITTABLE_TRIANGLE = 0, 1
 RP_SCATTER_NONE, RP_SCATTER_LAMBERT, RP_SCATTER_METAL, RP_SCATTER_DIELECTRIC = 0, 1, 2, 3
 RP_ABSORB_BLACK_BODY, RP_ABSORB_WHITE_BODY, RP_ABSORB_ALBEDO, RP_ABSORB_ALBEDO_MAP = 0, 1, 2, 3
@@ -23,7 +23,10 @@ RP_ABSORB_BLACK_BODY, RP_ABSORB_WHITE_BODY, RP_ABSORB_ALBEDO, RP_ABSORB_ALBEDO_M
 (RP_TEXTURE_MISSING, RP_TEXTURE_DEBUG_UVS, RP_TEXTURE_SOLID, RP_TEXTURE_IMAGE, RP_TEXTURE_CHECKER,
  RP_TEXTURE_NOISE, RP_TEXTURE_PERLIN) = range(7)
 RP_ROOT_BVH, RP_ROOT_LIST = 0, 1
-RP_COUNTERS_LEN = 8  # device counter block: rays, samples, pixels, status, queue, reserved x3
+RP_COUNTERS_LEN = 4  # device counter block: rays, samples, pixels, status (include/rp.h)
+RP_SAMPLES_PER_STREAM = 32
+RP_COMM_ID_BYTES = 128
+RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
 
 
 class rp_hittable(Structure):
@@ -74,7 +77,14 @@ class rp_camera(Structure):
 class rp_render_params(Structure):
     _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_bounce", c_uint32),
                 ("seed", c_uint64), ("tile_w", c_uint32), ("tile_h", c_uint32), ("shard", c_uint32),
-                ("num_shards", c_uint32)]
+                ("num_shards", c_uint32), ("samples_per_stream", c_uint32), ("reserved", c_uint32)]
+
+
+class rp_scene_options(Structure):
+    _fields_ = [("builder", c_uint32), ("max_leaf", c_uint32), ("cost_traverse", c_double),
+                ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
+                ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
+                ("reserved", c_uint32 * 4)]
 
 
 class rp_stats(Structure):
@@ -106,9 +116,13 @@ _host = None
 RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_create", "rp_scene_destroy",
               "rp_scene_info", "rp_shard_pixel_count", "rp_shard_unpack", "rp_render", "rp_render_device",
               "rp_intersect", "rp_diagnostics", "rp_workspace_create", "rp_workspace_destroy",
-              "rp_render_device_ws", "rp_shard_to_bgra8", "rp_srgb_thresholds"]
+              "rp_render_device_ws", "rp_shard_to_bgra8", "rp_srgb_thresholds", "rp_scene_options_init",
+              "rp_scene_create_ex", "rp_workspace_reserve", "rp_comm_unique_id", "rp_comm_create", "rp_comm_destroy",
+              "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
+              "rp_render_multi"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
-                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_last_error"]
+                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_last_error",
+                "rph_stdrng_u64"]
 
 
 def rp_lib_path() -> str:
@@ -124,7 +138,7 @@ def rp() -> ctypes.CDLL:
     global _rp
     if _rp is not None:
         return _rp
-    path = os.environ.get("RP_LIB") or rp_lib_path()  # RP_LIB: e.g. lib/librp_diag.so
+    path = os.environ.get("RP_LIB") or rp_lib_path()  # RP_LIB: lib/librp_diag.so (diagnostic counters)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `make -C raytracing-potato_amd` "
                            "(or __graft_entry__.build()); there is no CPU fallback for the render path")
@@ -156,6 +170,28 @@ def rp() -> ctypes.CDLL:
     lib.rp_srgb_thresholds.argtypes = [c_void_p]
     lib.rp_intersect.argtypes = [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]
     lib.rp_diagnostics.argtypes = [c_void_p, c_void_p, c_uint32, c_int]
+    lib.rp_scene_options_init.argtypes = [POINTER(rp_scene_options)]
+    lib.rp_scene_create_ex.argtypes = [POINTER(rp_scene_desc), c_int, POINTER(rp_scene_options), POINTER(c_void_p)]
+    lib.rp_workspace_reserve.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params)]
+    lib.rp_comm_unique_id.argtypes = [c_void_p]
+    lib.rp_comm_create.argtypes = [c_void_p, c_int, c_int, c_int, POINTER(c_void_p)]
+    lib.rp_comm_destroy.argtypes = [c_void_p]
+    lib.rp_comm_destroy.restype = None
+    lib.rp_comm_info.argtypes = [c_void_p, POINTER(c_int), POINTER(c_int), POINTER(c_int)]
+    lib.rp_frame_gather.argtypes = [c_void_p, c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]
+    lib.rp_gather_stride.argtypes = [POINTER(rp_render_params), POINTER(c_uint64)]
+    lib.rp_frame_assemble.argtypes = [POINTER(rp_render_params), c_void_p, c_uint32, c_void_p, c_void_p]
+    lib.rp_render_gather.argtypes = [c_void_p, c_void_p, c_void_p, POINTER(rp_camera), POINTER(rp_render_params),
+                                     c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.rp_multi_create.argtypes = [POINTER(rp_scene_desc), c_void_p, c_int, POINTER(rp_scene_options),
+                                    POINTER(c_void_p)]
+    lib.rp_multi_destroy.argtypes = [c_void_p]
+    lib.rp_multi_destroy.restype = None
+    lib.rp_render_multi.argtypes = [c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p, c_void_p,
+                                    POINTER(rp_stats)]
+    if lib.rp_abi_version() != 4:
+        raise RuntimeError(f"{path}: ABI version {lib.rp_abi_version()}, bindings expect 4 (rebuild)")
     _rp = lib
     return lib
 
@@ -183,6 +219,7 @@ def host() -> ctypes.CDLL:
     lib.rph_bvh_selfcheck.argtypes = [POINTER(rp_scene_desc), POINTER(c_uint64)]
     lib.rph_bvh_traversal_stats.argtypes = [POINTER(rp_scene_desc), c_void_p, c_uint64, c_void_p]
     lib.rph_last_error.restype = c_char_p
+    lib.rph_stdrng_u64.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p]
     _host = lib
     return lib
 

@@ -1,10 +1,12 @@
-"""Multi-GPU frame assembly: one process per GPU, image tiles interleaved across ranks (tile t goes to
-rank t % world), one collective per frame -- an all-gather of the per-rank shard buffers over RCCL
-(xGMI) -- then a device-side scatter of slot order into frame order.  The scene is replicated per GPU.
+"""Multi-GPU frames: one process per GPU, image tiles interleaved across ranks (tile t goes to rank t %
+world), one RCCL all-gather per frame over xGMI inside librp.so (rp_frame_gather / rp_render_gather), then
+a device-side de-interleave into frame order.  The scene is replicated per GPU.
 
-The reference's only parallelism is its thread tile queue (main.rs:36-98, `Arc<Mutex<Vec<Tile>>>`);
-this replaces it across devices.  Per-pixel RNG seeding makes the gathered frame bitwise identical for
-any world size (tests/test_dist.py, tests/test_gpu_parity.py::test_shards_cover_frame_bitwise).
+The reference's only parallelism is its thread tile queue (main.rs:36-98, `Arc<Mutex<Vec<Tile>>>`); this
+replaces it across devices.  Per-pixel RNG seeding makes the gathered frame bitwise identical for any world
+size (tests/test_dist.py, tests/test_gpu_configs.py).  torch.distributed (gloo) is only the bootstrap: it
+carries rank 0's RCCL unique id to the other ranks and the benchmark's barrier and max-time reduction; the
+frame itself never passes through torch.
 """
 from __future__ import annotations
 
@@ -12,7 +14,7 @@ from dataclasses import replace
 
 import numpy as np
 
-from .scene import RenderParams, shard_slot_count, shard_slot_pixels
+from .scene import RenderParams, shard_slot_count
 
 
 def shard_params(params: RenderParams, rank: int, world: int) -> RenderParams:
@@ -20,71 +22,38 @@ def shard_params(params: RenderParams, rank: int, world: int) -> RenderParams:
 
 
 def max_slots(params: RenderParams, world: int) -> int:
-    """Shard 0 holds the most tiles: the padded per-rank buffer length (in pixels) for the all-gather."""
+    """Shard 0 holds the most tiles: the per-rank buffer length (slots) of a gathered frame
+    (rp_gather_stride)."""
     return shard_slot_count(replace(params, shard=0, num_shards=world))
 
 
-class FrameAssembler:
-    """Precomputed (slot -> pixel) scatter indices for every rank's shard, as torch tensors on `device`."""
+def assemble_frame(gathered: np.ndarray, params: RenderParams, world: int) -> np.ndarray:
+    """NumPy restatement of the device frame assembly (rp_kernel.hip frame_assemble_kernel, rp_frame_assemble):
+    gathered = (world * stride, C) slots, rank r's shard at r * stride; returns (H, W, C) in frame order.
+    Pixel (i, j) is in tile t = (j / th) * tiles_x + i / tw, owned by rank t % world as its shard tile
+    k = t / world, slot k * tw * th + (j % th) * tw + i % tw."""
+    tw, th = params.tile_w, params.tile_h
+    tiles_x = -(-params.width // tw)
+    stride = max_slots(params, world)
+    j, i = np.mgrid[0:params.height, 0:params.width]
+    t = (j // th) * tiles_x + i // tw
+    r, k = t % world, t // world
+    slot = r * stride + k * tw * th + (j % th) * tw + i % tw
+    return gathered[slot]
 
-    def __init__(self, params: RenderParams, world: int, device):
-        import torch
-        self.params = params
-        self.world = world
-        self.slots = max_slots(params, world)
-        src, dst = [], []
-        for r in range(world):
-            pix = shard_slot_pixels(shard_params(params, r, world))
-            ok = np.nonzero(pix >= 0)[0]
-            src.append(r * self.slots + ok)
-            dst.append(pix[ok])
-        self.src = torch.as_tensor(np.concatenate(src), dtype=torch.int64, device=device)
-        self.dst = torch.as_tensor(np.concatenate(dst), dtype=torch.int64, device=device)
-        self.device = device
 
-    def new_shard_buffer(self, dtype=None):
-        import torch
-        return torch.zeros(3 * self.slots, dtype=dtype or torch.float64, device=self.device)
+def share_unique_id(rank: int, world: int, group=None) -> bytes:
+    """Rank 0's RCCL unique id (rp_comm_unique_id), broadcast to every rank over torch.distributed (any
+    backend; gloo suffices)."""
+    import torch.distributed as dist
+    from .render import comm_unique_id
+    box = [comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(box, src=0, group=group)
+    return box[0]
 
-    def gather(self, shard_buf, group=None, out=None):
-        """All-gather every rank's shard buffer and scatter into an (h, w, 3) frame tensor (every rank)."""
-        import torch
-        import torch.distributed as dist
-        p = self.params
-        if self.world > 1:
-            gathered = torch.empty(self.world * 3 * self.slots, dtype=shard_buf.dtype, device=shard_buf.device)
-            if dist.get_backend(group) == "gloo":  # gloo has no all_gather_into_tensor
-                dist.all_gather(list(gathered.view(self.world, -1).unbind(0)), shard_buf, group=group)
-            else:
-                dist.all_gather_into_tensor(gathered, shard_buf, group=group)
-        else:
-            gathered = shard_buf
-        if out is None:
-            out = torch.zeros(p.height * p.width, 3, dtype=shard_buf.dtype, device=shard_buf.device)
-        out.view(-1, 3)[self.dst] = gathered.view(-1, 3)[self.src]
-        return out.view(p.height, p.width, 3)
 
-    def new_bgra_buffer(self):
-        import torch
-        return torch.zeros(4 * self.slots, dtype=torch.uint8, device=self.device)
-
-    def gather_bgra(self, shard_bgra, group=None, out=None):
-        """Like gather() for the output stage's bytes (DeviceScene.to_bgra8): 4 bytes per pixel instead of
-        24, moved and scattered as one int32 each; returns the (h, w, 4) B, G, R, A frame -- the body of
-        the reference's output.tga (rtpotato.render.tga_bytes)."""
-        import torch
-        import torch.distributed as dist
-        p = self.params
-        words = shard_bgra.view(torch.int32)
-        if self.world > 1:
-            gathered = torch.empty(self.world * self.slots, dtype=torch.int32, device=words.device)
-            if dist.get_backend(group) == "gloo":
-                dist.all_gather(list(gathered.view(self.world, -1).unbind(0)), words, group=group)
-            else:
-                dist.all_gather_into_tensor(gathered, words, group=group)
-        else:
-            gathered = words
-        if out is None:
-            out = torch.zeros(p.height * p.width * 4, dtype=torch.uint8, device=words.device)
-        out.view(torch.int32)[self.dst] = gathered[self.src]
-        return out.view(p.height, p.width, 4)
+def bootstrap_comm(rank: int, world: int, device: int, group=None):
+    """rp_comm for this rank on `device`: every rank joins rank 0's communicator (rp_comm_create)."""
+    from .render import Comm
+    return Comm(share_unique_id(rank, world, group), world, rank, device)

@@ -13,15 +13,32 @@ from . import _ffi as F
 from .scene import RenderParams, Scene, shard_slot_count
 
 
-class DeviceScene:
-    """rp_scene: the scene's acceleration structure and tables resident in one GPU's HBM."""
+def scene_options(**kw) -> F.rp_scene_options:
+    """rp_scene_options with the library defaults (rp_scene_options_init), fields overridden by keyword:
+    builder ("auto" | "host" | "gpu" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
+    self_check, trav_threshold, tile_order, probe_n."""
+    o = F.rp_scene_options()
+    F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
+    for k, v in kw.items():
+        if k == "builder" and isinstance(v, str):
+            v = {"auto": F.RP_BUILDER_AUTO, "host": F.RP_BUILDER_HOST, "gpu": F.RP_BUILDER_DEVICE}[v]
+        if not hasattr(o, k) or k == "reserved":
+            raise KeyError(f"unknown scene option {k!r}")
+        setattr(o, k, v)
+    return o
 
-    def __init__(self, scene: Scene, device: int = 0):
+
+class DeviceScene:
+    """rp_scene: the scene's acceleration structure and tables resident in one GPU's HBM.  `options`: a dict of
+    rp_scene_options fields (scene_options())."""
+
+    def __init__(self, scene: Scene, device: int = 0, options: dict | None = None):
         self.scene = scene
         self.device = device
         self._desc = scene.desc()
         h = ctypes.c_void_p()
-        F.check(F.rp().rp_scene_create(self._desc.ptr(), device, ctypes.byref(h)))
+        opt = scene_options(**(options or {}))
+        F.check(F.rp().rp_scene_create_ex(self._desc.ptr(), device, ctypes.byref(opt), ctypes.byref(h)))
         self.handle = h
 
     def info(self) -> dict:
@@ -58,6 +75,12 @@ class DeviceScene:
     def __exit__(self, *exc):
         self.close()
 
+    def reserve(self, params: RenderParams, workspace: "Workspace | None" = None) -> None:
+        """rp_workspace_reserve: device memory the asynchronous renders (and frame gathers) of `params`' shape
+        need, in `workspace` (default: the scene's own)."""
+        p = params.to_c()
+        F.check(F.rp().rp_workspace_reserve(self.handle, workspace.handle if workspace else None, ctypes.byref(p)))
+
     # ---- synchronous host-buffer render -----------------------------------------------------------
     def render(self, params: RenderParams, camera=None, foreground: bool = False):
         """Full frame (only the shard's pixels written, others zero): (rgb (h, w, 3) f64,
@@ -75,8 +98,9 @@ class DeviceScene:
     def render_device(self, params: RenderParams, out, counters, fg=None, camera=None, stream=None,
                       workspace: "Workspace | None" = None) -> None:
         """Render the shard into `out` (torch f64 tensor, >= shard_slot_count*3 elements) on `stream`
-        (torch stream; default: current).  counters: torch int64 tensor of 8 elements.  workspace: one
-        from self.workspace() (default: the scene's own, rp_render_device)."""
+        (torch stream; default: current).  counters: torch int64 tensor of RP_COUNTERS_LEN elements.
+        workspace: one from self.workspace() (default: the scene's own, rp_render_device); frames of more
+        than one sample batch need self.reserve(params, workspace) first."""
         import torch
         cam = (camera or self.scene.camera).to_c()
         p = params.to_c()
@@ -105,6 +129,41 @@ class DeviceScene:
         F.check(F.rp().rp_shard_to_bgra8(self.handle, ctypes.byref(p), shard_rgb.data_ptr(), out.data_ptr(),
                                          ctypes.c_void_p(s.cuda_stream)))
 
+    def frame_gather(self, comm: "Comm", params: RenderParams, shard_rgb, frame_bgra=None, frame_rgb=None,
+                     counters=None, stream=None, workspace: "Workspace | None" = None) -> None:
+        """rp_frame_gather: this rank's finished shard (`shard_rgb`, torch f64) all-gathered over RCCL with the
+        other ranks' and de-interleaved into frame order: `frame_bgra` (torch uint8, W*H*4: to_srgb_u8 in
+        tga::save order) and/or `frame_rgb` (torch f64, W*H*3); `counters` (int64, 4) summed over ranks."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(shard_rgb.device)
+        n = params.width * params.height
+        if frame_bgra is not None:
+            assert frame_bgra.dtype == torch.uint8 and frame_bgra.is_cuda and frame_bgra.numel() >= 4 * n
+        if frame_rgb is not None:
+            assert frame_rgb.dtype == torch.float64 and frame_rgb.is_cuda and frame_rgb.numel() >= 3 * n
+        p = params.to_c()
+        F.check(F.rp().rp_frame_gather(comm.handle, self.handle, workspace.handle if workspace else None,
+                                       ctypes.byref(p), shard_rgb.data_ptr(),
+                                       frame_bgra.data_ptr() if frame_bgra is not None else None,
+                                       frame_rgb.data_ptr() if frame_rgb is not None else None,
+                                       counters.data_ptr() if counters is not None else None,
+                                       ctypes.c_void_p(s.cuda_stream)))
+
+    def render_gather(self, comm: "Comm", params: RenderParams, frame_bgra=None, frame_rgb=None, counters=None,
+                      camera=None, stream=None, workspace: "Workspace | None" = None) -> None:
+        """rp_render_gather: render this rank's shard and gather the frame (see frame_gather)."""
+        import torch
+        dev = (frame_bgra if frame_bgra is not None else frame_rgb).device
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        cam = (camera or self.scene.camera).to_c()
+        p = params.to_c()
+        F.check(F.rp().rp_render_gather(comm.handle, self.handle, workspace.handle if workspace else None,
+                                        ctypes.byref(cam), ctypes.byref(p),
+                                        frame_bgra.data_ptr() if frame_bgra is not None else None,
+                                        frame_rgb.data_ptr() if frame_rgb is not None else None,
+                                        counters.data_ptr() if counters is not None else None,
+                                        ctypes.c_void_p(s.cuda_stream)))
+
     def intersect(self, rays: np.ndarray):
         """Hittable::hit on the root for (n, 8) rays -> ((n, 9) hits, (n,) material ids)."""
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 8)
@@ -130,6 +189,73 @@ class Workspace:
             ws = self.scene.__dict__.get("_workspaces", [])
             if self in ws:
                 ws.remove(self)
+
+
+def comm_unique_id() -> bytes:
+    """rp_comm_unique_id: the RCCL id rank 0 makes and shares with the other ranks out of band."""
+    buf = (ctypes.c_uint8 * F.RP_COMM_ID_BYTES)()
+    F.check(F.rp().rp_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """rp_comm: this rank's RCCL communicator (one process per GPU)."""
+
+    def __init__(self, unique_id: bytes, nranks: int, rank: int, device: int):
+        assert len(unique_id) == F.RP_COMM_ID_BYTES
+        h = ctypes.c_void_p()
+        buf = (ctypes.c_uint8 * F.RP_COMM_ID_BYTES).from_buffer_copy(unique_id)
+        F.check(F.rp().rp_comm_create(buf, nranks, rank, device, ctypes.byref(h)))
+        self.handle = h
+        self.nranks, self.rank, self.device = nranks, rank, device
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            F.rp().rp_comm_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class MultiScene:
+    """rp_multi: one process driving several GPUs (a scene copy per device, one RCCL communicator)."""
+
+    def __init__(self, scene: Scene, devices, options: dict | None = None):
+        self.scene = scene
+        self._desc = scene.desc()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        opt = scene_options(**(options or {}))
+        h = ctypes.c_void_p()
+        F.check(F.rp().rp_multi_create(self._desc.ptr(), devs, len(devices), ctypes.byref(opt), ctypes.byref(h)))
+        self.handle = h
+        self.devices = list(devices)
+
+    def render(self, params: RenderParams, camera=None, rgb: bool = True, bgra: bool = False):
+        """rp_render_multi: (rgb (h, w, 3) f64 or None, bgra (h, w, 4) u8 or None, stats)."""
+        cam = (camera or self.scene.camera).to_c()
+        p = params.to_c()
+        out = np.zeros((params.height, params.width, 3)) if rgb else None
+        ob = np.zeros((params.height, params.width, 4), dtype=np.uint8) if bgra else None
+        st = F.rp_stats()
+        F.check(F.rp().rp_render_multi(self.handle, ctypes.byref(cam), ctypes.byref(p),
+                                       out.ctypes.data if out is not None else None,
+                                       ob.ctypes.data if ob is not None else None, ctypes.byref(st)))
+        return out, ob, {"rays": st.rays, "samples": st.samples, "pixels": st.pixels, "seconds": st.seconds}
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            F.rp().rp_multi_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def unpack_shard(params: RenderParams, shard_buf: np.ndarray, channels: int = 3,
@@ -169,7 +295,8 @@ def device_count() -> int:
     return n.value if rc == F.RP_OK else 0
 
 
-def render(scene: Scene, params: RenderParams, device: int = 0, foreground: bool = False):
+def render(scene: Scene, params: RenderParams, device: int = 0, foreground: bool = False,
+           options: dict | None = None):
     """One-shot: upload the scene, render the frame, return (rgb, fg, stats)."""
-    with DeviceScene(scene, device) as ds:
+    with DeviceScene(scene, device, options) as ds:
         return ds.render(params, foreground=foreground)

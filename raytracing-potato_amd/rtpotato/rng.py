@@ -11,6 +11,7 @@ import numpy as np
 
 _CONST = np.array([0x61707865, 0x3320646E, 0x79622D32, 0x6B206574], dtype=np.uint32)
 MASK64 = (1 << 64) - 1
+BULK_DRAWS = 1 << 20  # draws per call from which the threaded C++ generator takes over
 
 
 def _rotl(x: np.ndarray, n: int) -> np.ndarray:
@@ -85,6 +86,14 @@ class StdRng:
         self._cache_start = first_block * 8
 
     def next_u64_array(self, n: int) -> np.ndarray:
+        if n >= BULK_DRAWS:  # bulk: the host library's threaded ChaCha12 (rph_stdrng_u64), same stream
+            import ctypes
+            from . import _ffi as F
+            out = np.empty(n, dtype=np.uint64)
+            seed = np.ascontiguousarray(self.key, dtype="<u4").tobytes()
+            F.check_host(F.host().rph_stdrng_u64(seed, self.pos, n, out.ctypes.data))
+            self.pos += n
+            return out
         self._ensure(n)
         a = self._cache[self.pos - self._cache_start: self.pos - self._cache_start + n]
         self.pos += n

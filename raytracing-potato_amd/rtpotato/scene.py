@@ -349,12 +349,14 @@ class RenderParams:
     tile_h: int = 32
     shard: int = 0
     num_shards: int = 1
+    samples_per_stream: int = 0  # RNG contract batch size (0 -> RP_SAMPLES_PER_STREAM = 32; >= spp: one stream)
 
     def to_c(self) -> F.rp_render_params:
         p = F.rp_render_params()
         p.width, p.height, p.spp, p.max_bounce = self.width, self.height, self.spp, self.max_bounce
         p.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         p.tile_w, p.tile_h, p.shard, p.num_shards = self.tile_w, self.tile_h, self.shard, self.num_shards
+        p.samples_per_stream = self.samples_per_stream
         return p
 
 

@@ -147,6 +147,46 @@ def bunny_full() -> Scene:  # config C3 / C4
     return _bunny_scene("bunny", materials, textures, Emit.SkySphere(0), extra, name="bunny_full")
 
 
+def variants() -> Scene:
+    """Not in example_scenes.rs: the material and texture variants no catalogue scene uses, in one small
+    scene -- Emit::Color as a light and on a scattering surface (material.rs:52), Texture::Noise with a
+    positive and a negative seed (texture.rs:62-68), Texture::DebugUVs on a sphere and on an uv-mapped
+    triangle (texture.rs:24), Texture::Missing (texture.rs:23) and an Emit::None background (material.rs:51):
+    all light comes from the emissive sphere."""
+    textures = [Texture.Noise(7), Texture.DebugUVs, Texture.Missing, Texture.Noise(-3)]
+    materials = [
+        Material.new(Scatter.Lambert, Absorb.AlbedoMap(0), Emit.None_),                             # ground: Noise
+        Material.new(Scatter.None_, Absorb.BlackBody, Emit.Color(rgb(4.0, 3.5, 3.0))),               # light
+        Material.new(Scatter.Lambert, Absorb.AlbedoMap(1), Emit.None_),                             # DebugUVs
+        Material.new(Scatter.Metal(0.3), Absorb.AlbedoMap(2), Emit.Color(rgb(0.25, 0.125, 0.0625))),  # Missing
+        Material.new(Scatter.Dielectric(1.3), Absorb.AlbedoMap(3), Emit.None_),                     # Noise(-3)
+    ]
+    mesh = Mesh(np.array([[-3.0, -0.5, -3.0], [3.0, -0.5, -3.0], [0.0, 3.0, -3.5]]),
+                np.array([[0.0, 0.0, 1.0]] * 3), np.array([[0.0, 0.0], [1.0, 0.0], [0.5, 1.0]]),
+                np.array([0, 1, 2], dtype=np.uint32), material=2)
+    root = hittables(Hittable.Sphere((0.0, -100.5, -1.0), 100.0, 0), Hittable.Sphere((0.0, 2.2, -1.2), 0.8, 1),
+                     Hittable.Sphere((-1.1, 0.0, -1.0), 0.5, 2), Hittable.Sphere((0.0, 0.0, -1.0), 0.5, 3),
+                     Hittable.Sphere((1.1, 0.0, -1.0), 0.5, 4), Hittable.Triangle(0, 0))
+    cam = _cam(FRAC_PI_2, 1.0, 0.0, (0.0, 1.0, 2.5), (0.0, 0.2, -1.0))
+    return Scene(cam, SceneData(materials, textures, [mesh]), root, Emit.None_, F.RP_ROOT_BVH, "variants")
+
+
+def variants_sky() -> Scene:
+    """Not in example_scenes.rs: Emit::SkySphere over a non-image texture (DebugUVs) as the background, a
+    surface that reads two textures in one hit (Absorb::AlbedoMap of a Checker of Noise / DebugUVs and
+    Emit::SkySphere of a Perlin texture, sampled at the hit record: material.rs:59), on a List root."""
+    textures = [Texture.DebugUVs, Texture.Noise(11), Texture.Checker(0, 1), Texture.Perlin(5), Texture.Missing]
+    materials = [
+        Material.new(Scatter.Lambert, Absorb.AlbedoMap(2), Emit.SkySphere(3)),
+        Material.new(Scatter.Metal(0.1), Absorb.AlbedoMap(4), Emit.SkySphere(0)),
+        Material.new(Scatter.Lambert, Absorb.AlbedoMap(1), Emit.None_),
+    ]
+    root = hittables(Hittable.Sphere((0.0, -50.5, -1.0), 50.0, 2), Hittable.Sphere((-0.6, 0.1, -1.0), 0.6, 0),
+                     Hittable.Sphere((0.7, 0.0, -1.3), 0.5, 1))
+    cam = _cam(FRAC_PI_2, 1.0, 0.0, (0.0, 0.8, 1.8), (0.0, 0.0, -1.0))
+    return Scene(cam, SceneData(materials, textures, []), root, Emit.SkySphere(0), F.RP_ROOT_LIST, "variants_sky")
+
+
 def random_mesh(n_triangles: int = 10_000_000, seed: int = 0xC5) -> Scene:
     """Config C5: n random small triangles.  Per triangle, in draw order: centroid (3 x ClosedRange(-1, 1)),
     then 9 offsets ClosedRange(-0.005, 0.005) for vertices a, b, c; flat normal normalize((b-a) x (c-a))."""
@@ -172,6 +212,7 @@ CATALOGUE = {
     "three_balls": three_balls, "more_balls": more_balls, "more_balls_optimized": more_balls_optimized,
     "two_balls": two_balls, "earth": earth, "one_triangle": one_triangle, "glass_bunny": glass_bunny,
     "bunny": bunny, "bunny_lambert": bunny_lambert, "bunny_full": bunny_full, "random_mesh": random_mesh,
+    "variants": variants, "variants_sky": variants_sky,
 }
 
 

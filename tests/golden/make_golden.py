@@ -127,6 +127,39 @@ def matvec(m, v):  # column-major, column axpy accumulation
             (v[0] * m[2] + v[1] * m[5]) + v[2] * m[8])
 
 
+# ------------------------------------------------------------------ noise (randomness.rs:86-110)
+_M64 = 1 << 64
+
+
+def _wrap(x):  # Wrapping<isize>: two's-complement 64-bit
+    x %= _M64
+    return x - _M64 if x >= 1 << 63 else x
+
+
+def _floor(x):
+    return float(np.floor(x))
+
+
+def _as_isize(x):  # Rust `f64 as isize`: saturating, NaN -> 0
+    if x != x:
+        return 0
+    if x >= 9223372036854775807.0:
+        return (1 << 63) - 1
+    if x <= -9223372036854775808.0:
+        return -(1 << 63)
+    return int(x)
+
+
+def noise_integer(x, y, z, seed):
+    h = _wrap(0x369E6D3B899E43CF * x + 0x53F89E7FFDA3B07D * y + 0x3B13C1CA4937E629 * z + 0x577C2C6E4019D645 * seed)
+    h = _wrap((h >> 13) ^ h)  # arithmetic shift of the signed value
+    return _wrap(h * (h * h * 60493 + 19990303) + 1376312589)
+
+
+def noise_real(x, y, z, seed):
+    return float(noise_integer(x, y, z, seed)) / float((1 << 63) - 1)
+
+
 # ------------------------------------------------------------------ scene (plain Python data)
 class PyScene:
     def __init__(self, scene):
@@ -222,8 +255,12 @@ class PyScene:
             uv = (0.5 - math.atan2(n[2], n[0]) / (2.0 * math.pi), math.asin(n[1]) / math.pi + 0.5)
         return best_t, p, n, uv, mat
 
-    def texture(self, tid, h):  # texture.rs:21-49 (kinds used by the configs)
+    def texture(self, tid, h):  # texture.rs:21-118
         t = self.texs[tid]
+        if t.kind == 0:  # Missing
+            return (0.0, 0.0, 0.0)
+        if t.kind == 1:  # DebugUVs
+            return (h[3][0], h[3][1], 0.0)
         if t.kind == 2:
             return t.color
         if t.kind == 3:
@@ -233,6 +270,28 @@ class PyScene:
             y = min(max(h[3][1] * hgt, 0.0), hgt - 1.0)
             px = img[int(y), int(x)]
             return (float(px[0]) / 255.0, float(px[1]) / 255.0, float(px[2]) / 255.0)
+        p = h[1]
+        fp = (_floor(p[0]), _floor(p[1]), _floor(p[2]))
+        if t.kind == 4:  # Checker: (floor x + floor y + floor z) % 2.0 == 0.0 (Rust % on f64 = fmod)
+            return self.texture(t.even if math.fmod((fp[0] + fp[1]) + fp[2], 2.0) == 0.0 else t.odd, h)
+        if t.kind == 5:  # Noise
+            x = noise_real(_as_isize(fp[0]), _as_isize(fp[1]), _as_isize(fp[2]), t.seed)
+            x = 0.5 * x + 0.5
+            return (x, x, x)
+        if t.kind == 6:  # Perlin
+            fl = [_as_isize(c) for c in fp]
+            cl = [_wrap(c + 1) for c in fl]
+            def grad_dot(cx, cy, cz):
+                g = (noise_real(cx, cy, cz, _wrap(t.seed + 1)), noise_real(cx, cy, cz, _wrap(t.seed + 2)),
+                     noise_real(cx, cy, cz, _wrap(t.seed + 3)))
+                return dot(sub(p, (float(cx), float(cy), float(cz))), g)
+            k = [grad_dot(cl[0] if q & 1 else fl[0], cl[1] if q & 2 else fl[1], cl[2] if q & 4 else fl[2])
+                 for q in range(8)]
+            tt = [(c * (c * 6.0 - 15.0) + 10.0) * c * c * c for c in sub(p, fp)]
+            mix = lambda a, b, w: (b - a) * w + a
+            k12, k34, k56, k78 = mix(k[0], k[1], tt[0]), mix(k[2], k[3], tt[0]), mix(k[4], k[5], tt[0]), mix(k[6], k[7], tt[0])
+            x = 0.5 * mix(mix(k12, k34, tt[1]), mix(k56, k78, tt[1]), tt[2]) + 0.5
+            return (x, x, x)
         raise NotImplementedError(t.kind)
 
     def emit(self, e, d, h):  # material.rs:49-60
@@ -368,7 +427,9 @@ def main():
     out["rays"], out["ray_hits"], out["ray_mats"] = rays, hits, mats
 
     # small images under the RNG contract
-    for name, (W, H, spp) in {"bunny": (16, 9, 2), "bunny_lambert": (12, 8, 2), "bunny_full": (12, 8, 2)}.items():
+    images = {"bunny": (16, 9, 2), "bunny_lambert": (12, 8, 2), "bunny_full": (12, 8, 2), "variants": (24, 16, 4),
+              "variants_sky": (24, 16, 4), "two_balls": (16, 12, 2), "three_balls": (16, 12, 2)}
+    for name, (W, H, spp) in images.items():
         sc = scenes.configure(scenes.CATALOGUE[name](), W, H)
         img, rays_n = PyScene(sc).render(W, H, spp, scenes.DEFAULT_SEED)
         out[f"img_{name}"] = img

@@ -41,7 +41,7 @@ def test_librp_host_exports_all_rp_host_h_symbols():
 def test_librp_loads_and_reports_without_gpu():
     from rtpotato import _ffi as F
     L = F.rp()
-    assert L.rp_abi_version() == 3
+    assert L.rp_abi_version() == 4
     n = ctypes.c_int(-1)
     rc = L.rp_device_count(ctypes.byref(n))
     assert rc in (F.RP_OK, F.RP_ENODEV) and n.value >= 0
@@ -56,8 +56,9 @@ def test_struct_layouts_match_c():
 #include <stdio.h>
 #include "rp.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(rp_hittable), sizeof(rp_mesh), sizeof(rp_material),
-         sizeof(rp_texture), sizeof(rp_scene_desc), sizeof(rp_camera), sizeof(rp_render_params), sizeof(rp_stats));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %d %d %d\n", sizeof(rp_hittable), sizeof(rp_mesh), sizeof(rp_material),
+         sizeof(rp_texture), sizeof(rp_scene_desc), sizeof(rp_camera), sizeof(rp_render_params), sizeof(rp_stats),
+         sizeof(rp_scene_options), RP_COUNTERS_LEN, RP_SAMPLES_PER_STREAM, RP_COMM_ID_BYTES);
   return 0;
 }'''
     with tempfile.TemporaryDirectory() as d:
@@ -67,8 +68,8 @@ int main(void) {
         subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), c, "-o", exe], check=True)
         sizes = [int(x) for x in subprocess.run([exe], capture_output=True, text=True).stdout.split()]
     ours = [ctypes.sizeof(t) for t in (F.rp_hittable, F.rp_mesh, F.rp_material, F.rp_texture, F.rp_scene_desc,
-                                        F.rp_camera, F.rp_render_params, F.rp_stats)]
-    assert sizes == ours
+                                        F.rp_camera, F.rp_render_params, F.rp_stats, F.rp_scene_options)]
+    assert sizes == ours + [F.RP_COUNTERS_LEN, F.RP_SAMPLES_PER_STREAM, F.RP_COMM_ID_BYTES]
     assert F.hittable_dtype().itemsize == ctypes.sizeof(F.rp_hittable)
 
 
@@ -82,3 +83,30 @@ def test_no_oracle_in_product():
         for f in files:
             if f.endswith(".py"):
                 assert "oracle" not in open(os.path.join(root, f)).read().replace("no oracle", "")
+
+
+def test_scene_options_defaults_without_gpu():
+    """rp_scene_options_init is host-only: the documented defaults."""
+    from rtpotato.render import scene_options
+    o = scene_options()
+    assert (o.builder, o.max_leaf, o.cost_traverse, o.always_max, o.lds_depth, o.trav_threshold, o.tile_order,
+            o.probe_n) == (0, 4, 0.7, 4, 0, 24, 0, 16)
+    o = scene_options(builder="gpu", lds_depth=17)
+    assert o.builder == 2 and o.lds_depth == 17
+
+
+def test_product_library_reads_no_environment():
+    """Every knob is an argument: librp.so's sources call no getenv (env vars changed results)."""
+    import glob
+    for f in glob.glob(os.path.join(PKG, "csrc", "*")):
+        assert "getenv" not in open(f).read(), f
+
+
+def test_product_kernel_refuses_result_changing_macros():
+    """A build of the product kernel with a timing ablation (wrong streams or colours) is refused."""
+    import subprocess
+    src = os.path.join(PKG, "csrc", "rp_kernel.hip")
+    for macro in ("RPK_ABLATE_RNG", "RPK_ABLATE_TEX", "RPK_BATCH_LEAF"):
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-E", f"-D{macro}", src, "-o", os.devnull],
+                           capture_output=True, text=True)
+        assert r.returncode != 0 and "result-changing" in r.stderr, macro

@@ -1,6 +1,8 @@
-"""Multi-process frame assembly (rtpotato.dist) on CPU with gloo, world size 2 and 3: each rank renders
-its interleaved tile shard (here with the CPU oracle, whose per-pixel seeding the GPU shares), the
-all-gather + de-interleave must rebuild the single-process frame bit for bit."""
+"""Multi-process frames on CPU with gloo, world size 2 and 3: each rank renders its interleaved tile shard
+(here with the CPU oracle, whose per-pixel seeding the GPU shares) into a buffer padded to the gather
+stride, the buffers are all-gathered, and the NumPy restatement of the device frame assembly
+(rtpotato.dist.assemble_frame = rp_frame_assemble's index arithmetic) must rebuild the single-process frame
+bit for bit.  The RCCL bootstrap (rank 0's unique id broadcast over gloo) runs for real."""
 import os
 import socket
 
@@ -23,34 +25,40 @@ def _worker(rank, world, port, result_dir):
     import torch.distributed as dist
     from parity import oracle_render
     from rtpotato import scenes
-    from rtpotato.dist import FrameAssembler, shard_params
+    from rtpotato.dist import assemble_frame, max_slots, shard_params, share_unique_id
     from rtpotato.scene import RenderParams, shard_slot_pixels
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    uid = share_unique_id(rank, world)
+    ids = [None] * world
+    dist.all_gather_object(ids, uid)
     scene = scenes.configure(scenes.bunny_full(), 75, 41)
     params = RenderParams(75, 41, 2, 8, 77, 16, 16)
     sp = shard_params(params, rank, world)
     frame, _, ctr = oracle_render(scene, sp, threads=2)
-    asm = FrameAssembler(params, world, "cpu")
-    buf = asm.new_shard_buffer()
+    stride = max_slots(params, world)
+    buf = torch.zeros(stride, 3, dtype=torch.float64)
     pix = shard_slot_pixels(sp)
     ok = pix >= 0
-    b = buf.view(-1, 3)
-    b[:len(pix)][torch.as_tensor(ok)] = torch.as_tensor(frame.reshape(-1, 3)[pix[ok]])
-    out = asm.gather(buf)
-    # the output-stage bytes (B, G, R, A per slot, as rp_shard_to_bgra8 writes them) gather the same way
+    buf[:len(pix)][torch.as_tensor(ok)] = torch.as_tensor(frame.reshape(-1, 3)[pix[ok]])
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = assemble_frame(torch.cat(parts).numpy(), params, world)
+    # the output-stage bytes (B, G, R, A per slot, as rp_shard_to_bgra8 writes them) assemble the same way
     from rtpotato import _ffi as F
     lin = np.ascontiguousarray(buf.numpy())
-    rgba = np.zeros((lin.size // 3, 4), dtype=np.uint8)
-    F.host().rph_to_srgb_u8(lin.ctypes.data, lin.size // 3, rgba.ctypes.data)
-    bgra = asm.new_bgra_buffer()
-    bgra.copy_(torch.as_tensor(rgba[:, [2, 1, 0, 3]].reshape(-1)))
-    out8 = asm.gather_bgra(bgra)
+    rgba = np.zeros((stride, 4), dtype=np.uint8)
+    F.host().rph_to_srgb_u8(lin.ctypes.data, stride, rgba.ctypes.data)
+    words = torch.as_tensor(np.ascontiguousarray(rgba[:, [2, 1, 0, 3]]).view(np.int32).reshape(-1))
+    wparts = [torch.zeros_like(words) for _ in range(world)]
+    dist.all_gather(wparts, words)
+    out8 = assemble_frame(torch.cat(wparts).numpy()[:, None], params, world).view(np.uint8)
     rays = torch.tensor([ctr["rays"]], dtype=torch.int64)
     dist.all_reduce(rays)
     if rank == 0:
-        np.save(os.path.join(result_dir, "frame.npy"), out.numpy())
-        np.save(os.path.join(result_dir, "frame8.npy"), out8.numpy())
+        np.save(os.path.join(result_dir, "frame.npy"), out)
+        np.save(os.path.join(result_dir, "frame8.npy"), out8)
         np.save(os.path.join(result_dir, "rays.npy"), rays.numpy())
+        np.save(os.path.join(result_dir, "ids.npy"), np.array([np.frombuffer(i, dtype=np.uint8) for i in ids]))
     dist.destroy_process_group()
 
 
@@ -69,6 +77,8 @@ def test_gather_rebuilds_frame(tmp_path, world):
     rgba = np.zeros((41 * 75, 4), dtype=np.uint8)
     F.host().rph_to_srgb_u8(np.ascontiguousarray(ref).ctypes.data, 41 * 75, rgba.ctypes.data)
     assert np.array_equal(np.load(tmp_path / "frame8.npy").reshape(-1, 4), rgba[:, [2, 1, 0, 3]])
+    ids = np.load(tmp_path / "ids.npy")
+    assert ids.shape == (world, F.RP_COMM_ID_BYTES) and (ids == ids[0]).all() and ids[0].any()
 
 
 def test_max_slots_and_shard_partition():

@@ -21,8 +21,8 @@ def _scene(name, w, h, spp, **kw):
     return sc, RenderParams(w, h, spp, 8, scenes.DEFAULT_SEED)
 
 
-def _check(gpu, scene, params, min_exact=0.999, foreground=True):
-    rgb, fg, st = gpu.render(scene, params, foreground=foreground)
+def _check(gpu, scene, params, min_exact=0.999, foreground=True, options=None):
+    rgb, fg, st = gpu.render(scene, params, foreground=foreground, options=options)
     ref, ref_fg, ctr = oracle_render(scene, params, threads=8, foreground=foreground)
     mask = shard_mask(params)
     c = compare(rgb, ref, mask)
@@ -45,10 +45,14 @@ def test_c1_bunny_config(gpu):
 
 
 @pytest.mark.parametrize("name", ["three_balls", "more_balls", "more_balls_optimized", "two_balls", "earth",
-                                  "one_triangle", "glass_bunny", "bunny", "bunny_lambert", "bunny_full"])
+                                  "one_triangle", "glass_bunny", "bunny", "bunny_lambert", "bunny_full", "variants",
+                                  "variants_sky"])
 def test_catalogue_scenes(gpu, name):
-    """Every scene of example_scenes.rs (+ C2/C3 materials): all Scatter/Absorb/Emit/Texture kinds,
-    List and Bvh roots, lens sampling (three_balls, more_balls)."""
+    """Every scene of example_scenes.rs, the C2/C3 material sets, and the two variant scenes: together every
+    Scatter (None/Lambert/Metal/Dielectric), Absorb (Black/White/Albedo/AlbedoMap), Emit (None background in
+    `variants`, DebugNormals, Color in `variants`, SkyGradient, SkySphere over Image / DebugUVs / Perlin) and
+    Texture kind (Missing, DebugUVs, Solid, Image, Checker, Noise, Perlin); List and Bvh roots; lens sampling
+    (three_balls, more_balls)."""
     scene, params = _scene(name, 64, 36, 4)
     _check(gpu, scene, params)
 
@@ -159,7 +163,7 @@ def test_render_device_torch(gpu):
     scene, params = _scene("bunny_full", 64, 40, 4)
     n = shard_slot_count(params)
     out = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
-    ctr = torch.zeros(8, dtype=torch.int64, device="cuda")
+    ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
     with gpu.DeviceScene(scene) as ds:
         ds.render_device(params, out, ctr)
         torch.cuda.synchronize()
@@ -170,11 +174,9 @@ def test_render_device_torch(gpu):
 
 
 @pytest.mark.parametrize("builder", ["host", "gpu"])
-def test_intersect_rays(gpu, monkeypatch, builder):
+def test_intersect_rays(gpu, builder):
     """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle --
-    over the host SAH tree and the device-built LBVH (RP_BVH_BUILDER)."""
-    monkeypatch.setenv("RP_BVH_BUILDER", builder)
-    monkeypatch.setenv("RP_BVH_CHECK", "1")
+    over the host SAH tree and the device-built LBVH (rp_scene_options.builder)."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     rng = np.random.default_rng(5)
@@ -191,7 +193,7 @@ def test_intersect_rays(gpu, monkeypatch, builder):
     rays[400:600, 7] = rng.uniform(0.1, 3.0, size=200)
     rays[600:700, 0] = 0.0
     rays[600:700, 3] = 0.0
-    with gpu.DeviceScene(scene) as ds:
+    with gpu.DeviceScene(scene, options={"builder": builder, "self_check": 1}) as ds:
         hits, mats = ds.intersect(rays)
     d_ = scene.desc()
     os_ = O.OracleScene(d_.addr(), d_)
@@ -261,10 +263,13 @@ def test_workspaces_frames_in_flight(gpu):
     n = shard_slot_count(params)
     with gpu.DeviceScene(scene) as ds:
         ref = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
-        c0 = torch.zeros(8, dtype=torch.int64, device="cuda")
+        c0 = torch.zeros(4, dtype=torch.int64, device="cuda")
+        ds.reserve(params)
         ds.render_device(params, ref, c0)
         torch.cuda.synchronize()
         wss = [ds.workspace(), ds.workspace()]
+        for w in wss:
+            ds.reserve(params, w)
         streams = [torch.cuda.Stream(), torch.cuda.Stream()]
         outs = [torch.zeros_like(ref) for _ in range(4)]
         ctrs = [torch.zeros_like(c0) for _ in range(4)]
@@ -278,41 +283,39 @@ def test_workspaces_frames_in_flight(gpu):
 
 
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000), ("three_balls", None)])
-def test_device_bvh_builder(gpu, monkeypatch, name, arg):
+def test_device_bvh_builder(gpu, name, arg):
     """Scenes over the device-built tree (rp_bvh_gpu.hip: LBVH + wide collapse), with the host builder's
-    structural self-check on the downloaded tree (RP_BVH_CHECK): same image and ray counts as the oracle."""
+    structural self-check on the downloaded tree (options.self_check): same image and ray counts as the
+    oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
-    monkeypatch.setenv("RP_BVH_BUILDER", "gpu")
-    monkeypatch.setenv("RP_BVH_CHECK", "1")
+    opt = {"builder": "gpu", "self_check": 1}
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
-    with gpu.DeviceScene(sc) as ds:
+    with gpu.DeviceScene(sc, options=opt) as ds:
         info = ds.info()
         assert info["nodes"] >= 1 and (info["max_depth"] >= 4 or name == "three_balls")
-    _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED))
+    _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
-def test_spilled_traversal_stack(gpu, monkeypatch, name, arg):
+def test_spilled_traversal_stack(gpu, name, arg):
     """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
-    deep trees such as C5's use): forced here with RP_LDS_DEPTH=17, so nearly every traversal spills --
-    same image as the oracle."""
+    deep trees such as C5's use): forced here with options.lds_depth = 17, so nearly every traversal spills
+    -- same image as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
-    monkeypatch.setenv("RP_LDS_DEPTH", "17")
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
-    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED))
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 17})
 
 
-@pytest.mark.parametrize("always_max", ["0", "4"])
-def test_always_tested_primitives(gpu, monkeypatch, always_max):
+@pytest.mark.parametrize("always_max", [0, 4])
+def test_always_tested_primitives(gpu, always_max):
     """Primitives whose box dwarfs the rest of the scene (the C3 ground sphere) are kept out of the tree and
-    tested first for every ray (rp_bvh.h BuildOptions::always_max, the default 4); RP_ALWAYS_MAX=0 puts
-    them back in the tree.  Same image as the oracle either way, on the full-materials bunny scene (ground,
-    two balls, bunny) and on two_balls (a scene of two spheres only)."""
+    tested first for every ray (options.always_max, the default 4); 0 puts them back in the tree.  Same
+    image as the oracle either way, on the full-materials bunny scene (ground, two balls, bunny) and on
+    two_balls (a scene of two spheres only)."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
-    monkeypatch.setenv("RP_ALWAYS_MAX", always_max)
     for name in ("bunny_full", "two_balls"):
         sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
-        _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED))
+        _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"always_max": int(always_max)})

@@ -133,3 +133,17 @@ def test_u8_unit_division_free_is_exact():
         q0 = float(x) * R
         q = libm.fma(libm.fma(-q0, 255.0, float(x)), R, q0)
         assert struct.pack("<d", q) == struct.pack("<d", float(x) / 255.0), x
+
+
+def test_bulk_stdrng_matches_oracle_stream(oracle):
+    """rph_stdrng_u64 (the threaded host generator behind rtpotato.rng bulk draws, used to build the C5
+    mesh) is rand 0.8 StdRng's stream: equal to the oracle's next_u64 sequence, from any start draw."""
+    import numpy as np
+    from rtpotato.rng import BULK_DRAWS, StdRng
+    for seed in (0xC5, 0, 2**64 - 1):
+        ref = oracle.stream_u64(seed, 3000)
+        r = StdRng.seed_from_u64(seed)
+        assert np.array_equal(r.next_u64_array(BULK_DRAWS)[:3000], ref)
+        r = StdRng.seed_from_u64(seed)
+        r.next_u64_array(777)
+        assert np.array_equal(r.next_u64_array(BULK_DRAWS)[:3000 - 777], ref[777:])

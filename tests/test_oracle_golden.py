@@ -43,7 +43,8 @@ def test_ray_hits(oracle, golden):
     assert np.array_equal(hits[hit], ref[hit])
 
 
-@pytest.mark.parametrize("name", ["bunny", "bunny_lambert", "bunny_full"])
+@pytest.mark.parametrize("name", ["bunny", "bunny_lambert", "bunny_full", "variants", "variants_sky", "two_balls",
+                                  "three_balls"])
 def test_images(oracle, golden, name):
     from rtpotato import scenes
     from rtpotato.scene import RenderParams

@@ -74,14 +74,13 @@ def test_shard_to_bgra8_matches_host(gpu):
     import torch
     from rtpotato import _ffi as F
     from rtpotato import scenes
-    from rtpotato.dist import FrameAssembler
     from rtpotato.render import tga_bytes, unpack_shard
     from rtpotato.scene import RenderParams, shard_slot_count
     sc = scenes.configure(scenes.bunny_full(), 70, 45)
     for params in (RenderParams(70, 45, 8, 8, 11, 16, 16), RenderParams(70, 45, 8, 8, 11, 16, 16, 1, 3)):
         n = shard_slot_count(params)
         rgb = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
-        ctr = torch.zeros(8, dtype=torch.int64, device="cuda")
+        ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
         out = torch.zeros(4 * n, dtype=torch.uint8, device="cuda")
         with gpu.DeviceScene(sc) as ds:
             ds.render_device(params, rgb, ctr)
@@ -93,8 +92,12 @@ def test_shard_to_bgra8_matches_host(gpu):
         got = out.cpu().numpy().reshape(n, 4)
         assert np.array_equal(got, ref[:, [2, 1, 0, 3]])
         if params.num_shards == 1:
-            asm = FrameAssembler(params, 1, torch.device("cuda"))
-            frame = asm.gather_bgra(out).cpu().numpy()
+            import ctypes
+            fr = torch.zeros(params.width * params.height * 4, dtype=torch.uint8, device="cuda")
+            F.check(F.rp().rp_frame_assemble(ctypes.byref(params.to_c()), out.data_ptr(), 1, fr.data_ptr(),
+                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+            torch.cuda.synchronize()
+            frame = fr.cpu().numpy().reshape(params.height, params.width, 4)
             full = unpack_shard(params, lin)
             rgba = np.zeros((params.height, params.width, 4), dtype=np.uint8)
             F.host().rph_to_srgb_u8(np.ascontiguousarray(full).ctypes.data, params.width * params.height,

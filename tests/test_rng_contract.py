@@ -43,3 +43,21 @@ def test_single_batch_frames_are_the_per_pixel_stream():
     m = np.any(shard != 0, axis=2)
     assert m.sum() > 0
     assert np.array_equal(full[m], shard[m])
+
+
+def test_samples_per_stream_parameter():
+    """rp_render_params.samples_per_stream N: N >= spp is SURVEY.md 8c's one stream per pixel whatever N is;
+    N = 1 makes sample s its own stream seed + s*W*H (the mean of spp one-sample frames)."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    w, h, spp, seed = 12, 8, 40, 31
+    scene = scenes.configure(scenes.bunny_full(), w, h)
+    one, _, c1 = oracle_render(scene, RenderParams(w, h, spp, 8, seed, samples_per_stream=spp), threads=8)
+    big, _, c2 = oracle_render(scene, RenderParams(w, h, spp, 8, seed, samples_per_stream=1000), threads=8)
+    assert np.array_equal(one, big) and c1["rays"] == c2["rays"]
+    default, _, _ = oracle_render(scene, RenderParams(w, h, spp, 8, seed), threads=8)
+    assert not np.array_equal(one, default)  # 40 > 32: the default splits the pixel into two streams
+    single, _, c3 = oracle_render(scene, RenderParams(w, h, 3, 8, seed, samples_per_stream=1), threads=8)
+    parts = [oracle_render(scene, RenderParams(w, h, 1, 8, seed + b * w * h), threads=8) for b in range(3)]
+    np.testing.assert_allclose(single, sum(p[0] for p in parts) / 3, rtol=1e-12, atol=1e-14)
+    assert c3["rays"] == sum(p[2]["rays"] for p in parts)

@@ -1,6 +1,6 @@
 """Timing-only A/B: C3 64-spp frame time per variant, interleaved rounds.  A variant is a library file
-under raytracing-potato_amd/lib, optionally with a traversal threshold and env knobs:
-`librp.so@16` (RP_TRAV_THRESHOLD), `librp.so@40:RP_BVH_MAX_LEAF=2,RP_BVH_COST_TRAVERSE=1.5`."""
+under raytracing-potato_amd/lib, optionally with a traversal threshold and rp_scene_options fields:
+`librp.so@16` (trav_threshold), `librp.so@40:max_leaf=2,cost_traverse=1.5`."""
 import os, sys, json, subprocess
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 libs = sys.argv[1:]
@@ -11,11 +11,12 @@ for rnd in range(2):
         head, _, extra = spec.partition(":")
         lib, _, thr = head.partition("@")
         env = dict(os.environ)
+        opts = {}
         if thr:
-            env["RP_TRAV_THRESHOLD"] = thr
+            opts["trav_threshold"] = int(thr)
         for kv in filter(None, extra.split(",")):
             k, _, v = kv.partition("=")
-            env[k] = v
+            opts[k] = float(v) if "." in v else (v if k == "builder" else int(v))
         code = f"""
 import os,sys
 sys.path[:0]=['{REPO}','{REPO}/raytracing-potato_amd']
@@ -24,7 +25,7 @@ from dataclasses import replace
 from rtpotato import scenes
 from rtpotato.render import DeviceScene
 sc,p=scenes.config_scene("C3"); p=replace(p, spp=int(os.environ.get("ABLATE_SPP","64")))
-ds=DeviceScene(sc); ds.render(replace(p,spp=4))
+ds=DeviceScene(sc, options={opts!r}); ds.render(replace(p,spp=4))
 ts=[ds.render(p)[2]['seconds'] for _ in range(2)]
 print(min(ts))
 """

@@ -33,13 +33,11 @@ def main():
     print(f"[bvh] mesh ready {out['mesh_seconds']}s", file=sys.stderr, flush=True)
     for spec in a.builders.split(","):
         b, _, leaf = spec.partition("@")  # builder[@max_leaf]
-        os.environ["RP_BVH_BUILDER"] = b
+        opt = {"builder": b}
         if leaf:
-            os.environ["RP_BVH_MAX_LEAF"] = leaf
-        else:
-            os.environ.pop("RP_BVH_MAX_LEAF", None)
+            opt["max_leaf"] = int(leaf)
         t = time.time()
-        ds = DeviceScene(sc)
+        ds = DeviceScene(sc, options=opt)
         setup = time.time() - t
         info = ds.info()
         ds.render(replace(params, spp=1, width=256, height=256))

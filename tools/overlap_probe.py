@@ -33,7 +33,9 @@ def main():
         p = replace(params, shard=0, num_shards=n)
         m = shard_slot_count(p)
         bufs = [torch.zeros(3 * m, dtype=torch.float64, device="cuda") for _ in range(2)]
-        ctrs = [torch.zeros(8, dtype=torch.int64, device="cuda") for _ in range(2)]
+        ctrs = [torch.zeros(4, dtype=torch.int64, device="cuda") for _ in range(2)]
+        for ds in dss:
+            ds.reserve(p)
         res = {}
         for mode in ("serial", "two_streams", "serial", "two_streams"):
             k2 = 2 if mode == "two_streams" else 1

@@ -1,0 +1,104 @@
+"""Per-ray roofline record of the frame kernel from rocprofv3 --pmc passes over one bench frame.
+
+    python tools/roofline.py --config C3 --bench BENCH.json --out OUT.json PASS_DIR [PASS_DIR ...]
+
+Each PASS_DIR is the -d directory of one `rocprofv3 --pmc ... -- python3 bench.py --steps 1 --warmup 0`
+run (one dispatch of the frame kernel per run); BENCH.json is that bench's stdout line (its rays per frame).
+The record bench.py prices its `roofline` with (kernel_record()): per ray of the frame kernel
+  - traffic_bytes_per_ray: memory-side bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE doubled,
+    the gfx950 correction of MI355X_MICROARCH.md "HBM"; Infinity-Cache hits are counted, so this is an upper
+    bound of HBM traffic),
+  - valu_per_ray / salu_per_ray / vmem_per_ray / lds_per_ray: wave-instructions,
+and for the frame: the SQ cycle budget (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES, all in
+quad-cycles), the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel duration), the VALU-issue fraction at
+that clock and at 2.4 GHz (a wave64 VALU instruction holds a SIMD-32 for 2 cycles), and the instruction mix.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import subprocess
+
+KERNEL = "render_kernel<false, "  # the frame kernel (either stack variant), not the probe
+SIMDS = 1024
+PEAK_CLOCK = 2.4e9
+
+
+def read_pass(d):
+    """{counter: value} of the frame kernel's dispatch in one pass (rows of a dispatch summed), and its
+    duration in ns."""
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    dur = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if KERNEL not in row["Kernel_Name"]:
+                continue
+            did = row["Dispatch_Id"]
+            per[did][row["Counter_Name"]] += float(row["Counter_Value"])
+            dur[did] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+    if not per:
+        raise SystemExit(f"no {KERNEL} rows under {d}")
+    if len(per) != 1:
+        raise SystemExit(f"{d}: {len(per)} frame-kernel dispatches (expected one: --steps 1 --warmup 0)")
+    did = next(iter(per))
+    return dict(per[did]), dur[did]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--bench", required=True)
+    ap.add_argument("--out", required=True)
+    ap.add_argument("passes", nargs="+")
+    a = ap.parse_args()
+    bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
+    rays = float(bench["config"]["rays_per_frame"])
+    c, durs = {}, {}
+    for d in a.passes:
+        vals, ns = read_pass(d)
+        c.update(vals)
+        durs[os.path.basename(d.rstrip("/"))] = ns
+    rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    rec = {"kernel": KERNEL, "config": a.config, "git": rev, "rays": rays, "counters": c,
+           "kernel_ns_per_pass": durs, "bench_ms_per_step": bench.get("ms_per_step")}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        fetch, write = 2.0 * c["FETCH_SIZE"] * 1024.0, c["WRITE_SIZE"] * 1024.0
+        rec.update({"fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
+                    "traffic_bytes_per_ray": (fetch + write) / rays,
+                    "fetch_bytes_per_ray": fetch / rays, "write_bytes_per_ray": write / rays})
+    for k, name in (("SQ_INSTS_VALU", "valu_per_ray"), ("SQ_INSTS_SALU", "salu_per_ray"),
+                    ("SQ_INSTS_VMEM_RD", "vmem_rd_per_ray"), ("SQ_INSTS_VMEM_WR", "vmem_wr_per_ray"),
+                    ("SQ_INSTS_LDS", "lds_per_ray"), ("SQ_INSTS_SMEM", "smem_per_ray"),
+                    ("SQ_INSTS_BRANCH", "branch_per_ray")):
+        if k in c:
+            rec[name] = c[k] / rays
+    if all(k in c for k in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")):
+        w = c["SQ_WAVE_CYCLES"]
+        rec["cycle_budget"] = {
+            "wait_any": round(c["SQ_WAIT_ANY"] / w, 4), "wait_inst_any": round(c["SQ_WAIT_INST_ANY"] / w, 4),
+            "active_inst_any": round(c["SQ_ACTIVE_INST_ANY"] / w, 4),
+            "closure": round((c["SQ_WAIT_ANY"] + c["SQ_WAIT_INST_ANY"] + c["SQ_ACTIVE_INST_ANY"]) / w, 4),
+            "waves": c.get("SQ_WAVES")}
+    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c:
+        ns = next((v for k, v in durs.items() if v > 0), None)
+        if ns:
+            clk = c["GRBM_GUI_ACTIVE"] / 8.0 / (ns * 1e-9)
+            rec["clock_ghz"] = round(clk / 1e9, 3)
+            rec["valu_issue_frac_at_clock"] = round(c["SQ_INSTS_VALU"] / (SIMDS * clk * ns * 1e-9 / 2.0), 4)
+            rec["valu_issue_frac_at_2p4ghz"] = round(c["SQ_INSTS_VALU"] / (SIMDS * PEAK_CLOCK * ns * 1e-9 / 2.0), 4)
+    mix = {k[len("SQ_INSTS_VALU_"):].lower(): c[k] / c["SQ_INSTS_VALU"] for k in c
+           if k.startswith("SQ_INSTS_VALU_") and "SQ_INSTS_VALU" in c}
+    if mix:
+        rec["valu_mix"] = {k: round(v, 4) for k, v in sorted(mix.items())}
+    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+        rec["valu_thread_cycles_per_active_quad"] = round(c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"], 3)
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        rec["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
+    json.dump(rec, open(a.out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in rec.items() if k != "counters"}))
+
+
+if __name__ == "__main__":
+    main()
