@@ -29,7 +29,6 @@ from __future__ import annotations
 
 import argparse
 import ctypes
-import glob
 import json
 import os
 import sys
@@ -61,13 +60,31 @@ def reference_equivalent(config: str):
 
 
 def kernel_record(config: str):
-    """The newest committed per-ray record of the frame kernel for this config (tools/roofline.py over
-    rocprofv3 --pmc passes): memory-side bytes per ray, VALU / SALU instructions per ray, cycle budget."""
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*", f"{config.lower()}_roofline.json")), reverse=True):
-        rec = json.load(open(f))
-        rec["source"] = os.path.relpath(f, REPO)
-        return rec
-    return None
+    """The committed per-ray record of the current frame kernel for this config (profiles/current.json ->
+    a tools/roofline.py record over rocprofv3 --pmc passes): memory-side bytes per ray, VALU / SALU
+    instructions per ray, cycle budget."""
+    try:
+        rel = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"][config]
+    except (OSError, KeyError):
+        return None
+    rec = json.load(open(os.path.join(REPO, rel)))
+    rec["source"] = rel
+    return rec
+
+
+class stdout_to_stderr:
+    """Route fd 1 to stderr while RCCL initialises: it prints a version banner on stdout, and rank 0's stdout
+    must be exactly the one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
 
 
 def host_cpu():
@@ -158,7 +175,8 @@ def main():
     info = ds.info()
     log(f"[rank {rank}] scene ready in {time.time() - t:.2f}s: {info}")
     sp = shard_params(params, rank, world)
-    comm = bootstrap_comm(rank, world, local)
+    with stdout_to_stderr():
+        comm = bootstrap_comm(rank, world, local)
     # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
     # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.

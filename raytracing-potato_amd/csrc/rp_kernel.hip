@@ -522,21 +522,28 @@ RPK_INLINE void trav_begin(const KScene& S, V3 o, V3 d, double tmin, double tmax
 
 // Stack entry i of a lane: in its LDS column (entry i at stk[i * stride]) or, for SPILL kernels, entries
 // >= S.lds_depth in the lane's global overflow run (S.spill[spl + i - lds_depth], L2-resident) -- a deep
-// tree (config C5: 43 entries) then keeps the LDS of four blocks per CU.
+// tree (config C5: 43 entries) then keeps the LDS of four blocks per CU.  The two parts are typed with
+// their address spaces (LDS = 3, global = 1): with generic pointers the compiler merged the LDS and the
+// spill store of a push into one FLAT store through a selected pointer (and the pops into FLAT loads),
+// which waits on both memory counters at every node visit.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint32_t glb_u32;
+RPK_INLINE glb_u32* spill_ptr(const KScene& S) { return (glb_u32*)S.spill; }
 template <bool SPILL>
-RPK_INLINE void stk_put(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, uint32_t i, uint32_t v) {
+RPK_INLINE void stk_put(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t i, uint32_t v) {
   if (!SPILL || i < S.lds_depth) stk[i * stride] = v;
-  else S.spill[spl + i - S.lds_depth] = v;
+  else spill_ptr(S)[spl + i - S.lds_depth] = v;
 }
 template <bool SPILL>
-RPK_INLINE uint32_t stk_get(const KScene& S, const uint32_t* stk, uint32_t stride, uint32_t spl, uint32_t i) {
-  return (!SPILL || i < S.lds_depth) ? stk[i * stride] : S.spill[spl + i - S.lds_depth];
+RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t i) {
+  if (!SPILL || i < S.lds_depth) return stk[i * stride];
+  return spill_ptr(S)[spl + i - S.lds_depth];
 }
 
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
 template <bool SPILL>
-RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
+RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
   double best = ts.best;
@@ -675,7 +682,7 @@ RPK_INLINE void trav_step(const KScene& S, uint32_t* stk, uint32_t stride, uint3
   ts.leaf = leaf;
 }
 
-RPK_INLINE void traverse(const KScene& S, uint32_t* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
+RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
                          HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
   Ray32 r;
   setup_ray32(o, d, tmin, r);
@@ -1083,7 +1090,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   // pixel fetch (queue drained), last wave exit -- minima stored bit-inverted so atomicMax serves both
   DIAG(if (!PROBE && threadIdx.x == 0) atomicMax(&kargs()->diag[10], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
   __syncthreads();
-  uint32_t* stk = lds_stack + threadIdx.x;
+  lds_u32* stk = (lds_u32*)(lds_stack + threadIdx.x);
 
   // per-WAVE totals (ballot popcounts: scalar registers, not three VGPRs through the shading code)
   uint64_t n_rays = 0, n_samples = 0, n_pixels = 0;
@@ -1423,7 +1430,7 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
   const double tmin = q[6], tmax = q[7];
   HitRec hr;
   bool overflow = false;
-  traverse(S, lds_stack + threadIdx.x, BLOCK, o, d, tmin, tmax, hr, overflow);
+  traverse(S, (lds_u32*)(lds_stack + threadIdx.x), BLOCK, o, d, tmin, tmax, hr, overflow);
   double* oh = out_hit + 9 * i;
   if (hr.prim >= 0) {
     Surf h;
