@@ -188,6 +188,10 @@ typedef struct rp_render_params {
  * exact-t ties between primitives (the closest hit does not depend on the tree).
  * Zero-initialised fields take the defaults; rp_scene_options_init fills them in explicitly. */
 enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2 };
+/* Render engines (same images bit for bit): the persistent megakernel (traversal and shading on the same
+ * lanes) and the stage-split engine (trace and shade passes over a pool of path slots; its renders
+ * synchronise the host: the pass loop polls the ray queue). */
+enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = host binned SAH below 2^20 hittables, device LBVH above */
   uint32_t max_leaf;        /* primitives per leaf, 1..8 (0 -> 4) */
@@ -198,7 +202,9 @@ typedef struct rp_scene_options {
   uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24) */
   uint32_t tile_order;      /* 0 = cost-ordered tiles (probe launch + sort), 1 = plain shard order */
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
-  uint32_t reserved[4];
+  uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
+  uint32_t wf_slots;        /* wavefront engine: path slots per resident lane (0 -> 4) */
+  uint32_t reserved[2];
 } rp_scene_options;
 
 typedef struct rp_stats {

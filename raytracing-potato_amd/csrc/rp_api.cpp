@@ -109,6 +109,7 @@ struct rp_workspace {
   uint32_t* d_gather_bgra = nullptr; //   all ranks' bytes (nranks x stride words)
   uint64_t gs_slots = 0;             // capacity of d_gs_* in slots
   uint64_t gather_slots = 0;         // capacity of d_gather_* in slots (over all ranks)
+  rpk::WfBuffers wf{};               // the stage-split engine's path-slot pool (engine = wavefront only)
 };
 
 struct rp_scene {
@@ -152,6 +153,10 @@ struct rp_multi {
 namespace {
 
 void ws_release(rp_workspace* w) {
+  for (void* p : {(void*)w->wf.ray, (void*)w->wf.tp, (void*)w->wf.sum, (void*)w->wf.hit, (void*)w->wf.prim,
+                  (void*)w->wf.st, (void*)w->wf.queue, (void*)w->wf.wc})
+    dfree(p);
+  if (w->wf.host_count) (void)hipHostFree(w->wf.host_count);
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
@@ -172,6 +177,22 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
+  }
+  if (s->opt.engine == RP_ENGINE_WAVEFRONT) {
+    rpk::WfBuffers& b = w->wf;
+    const uint64_t P = lanes * s->opt.wf_slots;
+    if (P >= 0x7fffffffull) {
+      ws_release(w);
+      return fail(RP_EINVAL, "too many wavefront path slots");
+    }
+    b.P = (uint32_t)P;
+    b.poll = 8;
+    if (!dalloc(&b.ray, 6 * P) || !dalloc(&b.tp, 3 * P) || !dalloc(&b.sum, 3 * P) || !dalloc(&b.hit, 3 * P) ||
+        !dalloc(&b.prim, P) || !dalloc(&b.st, 7 * P) || !dalloc(&b.queue, 2 * P) || !dalloc(&b.wc, 4) ||
+        hipHostMalloc(reinterpret_cast<void**>(&b.host_count), sizeof(uint32_t)) != hipSuccess) {
+      ws_release(w);
+      return fail(RP_ENOMEM, "hipMalloc wavefront path slots");
+    }
   }
   return RP_OK;
 }
@@ -245,6 +266,8 @@ rp_scene_options default_options() {
   o.trav_threshold = DEF_TRAV_THRESHOLD;
   o.tile_order = 0;
   o.probe_n = rpk::PROBE_LATTICE_N;
+  o.engine = RP_ENGINE_MEGAKERNEL;
+  o.wf_slots = 4;
   return o;
 }
 
@@ -263,6 +286,9 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
   if (o.tile_order > 1) return fail(RP_EINVAL, "options.tile_order must be 0 or 1");
   if (o.probe_n == 0) o.probe_n = d.probe_n;
+  if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
+  if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
+  if (o.wf_slots > 64) return fail(RP_EINVAL, "options.wf_slots must be 1..64");
   return RP_OK;
 }
 
@@ -509,7 +535,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
-  int e = rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
+  int e = s->opt.engine == RP_ENGINE_WAVEFRONT
+              ? rpk::launch_wavefront(ks, kp, d_rgb, d_fg, ctr, w->d_queue, w->wf, (int)resident, stream)
+              : rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
   if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
   if (kp.nbatch > 1) {
     e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);

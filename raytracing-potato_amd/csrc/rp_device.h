@@ -1,0 +1,1161 @@
+// rp_device.h -- device code shared by the gfx950 kernels (rp_kernel.hip: the persistent megakernel;
+// rp_wavefront.hip: the stage-split engine): the rand 0.8 StdRng keystream, f64 vector math, the
+// conservative-f32 wide-BVH traversal with exact f64 primitive tests, and the materials/textures.
+//
+// Arithmetic is IEEE binary64 in the reference's exact operation order (no contraction: the kernels are
+// compiled with -ffp-contract=off and the pragma below), so paths -- and the RNG draws they consume --
+// are the reference's.  References: render.rs:32-146, bvh.rs:93-124, hittable.rs:39-108,
+// material.rs:27-179, texture.rs:21-118, randomness.rs:9-110, utility.rs:67-154.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "rp_kernel.h"
+
+#pragma clang fp contract(off)
+
+// Every compile-time knob below changes timing only.  Experiments that change results (timing ablations
+// with wrong streams or colours) are not kept in this file, and a build asking for one is refused so a
+// library that writes wrong frames can never be produced from it.
+#if defined(RPK_ABLATE_RNG) || defined(RPK_ABLATE_UV) || defined(RPK_ABLATE_TEX) || defined(RPK_ABLATE_METAL) || \
+    defined(RPK_BATCH_LEAF)
+#error "result-changing experiment macros are not part of the product kernel"
+#endif
+
+namespace rpk {
+
+#define RPK_INLINE __device__ __forceinline__
+
+// Diagnostic build (-DRPK_DIAG, lib/librp_diag.so only): per-wave s_memtime phase stamps and lane
+// utilisation counters into KArgs::diag.  The product build compiles none of it.
+#ifdef RPK_DIAG
+#define DIAG(...) __VA_ARGS__
+RPK_INLINE uint64_t stamp() {
+#ifdef RPK_DIAG_NOSTAMP
+  return 0;
+#endif
+  const uint64_t t = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): s_memtime returns through the LGKM counter
+  return t;
+}
+__shared__ unsigned long long g_dreg[2 * DREG_N];
+// count one execution of region r by this wave and its active lanes (leader lane only; EXEC is read
+// directly, no ballot)
+#define DREG(r)                                                                        \
+  {                                                                                    \
+    const uint64_t ex_ = __builtin_amdgcn_read_exec();                                 \
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex_)) {                       \
+      atomicAdd(&g_dreg[2 * (r)], 1ull);                                               \
+      atomicAdd(&g_dreg[2 * (r) + 1], (unsigned long long)__popcll(ex_));             \
+    }                                                                                  \
+  }
+#else
+#define DIAG(...)
+#define DREG(r)
+#endif
+
+static constexpr int BLOCK = RENDER_BLOCK;
+typedef float f2 __attribute__((ext_vector_type(2)));
+RPK_INLINE f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+static constexpr uint32_t STACK_SLACK = 3;  // spare LDS stack entries for the branchless push (writes reach sp+2 <= cap+2)
+static constexpr double RAY_EPSILON = 1e-3;  // utility.rs:30
+static constexpr double SMOL = 1e-7;         // utility.rs:31
+static constexpr double PI_ = 3.14159265358979323846;
+static constexpr double TAU_ = 6.28318530717958647692;
+static constexpr double INF = __builtin_huge_val();
+
+// ------------------------------------------------------------------ RNG (rand 0.8 StdRng) -------
+
+RPK_INLINE uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+#define RPK_QR(a, b, c, d)              \
+  a += b; d ^= a; d = rotl(d, 16);      \
+  c += d; b ^= c; b = rotl(b, 12);      \
+  a += b; d ^= a; d = rotl(d, 8);       \
+  c += d; b ^= c; b = rotl(b, 7);
+
+// ChaCha12 block (rand_chacha 0.3: 64-bit block counter in words 12-13, zero nonce).
+RPK_INLINE void chacha12(const uint32_t k[8], uint32_t ctr, uint32_t o[16]) {
+  uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+  uint32_t x4 = k[0], x5 = k[1], x6 = k[2], x7 = k[3], x8 = k[4], x9 = k[5], x10 = k[6], x11 = k[7];
+  uint32_t x12 = ctr, x13 = 0, x14 = 0, x15 = 0;
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    RPK_QR(x0, x4, x8, x12);
+    RPK_QR(x1, x5, x9, x13);
+    RPK_QR(x2, x6, x10, x14);
+    RPK_QR(x3, x7, x11, x15);
+    RPK_QR(x0, x5, x10, x15);
+    RPK_QR(x1, x6, x11, x12);
+    RPK_QR(x2, x7, x8, x13);
+    RPK_QR(x3, x4, x9, x14);
+  }
+  o[0] = x0 + 0x61707865u; o[1] = x1 + 0x3320646eu; o[2] = x2 + 0x79622d32u; o[3] = x3 + 0x6b206574u;
+  o[4] = x4 + k[0]; o[5] = x5 + k[1]; o[6] = x6 + k[2]; o[7] = x7 + k[3];
+  o[8] = x8 + k[4]; o[9] = x9 + k[5]; o[10] = x10 + k[6]; o[11] = x11 + k[7];
+  o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
+}
+
+// rand_core 0.6 seed_from_u64: PCG32 expansion of the u64 into the 8 key words.
+RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    state = state * 6364136223846793005ull + 11634580027462260723ull;
+    uint32_t xs = (uint32_t)(((state >> 18) ^ state) >> 27);
+    uint32_t rot = (uint32_t)(state >> 59);
+    key[c] = (xs >> rot) | (xs << ((32 - rot) & 31));
+  }
+}
+
+// Main stream of one pixel.  Every draw on the path is a u64 (Standard f64), so the stream is the
+// keystream read two words at a time from word `pos`: exactly rand_chacha's 4-block-buffered stream.
+//
+// Keystream blocks are produced ahead of use into a per-lane slab in global memory (L2/MALL resident,
+// ~0.7 KB per lane): a ring of RING main-stream blocks and the two camera-jitter blocks the next
+// samples need.  Production happens in ONE place per round of the render loop (rng_refill), for every
+// lane that has room, so a ChaCha12 block (~600 VALU) runs with nearly all 64 lanes doing useful work;
+// the draw sites only load 16-word blocks from the ring.  Generating at the draw sites instead made the
+// wave pay a whole block whenever ANY lane crossed a block boundary (several per round at C3).  A draw
+// that finds the ring empty still generates its block in place (rare: the refill pass keeps > RNG_CRIT
+// blocks ahead of every lane).
+//
+// Slab layout per lane (uint4 units): [0,2) key words, [2, 2+4*RING) ring (block b in slot b % RING),
+// [2+4*RING, +8) jitter blocks (block b in slot b & 1).  Per-lane cursors (LDS): end = one past the
+// newest ring block; jtag[2] = block held by each jitter slot.
+#ifndef RPK_RING
+#define RPK_RING 8
+#endif
+#ifndef RPK_RNG_BATCH
+#define RPK_RNG_BATCH 48
+#endif
+static constexpr uint32_t RING = RPK_RING;
+// Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs) -- measured 3.7% faster on C3 than
+// 3 waves/SIMD with the whole traversal stack in LDS (-DRPK_W3).
+#ifndef RPK_W3
+#define RPK_W4
+#endif
+static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
+// The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS; the
+// host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to the lane's global run
+// (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).  -DRPK_COLD_IN_SLAB keeps them
+// in the keystream slab instead (v31 and before): C3 +2.6 %, C5 +4.6 % frame time -- the slab shrinks
+// from 720 to 672 B per lane and the shading site loses 6 global loads and 6 stores.
+#if defined(RPK_W4) && defined(RPK_COLD_IN_SLAB)
+#define RPK_COLD_SLAB
+#endif
+#ifdef RPK_COLD_SLAB
+static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
+#else
+static constexpr uint32_t SLAB_N = SLAB_COLD;
+#endif
+#ifndef RPK_RNG_CRIT
+#define RPK_RNG_CRIT 2
+#endif
+static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
+// Traversal wave-level exits (trav_step): leave the inner-node loop once at most RPK_LEAF_BREAK lanes of the
+// wave still look for a leaf (C3: 0 -> 3 is -2.7 % frame time), and the leaf loop once at most
+// RPK_PRIM_BREAK lanes still test primitives (their remaining run is parked as a leaf entry).
+#ifndef RPK_LEAF_BREAK
+#define RPK_LEAF_BREAK 3
+#endif
+#ifndef RPK_PRIM_BREAK
+#define RPK_PRIM_BREAK 0
+#endif
+static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // this many lanes with room force a refill pass
+
+struct Rng {
+  uint4* slab;     // global: this lane's slab
+  uint32_t pos;    // next keystream word (even)
+  uint32_t* end;   // LDS cursor: one past the newest ring block
+  uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
+};
+RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
+  const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
+  k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
+  k[4] = c.x; k[5] = c.y; k[6] = c.z; k[7] = c.w;
+}
+RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
+  r.slab[SLAB_KEY] = make_uint4(k[0], k[1], k[2], k[3]);
+  r.slab[SLAB_KEY + 1] = make_uint4(k[4], k[5], k[6], k[7]);
+}
+RPK_INLINE void store_block(uint4* dst, const uint32_t w[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint4 v = src[q];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+}
+RPK_INLINE uint4* ring_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_RING + 4 * (b % RING); }
+RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT + 4 * (b & 1u); }
+
+// The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
+// samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
+// round, not started) gets its key from the unit's seed and keystream block 0 here, batched with the other
+// lanes' ChaCha work -- at the fetch site the whole wave paid a ChaCha block for each fetching lane.
+RPK_INLINE void rng_refill(Rng& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
+  const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
+  const uint32_t b1 = (s + 1) >> 2, b2 = b1 + 1;
+  const bool j1 = alive && !fresh && 4 * b1 < spp && r.jtag[(b1 & 1u) * BLOCK] != b1;
+  const bool j2 = alive && !fresh && 4 * b2 < spp && r.jtag[(b2 & 1u) * BLOCK] != b2;
+  const bool crit = alive && (fresh || have <= RNG_CRIT);
+  const bool room = alive && (fresh || have < RING || j1 || j2);
+  if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
+  if (room) {
+    DREG(DREG_REFILL)
+    const bool main = fresh || crit || !(j1 || j2);
+    const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
+    uint32_t k[8], w[16];
+    if (fresh) {
+      DREG(DREG_BEGIN_PIXEL)
+      seed_key(seed, k);
+      store_key(r, k);
+    } else {
+      load_key(r, k);
+    }
+    chacha12(k, b, w);
+    store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);
+    if (fresh) {  // block 0 is also the jitter block of samples 0-3 (render.rs:74-82)
+      store_block(jit_slot(r, 0), w);
+      r.pos = 0;
+      *r.end = 1;
+      r.jtag[0] = 0;
+      r.jtag[BLOCK] = 0xFFFFFFFFu;
+    } else if (main) {
+      *r.end = end + 1;
+    } else {
+      r.jtag[(b & 1u) * BLOCK] = b;
+    }
+  }
+}
+
+// Jitter words 4s..4s+3 of the pixel-start stream (block s/4).
+// Keystream block b of the lane's key into dst, for the rare draw that finds its block not made yet.  Out
+// of line: the kernel is ~50 KB of code against a 64 KB instruction cache shared by two CUs, and each
+// inlined ChaCha12 is ~2.5 KB that only the fallback paths execute.
+static __device__ __attribute__((noinline)) void gen_block(const uint4* slab, uint32_t b, uint4* dst) {
+  const uint4 a = slab[SLAB_KEY], c = slab[SLAB_KEY + 1];
+  const uint32_t k[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  uint32_t w[16];
+  chacha12(k, b, w);
+  store_block(dst, w);
+}
+
+RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
+  const uint32_t b = s >> 2;
+  if (r.jtag[(b & 1u) * BLOCK] != b) {
+    DREG(DREG_JIT_FALLBACK)
+    gen_block(r.slab, b, jit_slot(r, b));
+    r.jtag[(b & 1u) * BLOCK] = b;
+  }
+  return jit_slot(r, b)[s & 3u];
+}
+
+// rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
+RPK_INLINE double u64_to_f64(uint64_t u) { return (double)(u >> 11) * (1.0 / 9007199254740992.0); }
+// The same value from the two keystream words, as hi * 2^-32 + (lo >> 11) * 2^-53: both terms and the sum
+// k * 2^-53 (k < 2^53) are exact, so the FMA returns the identical double in 2 cvt + 1 mul + 1 FMA.
+RPK_INLINE double words_f64(uint32_t lo, uint32_t hi) {
+  return __builtin_fma((double)hi, 0x1p-32, (double)(lo >> 11) * 0x1p-53);
+}
+// 2 * words_f64 - 1 (the distributions' `2.0 * r - 1.0`, randomness.rs:24,42,61): 2g = k * 2^-52 is exact and
+// so is k * 2^-52 - 1 (a multiple of 2^-52 of magnitude <= 1), whatever the order -- two exact FMAs.
+RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
+  return __builtin_fma((double)hi, 0x1p-31, __builtin_fma((double)(lo >> 11), 0x1p-52, -1.0));
+}
+// Every draw reads the ring directly: the RING blocks of a lane are one circular run of 16*RING words in
+// its slab (L2-resident), so stream word a sits at ring word a % (16*RING) while its block is held
+// (blocks [end - RING, end)).  A draw site makes sure every block it touches is there (ring_ensure:
+// generated in place when the refill pass has not made it yet, rare) and loads its u64 words with one
+// dwordx2 each.  Rejection loops (UnitBall / UnitSphere / UnitDisk) load and evaluate RPK_TRIES tries at
+// once and keep the first accepted one -- the draws consumed, and so the stream, are exactly the
+// sequential loop's.  A wave iterates until its slowest lane accepts: with
+// acceptance p a lane needs a geometric number of tries, and the wave's maximum over its ~20 shading lanes
+// is ~5 single tries for the ball (p = pi/6); each round pays one ring-load latency.  (Before, a draw
+// checked its block and the wave copied a 16-word block into LDS whenever any lane crossed one.)
+#ifndef RPK_TRIES
+#define RPK_TRIES 2
+#endif
+static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * RING words (a power of two)");
+RPK_INLINE uint2 ring_u64(const Rng& r, uint32_t a) {  // stream words a, a+1 (a even)
+  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RING - 1u)) >> 1];
+}
+RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64
+  const uint2 v = ring_u64(r, a);
+  return words_f64(v.x, v.y);
+}
+RPK_INLINE double ring_sym(const Rng& r, uint32_t a) {  // 2 * Standard f64 - 1
+  const uint2 v = ring_u64(r, a);
+  return words_sym(v.x, v.y);
+}
+RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
+  while (last_blk >= *r.end) {
+    DREG(DREG_RNG_FALLBACK)
+    const uint32_t b = *r.end;
+    gen_block(r.slab, b, ring_slot(r, b));
+    *r.end = b + 1;
+  }
+}
+// One Standard f64 draw (rand 0.8 gen::<f64>, two stream words)
+RPK_INLINE double gen_f64(Rng& r) {
+  ring_ensure(r, r.pos >> 4);
+  const double x = ring_f64(r, r.pos);
+  r.pos += 2;
+  return x;
+}
+
+// ------------------------------------------------------------------ math -------------------------
+
+struct V3 { double x, y, z; };
+RPK_INLINE V3 v3(double x, double y, double z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+RPK_INLINE V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+RPK_INLINE V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+RPK_INLINE V3 mulc(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+RPK_INLINE V3 smul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+RPK_INLINE double dot(V3 a, V3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }    // nalgebra dot
+RPK_INLINE double norm2(V3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }         // norm_squared
+RPK_INLINE V3 normalize(V3 a) { double n = sqrt(norm2(a)); return v3(a.x / n, a.y / n, a.z / n); }
+RPK_INLINE V3 reflect(V3 i, V3 n) { return sub(i, smul(2.0 * dot(i, n), n)); }         // utility.rs:106
+
+// Rust `as` casts saturate, NaN -> 0
+RPK_INLINE uint32_t sat_u32(double x) {
+  if (!(x > 0.0)) return 0u;
+  if (x >= 4294967295.0) return 4294967295u;
+  return (uint32_t)x;
+}
+RPK_INLINE int64_t sat_i64(double x) {
+  if (x != x) return 0;
+  if (x >= 9223372036854775807.0) return INT64_MAX;
+  if (x <= -9223372036854775808.0) return INT64_MIN;
+  return (int64_t)x;
+}
+
+// randomness.rs:91-105 (wrapping isize, arithmetic >> 13)
+RPK_INLINE int64_t noise_integer(int64_t x, int64_t y, int64_t z, int64_t seed) {
+  uint64_t h = 0x369E6D3B899E43CFull * (uint64_t)x + 0x53F89E7FFDA3B07Dull * (uint64_t)y +
+               0x3B13C1CA4937E629ull * (uint64_t)z + 0x577C2C6E4019D645ull * (uint64_t)seed;
+  h = (uint64_t)((int64_t)h >> 13) ^ h;
+  h = h * (h * h * 60493ull + 19990303ull) + 1376312589ull;
+  return (int64_t)h;
+}
+RPK_INLINE double noise_real(int64_t x, int64_t y, int64_t z, int64_t seed) {
+  return (double)noise_integer(x, y, z, seed) / 9223372036854775807.0;
+}
+
+// ------------------------------------------------------------------ traversal --------------------
+
+struct HitRec {
+  double t, u, v;  // u, v: barycentrics of hittable.rs:89-95 (triangles)
+  int32_t prim;    // -1 = miss
+};
+
+struct TravDiag {
+  uint32_t visits = 0, tests = 0, trips = 0;
+};
+
+// ---- conservative f32 box test ------------------------------------------------------------------
+//
+// Child boxes are f32, rounded outward from the exact f64 boxes.  The ray enters in f32 as o32 = fl(o),
+// inv = rcp(fl(d)) (<= 1 ulp), oinv = fl(o32 * inv), and each slab plane costs one FMA:
+// t^ = fma(lo, inv, -oinv).  Against the exact t = (lo - o) / d:
+//     |t^ - t| <= 5u |t| + |o - o32| |inv| (1 + 6u) + u |o32 inv|        (u = 2^-24)
+// so with D = max over axes of the last two terms, a box whose exact interval meets [t_min, best] at
+// some t* > 0 satisfies  tnear^ <= t*(1 + 5u) + D  and  tfar^ >= t*(1 - 5u) - D  (the near planes behind
+// the origin and tmin32 <= t* do not raise tnear^; every far plane lies at or beyond t*).  The test
+//     fma(tnear^, 1 - 2^-19, -slack) <= tfar^                    (slack >= 3D)
+// then passes every such box: its exact left side is <= t*(1+5u)(1-2^-19) + D - slack <= t*(1-5u) - 2D
+// - 22u t*, which leaves 22u t* + D to absorb the FMA's rounding (<= u (tnear^ + slack)).  It may pass a
+// few more boxes, never fewer: no primitive the reference's f64 test reaches is culled.  An empty slot
+// (lo = +inf, hi = -inf) gives tnear^ = +inf, tfar^ = -inf and fails.
+// Slopes are clamped to |inv| <= 2^64 (axis-parallel rays), so every t^ is finite.
+struct Ray32 {
+  float ix, iy, iz;     // rcp(fl(d))
+  float oix, oiy, oiz;  // fl(o32 * inv)
+  float slack;          // >= 3D (per ray)
+  float tmin;           // t_min rounded down
+  uint32_t nx, ny, nz;  // byte offset of the near plane of each axis within Node4 (lo_* or hi_*: by the
+                        // sign of the slope), the far plane is the other one
+};
+
+// next representable float towards +inf / -inf (finite inputs; the callers only step values that
+// rounded the wrong way, which are finite)
+RPK_INLINE float next_up(float f) {
+  const int32_t b = __float_as_int(f);
+  if (f == 0.0f) return __int_as_float(1);
+  return __int_as_float(f > 0.0f ? b + 1 : b - 1);
+}
+RPK_INLINE float next_down(float f) { return -next_up(-f); }
+RPK_INLINE float f32_down(double x) {
+  const float f = (float)x;
+  return (double)f > x ? next_down(f) : f;
+}
+RPK_INLINE float f32_up(double x) {
+  const float f = (float)x;
+  return (double)f < x ? next_up(f) : f;
+}
+
+RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, Ray32& r) {
+  const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
+  // |inv| clamped to 2^64: a zero direction component gives a huge finite slope instead of inf, so the
+  // fma form never forms inf - inf; the slack term |o - o32| |inv| still covers an origin that rounded
+  // across a slab plane, and a slab the ray never reaches still yields a huge t (a miss), as in f64.
+  r.ix = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.x), -0x1p64f), 0x1p64f);
+  r.iy = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.y), -0x1p64f), 0x1p64f);
+  r.iz = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.z), -0x1p64f), 0x1p64f);
+  r.oix = ox * r.ix;
+  r.oiy = oy * r.iy;
+  r.oiz = oz * r.iz;
+  // |o - o32| is exact in f64 (Sterbenz); an axis with no origin rounding contributes no origin term
+  const double ex = fabs(o.x - (double)ox), ey = fabs(o.y - (double)oy), ez = fabs(o.z - (double)oz);
+  const double k = 1.0 + 0x1p-20, u = 0x1p-23;
+  double D = 0.0;
+  D = fmax(D, (ex == 0.0 ? 0.0 : ex * fabs((double)r.ix) * k) + fabs((double)r.oix) * u);
+  D = fmax(D, (ey == 0.0 ? 0.0 : ey * fabs((double)r.iy) * k) + fabs((double)r.oiy) * u);
+  D = fmax(D, (ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)r.oiz) * u);
+  r.slack = f32_up(3.0 * D * k + 0x1p-126);
+  r.tmin = f32_down(tmin);
+  // Node4: lo_x at 0, hi_x at 16, lo_y at 32, hi_y at 48, lo_z at 64, hi_z at 80
+  r.nx = r.ix < 0.0f ? 16u : 0u;
+  r.ny = r.iy < 0.0f ? 48u : 32u;
+  r.nz = r.iz < 0.0f ? 80u : 64u;
+}
+
+// Closest hit over the 4-wide BVH (the reference's Hittable::Bvh::hit, bvh.rs:121-124 / hit_node
+// bvh.rs:93-119: any tree shape and visit order returns the same closest hit up to exact-t ties,
+// SURVEY.md 8a A9).  Primitive tests are the reference's exact f64 ones; t_max shrinks to the closest
+// hit so far and acceptance is `t <= t_max`, so an equal-t primitive tested later wins
+// (hittable.rs:52,99).  Structure: "while-while" -- descend inner nodes (near child first, the others
+// pushed far-to-near on the LDS stack) until this lane holds a leaf, then test the leaf's primitives;
+// the wave runs the expensive f64 leaf code once for every lane that reached a leaf.
+//
+// The traversal state is explicit (TravState) so a lane can stop between steps and resume later: the
+// render kernel steps traversal until few lanes are still traversing, shades the finished ones and
+// gives them new rays, then resumes (see render_kernel).
+struct TravState {
+  double best, bu, bv;
+  int32_t bestp;
+  uint32_t cur, sp;
+  uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
+};
+
+RPK_INLINE bool trav_done(const TravState& t) { return t.cur == rpl::ENTRY_EMPTY && t.leaf == 0u; }
+
+RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
+  t.best = tmax;
+  t.bu = 0.0;
+  t.bv = 0.0;
+  t.bestp = -1;
+  t.cur = S.root;
+  t.sp = 0;
+  t.leaf = 0;
+}
+
+// One exact f64 primitive test (the reference's Hittable::hit for a leaf, hittable.rs:39-101): on
+// acceptance `best` shrinks to t and the hit record is taken.
+RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, double& best, TravState& ts) {
+  // 32-bit byte offset from the wave-uniform base (scalar-base + vector-offset loads)
+  const double2* q = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(S.prims) +
+                                                      k * (uint32_t)sizeof(rpl::Prim));
+  const double2 g01 = q[0], g23 = q[1], g45 = q[2], g67 = q[3];
+  const double2 g8k = q[4];  // g[8], {kind, material}
+  const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+  if (kind == rpl::PRIM_TRIANGLE) {
+    // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
+    const V3 a = v3(g01.x, g01.y, g23.x);
+    const V3 ba = v3(g23.y, g45.x, g45.y);
+    const V3 ca = v3(g67.x, g67.y, g8k.x);
+    const V3 pa = sub(a, o);
+    const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                     - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
+    if (fabs(det) < SMOL) return;
+    const double inv_det = 1.0 / det;
+    const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                    + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                    + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+    const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                    + pa.y * (ca.z * d.x - ca.x * d.z)
+                    + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+    const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                    + pa.y * (ba.x * d.z - ba.z * d.x)
+                    + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
+    const double w = 1.0 - u - v;
+    if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) return;
+    best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
+  } else {
+    // hittable.rs:39-57
+    const V3 c = v3(g01.x, g01.y, g23.x);
+    const double radius = g23.y;
+    const V3 tc = sub(o, c);
+    const double a = norm2(d);
+    const double half_b = dot(d, tc);
+    const double cq = norm2(tc) - radius * radius;
+    const double delta = half_b * half_b - a * cq;
+    if (delta <= 0.0) return;
+    const double sq = sqrt(delta);
+    double t = (-half_b - sq) / a;
+    if (t < tmin || t > best) {
+      t = (-half_b + sq) / a;
+      if (t < tmin || t > best) return;
+    }
+    best = t; ts.bestp = (int32_t)k;
+  }
+}
+
+// A new ray: the always-tested primitives (KScene::n_always: boxes that dwarf the rest of the scene, kept
+// out of the tree by the host builder) get their exact tests here, one wave-uniform loop over the same
+// primitive for every starting lane, instead of a divergent leaf test deep in the prim loop; their hit
+// also bounds the traversal from the root.  The closest hit is the tree's (any test order, up to exact-t
+// ties).
+RPK_INLINE void trav_begin(const KScene& S, V3 o, V3 d, double tmin, double tmax, TravState& t) {
+  trav_init(S, tmax, t);
+  double best = t.best;
+  for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++) prim_test(S, k, o, d, tmin, best, t);
+  t.best = best;
+}
+
+// Stack entry i of a lane: in its LDS column (entry i at stk[i * stride]) or, for SPILL kernels, entries
+// >= S.lds_depth in the lane's global overflow run (S.spill[spl + i - lds_depth], L2-resident) -- a deep
+// tree (config C5: 43 entries) then keeps the LDS of four blocks per CU.  The two parts are typed with
+// their address spaces (LDS = 3, global = 1): with generic pointers the compiler merged the LDS and the
+// spill store of a push into one FLAT store through a selected pointer (and the pops into FLAT loads),
+// which waits on both memory counters at every node visit.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint32_t glb_u32;
+RPK_INLINE glb_u32* spill_ptr(const KScene& S) { return (glb_u32*)S.spill; }
+template <bool SPILL>
+RPK_INLINE void stk_put(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t i, uint32_t v) {
+  if (!SPILL || i < S.lds_depth) stk[i * stride] = v;
+  else spill_ptr(S)[spl + i - S.lds_depth] = v;
+}
+template <bool SPILL>
+RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t i) {
+  if (!SPILL || i < S.lds_depth) return stk[i * stride];
+  return spill_ptr(S)[spl + i - S.lds_depth];
+}
+
+// One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
+// parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
+template <bool SPILL>
+RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
+                          double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
+  uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
+  double best = ts.best;
+  float best32 = f32_up(best);
+  const uint32_t cap = S.stack_depth - STACK_SLACK;
+  // ---- inner nodes
+  while (!(cur & rpl::ENTRY_LEAF)) {
+    DIAG(if (td) td->visits++;)
+    DREG(DREG_NODE)
+    // Near/far planes chosen per ray by the slope signs (octant), so each child costs one max3 + max
+    // for t_near and one min3 + min for t_far.  For a valid box this is the same pair of values the
+    // min/max slab form picks (fma is monotone in the plane coordinate); an empty slot (lo = +inf,
+    // hi = -inf) gives t_near = +inf, t_far = -inf and a NaN limit, so it can never pass.
+    // 32-bit byte offsets from the (wave-uniform) node base: scalar-base + vector-offset addressing
+    const char* nb = reinterpret_cast<const char*>(S.nodes);
+    const uint32_t no = cur << 7;
+    const float4 nx = *reinterpret_cast<const float4*>(nb + (no + r.nx));
+    const float4 fx = *reinterpret_cast<const float4*>(nb + (no + (r.nx ^ 16u)));
+    const float4 ny = *reinterpret_cast<const float4*>(nb + (no + r.ny));
+    const float4 fy = *reinterpret_cast<const float4*>(nb + (no + (r.ny ^ 16u)));
+    const float4 nz = *reinterpret_cast<const float4*>(nb + (no + r.nz));
+    const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.nz ^ 16u)));
+    const uint4 ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
+    float tn[4];
+    uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
+    // slab planes of children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the
+    // same per-element rounding as fmaf
+    const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+    const f2 nox = {-r.oix, -r.oix}, noy = {-r.oiy, -r.oiy}, noz = {-r.oiz, -r.oiz};
+    const f2 NX[2] = {pk_fma(f2{nx.x, nx.y}, ix, nox), pk_fma(f2{nx.z, nx.w}, ix, nox)};
+    const f2 FX[2] = {pk_fma(f2{fx.x, fx.y}, ix, nox), pk_fma(f2{fx.z, fx.w}, ix, nox)};
+    const f2 NY[2] = {pk_fma(f2{ny.x, ny.y}, iy, noy), pk_fma(f2{ny.z, ny.w}, iy, noy)};
+    const f2 FY[2] = {pk_fma(f2{fy.x, fy.y}, iy, noy), pk_fma(f2{fy.z, fy.w}, iy, noy)};
+    const f2 NZ[2] = {pk_fma(f2{nz.x, nz.y}, iz, noz), pk_fma(f2{nz.z, nz.w}, iz, noz)};
+    const f2 FZ[2] = {pk_fma(f2{fz.x, fz.y}, iz, noz), pk_fma(f2{fz.z, fz.w}, iz, noz)};
+    f2 TN[2], TF[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        TN[q][e] = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
+        TF[q][e] = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
+      }
+      // fma(tnear, 1 - 2^-19, -slack) <= tfar (section 4.2 of DESIGN.md): one packed FMA per pair
+      const f2 lhs = pk_fma(TN[q], f2{1.0f - 0x1p-19f, 1.0f - 0x1p-19f}, f2{-r.slack, -r.slack});
+#pragma unroll
+      for (int e = 0; e < 2; e++) {
+        const int c = 2 * q + e;
+        tn[c] = lhs[e] <= TF[q][e] ? TN[q][e] : __builtin_huge_valf();
+      }
+    }
+    // sort (tn, entry) ascending: misses (+inf) go last
+#define RPK_CSWAP(a, b)                                   \
+{                                                       \
+  const bool sw = tn[b] < tn[a];                        \
+  const float t_ = sw ? tn[b] : tn[a];                  \
+  tn[b] = sw ? tn[a] : tn[b];                           \
+  tn[a] = t_;                                           \
+  const uint32_t c_ = sw ? cc[b] : cc[a];               \
+  cc[b] = sw ? cc[a] : cc[b];                           \
+  cc[a] = c_;                                           \
+}
+    RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
+#undef RPK_CSWAP
+    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1
+    // farther ones far-to-near without branches: slots sp..sp+2 are written unconditionally (the stack
+    // has STACK_SLACK spare entries; slots past the new top are garbage) and sp advances by k.
+    const float INFF = __builtin_huge_valf();
+    const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
+                           (uint32_t)(tn[3] != INFF);
+    const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
+    const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
+    if (!SPILL || sp + 2u < S.lds_depth) {
+      stk[sp * stride] = e0;
+      stk[(sp + 1u) * stride] = e1;
+      stk[(sp + 2u) * stride] = cc[1];
+    } else {
+      stk_put<SPILL>(S, stk, stride, spl, sp, e0);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 1u, e1);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, cc[1]);
+    }
+    sp += k;
+    if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
+      overflow = true;
+      sp = cap;
+    }
+    if (n_hit) cur = cc[0];
+    else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+#ifndef RPK_NO_SPECULATIVE
+    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
+    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.
+    if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+      leaf = cur;
+      cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+    }
+    // ... and once at most RPK_LEAF_BREAK lanes still look for one, the wave moves on to the leaves: the
+    // last few descents ran with most of the wave idle (those lanes resume their descent next step)
+    if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= RPK_LEAF_BREAK) break;
+#ifdef RPK_NODE_BREAK  // experiment: leave once at most this many lanes are still descending at all
+    if ((uint32_t)__popcll(__ballot(true)) <= RPK_NODE_BREAK) break;
+#endif
+#endif
+  }
+  if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+    leaf = cur;
+    cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+  }
+  // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
+  // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
+  // lanes with different leaf sizes advance together instead of the wave running every leaf's count.
+  uint32_t k = leaf & rpl::LEAF_FIRST_MASK;
+  uint32_t kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+  while (leaf != 0u) {
+    DIAG(if (td) td->tests++;)
+    DREG(DREG_PRIM)
+    prim_test(S, k, o, d, tmin, best, ts);
+    if (++k == kend) {
+      if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
+        leaf = cur;
+        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+        k = leaf & rpl::LEAF_FIRST_MASK;
+        kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+      } else {
+        leaf = 0u;
+      }
+    }
+    if (RPK_PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= RPK_PRIM_BREAK) {
+      // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
+      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
+      break;
+    }
+  }
+  ts.cur = cur;
+  ts.sp = sp;
+  ts.best = best;
+  ts.leaf = leaf;
+}
+
+RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
+                         HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
+  Ray32 r;
+  setup_ray32(o, d, tmin, r);
+  TravState t;
+  trav_begin(S, o, d, tmin, tmax, t);
+  while (!trav_done(t)) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
+  hr.t = t.best;
+  hr.u = t.bu;
+  hr.v = t.bv;
+  hr.prim = t.bestp;
+}
+
+// Hit record of the closest primitive (hittable.rs:59-62, 103-107).
+struct Surf {
+  V3 p, n;
+  double u, v;
+  uint32_t material;
+};
+
+// uv is computed only when the hit material reads it (rpl::Material::needs_uv): same values, and the
+// f64 atan2/asin of a sphere hit are skipped for untextured spheres (the ground).
+RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, bool force_uv = false) {
+  const rpl::Prim* p = S.prims + hr.prim;
+  s.p = add(o, smul(hr.t, d));  // Ray::at (utility.rs:67)
+  s.material = p->material;
+  s.u = 0.0;
+  s.v = 0.0;
+  const bool need_uv = force_uv || S.mats[s.material].needs_uv != 0;
+  if (p->kind == rpl::PRIM_TRIANGLE) {
+    const double u = hr.u, v = hr.v, w = 1.0 - u - v;
+    const rpl::PrimRef& pr = S.prim_refs[hr.prim];
+    const uint32_t i0 = pr.v[0], i1 = pr.v[1], i2 = pr.v[2];
+    const V3 n0 = v3(S.vnrm[3 * i0], S.vnrm[3 * i0 + 1], S.vnrm[3 * i0 + 2]);
+    const V3 n1 = v3(S.vnrm[3 * i1], S.vnrm[3 * i1 + 1], S.vnrm[3 * i1 + 2]);
+    const V3 n2 = v3(S.vnrm[3 * i2], S.vnrm[3 * i2 + 1], S.vnrm[3 * i2 + 2]);
+    s.n = add(add(smul(w, n0), smul(u, n1)), smul(v, n2));
+    if (need_uv) {
+      s.u = (w * S.vuv[2 * i0] + u * S.vuv[2 * i1]) + v * S.vuv[2 * i2];
+      s.v = (w * S.vuv[2 * i0 + 1] + u * S.vuv[2 * i1 + 1]) + v * S.vuv[2 * i2 + 1];
+    }
+  } else {
+    const V3 c = v3(p->g[0], p->g[1], p->g[2]);
+    s.n = normalize(sub(s.p, c));
+    return need_uv;  // the caller computes the sphere uv (shared site)
+  }
+  return false;
+}
+
+// ------------------------------------------------------------------ shading ----------------------
+
+// x / 255.0 for a byte x, correctly rounded without a division: q0 = x * fl(1/255) is off by at most
+// one ulp and one FMA residual step corrects it (exhaustively checked for all 256 x, tests/test_host.py).
+RPK_INLINE double u8_unit(uint32_t x) {
+  const double xd = (double)x, R = 1.0 / 255.0;
+  const double q0 = xd * R;
+  return __builtin_fma(__builtin_fma(-q0, 255.0, xd), R, q0);
+}
+
+// texture.rs:51-60: walk Checker indirections down to the texture that produces the value
+// (validate() guarantees the walk terminates).
+RPK_INLINE uint32_t tex_resolve(const KScene& S, uint32_t tid, const Surf& h) {
+  while (S.texs[tid].kind == 4) {
+    const rpl::Texture& t = S.texs[tid];
+    const double s = floor(h.p.x) + floor(h.p.y) + floor(h.p.z);
+    tid = fmod(s, 2.0) == 0.0 ? t.even : t.odd;
+  }
+  return tid;
+}
+
+// texture.rs:40-49 Image: clamp, then saturating `as u32` -> texel index
+RPK_INLINE uint64_t image_texel(const rpl::Texture& t, const Surf& h) {
+  const double w = (double)t.width, hh = (double)t.height;
+  double x = h.u * w, y = h.v * hh;
+  if (x < 0.0) x = 0.0;
+  if (x > w - 1.0) x = w - 1.0;
+  if (y < 0.0) y = 0.0;
+  if (y > hh - 1.0) y = hh - 1.0;
+  return t.texel_offset + (uint64_t)sat_u32(x) + (uint64_t)sat_u32(y) * t.width;
+}
+
+// texture.rs:21-118 value of a resolved (non-Checker) texture; `px` is the Image texel, fetched by the
+// caller ahead of use so its latency overlaps other shading work.
+RPK_INLINE V3 tex_value(const KScene& S, uint32_t tid, const Surf& h, uint32_t px) {
+  const rpl::Texture& t = S.texs[tid];
+  switch (t.kind) {
+    case 1:  // DebugUVs
+      return v3(h.u, h.v, 0.0);
+    case 2:  // Solid
+      return v3(t.color[0], t.color[1], t.color[2]);
+    case 3:  // Image
+      return v3(u8_unit(px & 0xffu), u8_unit((px >> 8) & 0xffu), u8_unit((px >> 16) & 0xffu));
+      case 5: {  // Noise (texture.rs:62-68)
+        double x = noise_real(sat_i64(floor(h.p.x)), sat_i64(floor(h.p.y)), sat_i64(floor(h.p.z)), t.seed);
+        x = 0.5 * x + 0.5;
+        return v3(x, x, x);
+      }
+      case 6: {  // Perlin (texture.rs:83-118)
+        const V3 p = h.p;
+        const V3 fp = v3(floor(p.x), floor(p.y), floor(p.z));
+        const int64_t fx = sat_i64(fp.x), fy = sat_i64(fp.y), fz = sat_i64(fp.z);
+        const int64_t cx = (int64_t)((uint64_t)fx + 1), cy = (int64_t)((uint64_t)fy + 1),
+                      cz = (int64_t)((uint64_t)fz + 1);
+        const int64_t s1 = (int64_t)((uint64_t)t.seed + 1), s2 = (int64_t)((uint64_t)t.seed + 2),
+                      s3 = (int64_t)((uint64_t)t.seed + 3);
+        double k[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int64_t X = (q & 1) ? cx : fx, Y = (q & 2) ? cy : fy, Z = (q & 4) ? cz : fz;
+          const V3 g = v3(noise_real(X, Y, Z, s1), noise_real(X, Y, Z, s2), noise_real(X, Y, Z, s3));
+          k[q] = dot(sub(p, v3((double)X, (double)Y, (double)Z)), g);
+        }
+        V3 tt = sub(p, fp);
+        tt.x = (tt.x * (tt.x * 6.0 - 15.0) + 10.0) * tt.x * tt.x * tt.x;
+        tt.y = (tt.y * (tt.y * 6.0 - 15.0) + 10.0) * tt.y * tt.y * tt.y;
+        tt.z = (tt.z * (tt.z * 6.0 - 15.0) + 10.0) * tt.z * tt.z * tt.z;
+        const double k12 = (k[1] - k[0]) * tt.x + k[0], k34 = (k[3] - k[2]) * tt.x + k[2];
+        const double k56 = (k[5] - k[4]) * tt.x + k[4], k78 = (k[7] - k[6]) * tt.x + k[6];
+        const double k1234 = (k34 - k12) * tt.y + k12, k5678 = (k78 - k56) * tt.y + k56;
+        const double kk = (k5678 - k1234) * tt.z + k1234;
+        const double x = 0.5 * kk + 0.5;
+        return v3(x, x, x);
+      }
+      default:  // Missing
+      return v3(0.0, 0.0, 0.0);
+  }
+}
+
+RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
+  tid = tex_resolve(S, tid, h);
+  const rpl::Texture& t = S.texs[tid];
+  const uint32_t px = t.kind == 3 ? S.texels[image_texel(t, h)] : 0u;
+  return tex_value(S, tid, h, px);
+}
+
+// material.rs:49-60 Emit::evaluate (SkySphere's texture value sampled by the caller)
+RPK_INLINE V3 emit_eval(uint32_t kind, V3 color, V3 tex, V3 d, const Surf& h) {
+  switch (kind) {
+    case 1: return h.n;                                  // DebugNormals
+    case 2: return color;                                // Color
+    case 3: {                                            // SkyGradient
+      const double t = 0.5 * (d.y / sqrt(norm2(d)) + 1.0);
+      return add(smul(1.0 - t, v3(1.0, 1.0, 1.0)), smul(t, v3(0.5, 0.7, 1.0)));
+    }
+    case 4: return tex;                                  // SkySphere
+    default: return v3(0.0, 0.0, 0.0);                   // None
+  }
+}
+
+// material.rs:74-81 Absorb::evaluate (AlbedoMap's texture value sampled by the caller)
+RPK_INLINE V3 absorb_eval(const rpl::Material& m, V3 tex) {
+  switch (m.absorb_kind) {
+    case 1: return v3(1.0, 1.0, 1.0);
+    case 2: return v3(m.absorb_color[0], m.absorb_color[1], m.absorb_color[2]);
+    case 3: return tex;
+    default: return v3(0.0, 0.0, 0.0);
+  }
+}
+
+// material.rs:27-34, 115-179 Scatter::evaluate.  Returns true and the new direction when scattered.
+template <class R>
+RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, R& rng, V3& nd) {
+  switch (m.scatter_kind) {
+    case 1: {  // Lambert (material.rs:115-130)
+      DREG(DREG_LAMBERT)
+      if (dot(h.n, d) > 0.0) return false;
+      double x = 0.0, y = 0.0, s = 0.0;
+      // UnitSphere (randomness.rs:58-73): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
+        DREG(DREG_LOOP_LAMBERT)
+        ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
+        double tx[RPK_TRIES], ty[RPK_TRIES];
+#pragma unroll
+        for (int j = 0; j < RPK_TRIES; j++) {
+          tx[j] = ring_sym(rng, a + 4u * j);
+          ty[j] = ring_sym(rng, a + 4u * j + 2u);
+        }
+        bool done = false;
+#pragma unroll
+        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+          const double qx = tx[j], qy = ty[j], qs = qx * qx + qy * qy;
+          if (qs < 1.0) { x = qx; y = qy; s = qs; rng.pos = a + 4u * (j + 1); done = true; }
+        }
+        if (done) break;
+      }
+      const double q = 2.0 * sqrt(1.0 - s);
+      nd = normalize(add(h.n, v3(x * q, y * q, 1.0 - 2.0 * s)));
+      return true;
+    }
+    case 2: {  // Metal (material.rs:132-152)
+      DREG(DREG_METAL)
+      if (dot(h.n, d) > 0.0) return false;
+      double x = 0.0, y = 0.0, z = 0.0;
+      // UnitBall (randomness.rs:39-53): tries of 3 draws, RPK_TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 6u * RPK_TRIES) {
+        DREG(DREG_LOOP_METAL)
+        ring_ensure(rng, (a + 6u * RPK_TRIES - 1u) >> 4);
+        double tx[RPK_TRIES], ty[RPK_TRIES], tz[RPK_TRIES];
+#pragma unroll
+        for (int j = 0; j < RPK_TRIES; j++) {
+          tx[j] = ring_sym(rng, a + 6u * j);
+          ty[j] = ring_sym(rng, a + 6u * j + 2u);
+          tz[j] = ring_sym(rng, a + 6u * j + 4u);
+        }
+        bool done = false;
+#pragma unroll
+        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+          const double qx = tx[j], qy = ty[j], qz = tz[j];
+          if ((qx * qx + qy * qy) + qz * qz < 1.0) { x = qx; y = qy; z = qz; rng.pos = a + 6u * (j + 1); done = true; }
+        }
+        if (done) break;
+      }
+      const V3 r = normalize(add(reflect(d, h.n), smul(m.scatter_param, v3(x, y, z))));
+      if (dot(h.n, r) < 0.0) return false;
+      nd = r;
+      return true;
+    }
+    case 3: {  // Dielectric (material.rs:154-179)
+      DREG(DREG_DIELEC)
+      double eta;
+      V3 n;
+      if (dot(h.n, d) > 0.0) { eta = m.scatter_param; n = v3(-h.n.x, -h.n.y, -h.n.z); }
+      else { eta = 1.0 / m.scatter_param; n = h.n; }
+      double r0 = (1.0 - eta) / (1.0 + eta);
+      r0 = r0 * r0;                                  // powi(2)
+      const double x = 1.0 + dot(n, d);
+      const double x2 = x * x;
+      const double reflectance = r0 + (1.0 - r0) * (x * (x2 * x2));  // powi(5), LLVM binary expansion
+      if (gen_f64(rng) < reflectance) {              // Bernoulli (randomness.rs:78-82)
+        nd = reflect(d, n);
+      } else {
+        const double cos_theta = dot(n, d);          // refract (utility.rs:111-119)
+        const double k = 1.0 - eta * eta * (1.0 - cos_theta * cos_theta);
+        if (k < 0.0) nd = reflect(d, n);
+        else nd = sub(smul(eta, d), smul(eta * cos_theta + sqrt(k), n));
+      }
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
+// Shading of one finished ray: the step of the reference's trace_path after the closest-hit query
+// (render.rs:104-118 / 133-145, material.rs:104-110): the hit's surface record or the miss's
+// Hit::at_infinity, textures, Scatter (the only RNG consumer), Absorb, Emit; T (*) emit goes into the sum
+// (forward accumulation: main.rs:80 adds the sample's total, the association differs in the last ulp only).
+// Returns true when the material scattered: (o, d) become the hit point and the new direction and T is
+// multiplied by the absorption.  Hits and misses share one spherical-uv site and one texture site, so a
+// wave with both pays for each f64 atan2/asin and texture walk once.
+template <class R, class D, class U>
+RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rng, D& T_x, D& T_y, D& T_z, D& sum_x,
+                          D& sum_y, D& sum_z, bool first, U& hits) {
+  const bool hit = hr.prim >= 0;
+  Surf h;
+  const rpl::Material* m = nullptr;
+  bool sph_uv;
+  if (hit) {
+    DREG(DREG_SURF)
+    sph_uv = surface(S, hr, o, d, h);
+    m = &S.mats[h.material];
+  } else {
+    DREG(DREG_MISS)
+    // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
+    h.p = d;
+    h.n = d;
+    h.u = 0.0;
+    h.v = 0.0;
+    h.material = 0;
+    sph_uv = S.background.needs_uv != 0;
+  }
+  if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
+    DREG(DREG_SPHUV)
+    const V3 q = hit ? h.n : d;
+    h.u = 0.5 - atan2(q.z, q.x) / TAU_;
+    h.v = asin(q.y) / PI_ + 0.5;
+  }
+  // Textures: each lane reads at most one here -- the absorb map of a hit or the sky sphere of a miss
+  // (or of an emissive hit); its Checker walk and Image texel load are issued BEFORE the scatter so
+  // the load latency overlaps it.  A hit reading both takes the second in a rare extra pass.
+  const uint32_t emit_kind = hit ? m->emit_kind : S.background.kind;
+  const uint32_t emit_tex = hit ? m->emit_tex : S.background.tex;
+  const bool ta = hit && m->absorb_kind == 3, te = emit_kind == 4;
+  const bool t1 = ta || te;
+  uint32_t tid1 = 0, px1 = 0;
+  // a miss under an Image sky sphere: size and offset are kernel arguments (scalar registers), so the
+  // texel load waits on no texture-table load
+  const bool sky_img = !hit && S.background.img_w != 0;
+  if (t1) {
+    if (sky_img) {
+      rpl::Texture t;
+      t.width = S.background.img_w;
+      t.height = S.background.img_h;
+      t.texel_offset = S.background.img_off;
+      tid1 = S.background.tex;
+      px1 = S.texels[image_texel(t, h)];
+    } else {
+      tid1 = tex_resolve(S, ta ? m->absorb_tex : emit_tex, h);
+      const rpl::Texture& t = S.texs[tid1];
+      if (t.kind == 3) px1 = S.texels[image_texel(t, h)];
+    }
+  }
+  // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
+  V3 nd = v3(0.0, 0.0, 0.0);
+  bool scattered = false;
+  if (hit) scattered = scatter_eval(*m, d, h, rng, nd);
+  V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
+  if (t1) {
+    DREG(DREG_TEX)
+    const V3 tv = sky_img ? v3(u8_unit(px1 & 0xffu), u8_unit((px1 >> 8) & 0xffu), u8_unit((px1 >> 16) & 0xffu))
+                          : tex_value(S, tid1, h, px1);
+    if (ta) tex_ab = tv;
+    else tex_em = tv;
+  }
+  if (ta && te) tex_em = tex_sample(S, emit_tex, h);
+  const double* ecol = hit ? m->emit_color : S.background.color;
+  const V3 em = emit_eval(emit_kind, v3(ecol[0], ecol[1], ecol[2]), tex_em, d, h);
+  // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142), accumulated forward: each
+  // bounce's T (*) emit goes straight into the pixel sum (main.rs:80 adds the sample's total; the
+  // association differs in the last ulp only)
+  sum_x = sum_x + T_x * em.x;
+  sum_y = sum_y + T_y * em.y;
+  sum_z = sum_z + T_z * em.z;
+  if (hit && first) hits++;
+  if (scattered) {
+    const V3 ab = absorb_eval(*m, tex_ab);
+    T_x = T_x * ab.x;
+    T_y = T_y * ab.y;
+    T_z = T_z * ab.z;
+    o = h.p;
+    d = nd;
+  }
+  return scattered;
+}
+
+// ------------------------------------------------------------------ render kernel ----------------
+
+RPK_INLINE V3 matvec(const double* m, V3 v) {  // nalgebra Matrix3 * Vector3 (column axpy)
+  return v3((v.x * m[0] + v.y * m[3]) + v.z * m[6], (v.x * m[1] + v.y * m[4]) + v.z * m[7],
+            (v.x * m[2] + v.y * m[5]) + v.z * m[8]);
+}
+
+// All launch arguments in one kernarg struct.  The persistent loop re-reads the fields it needs through
+// a laundered pointer to the kernarg segment (scalar loads, served by the constant cache) instead of
+// keeping ~70 uniform values live in SGPRs for the whole kernel: that SGPR pressure otherwise spills
+// into VGPR lanes and halves the wave occupancy of this register-bound kernel.
+struct KArgs {
+  KScene S;
+  KParams P;
+  double* out;
+  float* out_fg;
+  unsigned long long* ctr;
+  unsigned int* queue;       // the unit queue's next index (workspace-owned, zeroed before the launch)
+  unsigned long long* diag;  // RPK_DIAG builds only (DIAG_N counters)
+};
+typedef const __attribute__((address_space(4))) KArgs* KArgsPtr;
+
+RPK_INLINE KScene load_scene(KArgsPtr A) {
+  KScene S;
+  S.nodes = A->S.nodes;
+  S.prims = A->S.prims;
+  S.prim_refs = A->S.prim_refs;
+  S.vnrm = A->S.vnrm;
+  S.vuv = A->S.vuv;
+  S.mats = A->S.mats;
+  S.texs = A->S.texs;
+  S.texels = A->S.texels;
+  S.background.kind = A->S.background.kind;
+  S.background.tex = A->S.background.tex;
+  S.background.needs_uv = A->S.background.needs_uv;
+  S.background.img_w = A->S.background.img_w;
+  S.background.img_h = A->S.background.img_h;
+  S.background.img_off = A->S.background.img_off;
+  S.background.color[0] = A->S.background.color[0];
+  S.background.color[1] = A->S.background.color[1];
+  S.background.color[2] = A->S.background.color[2];
+  S.root = A->S.root;
+  S.always_first = A->S.always_first;
+  S.n_always = A->S.n_always;
+  S.stack_depth = A->S.stack_depth;
+  S.lds_depth = A->S.lds_depth;
+  S.spill = A->S.spill;
+  S.rng_slab = A->S.rng_slab;
+  return S;
+}
+
+RPK_INLINE KArgsPtr kargs() {
+  KArgsPtr p = (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+// Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
+// tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
+// row-major; slots of edge tiles outside the frame are skipped.  Returns false when the queue is drained.
+template <bool PROBE>
+RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t& batch) {
+  KArgsPtr A = kargs();
+  unsigned int* queue = A->queue;
+  const uint32_t tw = A->P.tw, th = A->P.th;
+  if (PROBE && A->P.probe_n) {  // cost probe: an n x n lattice per tile (cell centres), clamped into the frame
+    slot = atomicAdd(queue, 1u);
+    if ((uint64_t)slot >= A->P.n_queue) return false;
+    batch = 0;
+    const uint32_t n = A->P.probe_n;
+    const uint32_t k = slot / A->P.probe_px, sub = slot % A->P.probe_px;
+    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
+    pi = min(tx * tw + min((sub % n) * tw / n + tw / (2u * n), tw - 1u), A->P.W - 1u);
+    pj = min(ty * th + min((sub / n) * th / n + th / (2u * n), th - 1u), A->P.H - 1u);
+    return true;
+  }
+  const uint32_t tile_px = tw * th, tile_units = tile_px * A->P.nbatch;
+  for (;;) {
+    const uint32_t q = atomicAdd(queue, 1u);
+    if ((uint64_t)q >= A->P.n_queue) return false;
+    uint32_t k = q / tile_units;
+    const uint32_t rem = q - k * tile_units;
+    batch = rem / tile_px;
+    const uint32_t local = rem - batch * tile_px;
+    if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
+    slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
+    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
+    pi = tx * tw + local % tw;
+    pj = ty * th + local / tw;
+    if (pi < A->P.W && pj < A->P.H) return true;
+  }
+}
+
+// RNG contract (include/rp.h): batch b of pixel (i, j) is its own StdRng stream,
+// seed_from_u64(seed + b * W * H + j * W + i); batch 0 is the per-pixel stream of the original contract.
+RPK_INLINE uint64_t unit_seed(KArgsPtr A, uint32_t pi, uint32_t pj, uint32_t batch) {
+  return A->P.seed + (uint64_t)batch * A->P.W * A->P.H + (uint64_t)pj * A->P.W + pi;
+}
+// Samples in this unit's batch.
+RPK_INLINE uint32_t unit_spp(KArgsPtr A, uint32_t batch) {
+  return min(A->P.spp_batch, A->P.spp - batch * A->P.spp_batch);
+}
+
+// One camera sample (main.rs:75-76): make_uv_jitter draws 2s, 2s+1 of a CLONE of the pixel-start
+// stream (render.rs:74-82) = keystream words 4s..4s+3 = block s/4 at offset 4(s%4); Camera::shoot
+// (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
+template <class R>
+RPK_INLINE void start_sample(R& rng, uint32_t s, uint32_t pi, uint32_t pj, V3& o, V3& d) {
+  DREG(DREG_START_SAMPLE)
+  KArgsPtr A = kargs();
+  const uint4 jw = rng_jitter(rng, s);
+  const uint32_t w0 = jw.x, w1 = jw.y, w2 = jw.z, w3 = jw.w;
+  const double ju = ((double)pi + words_f64(w0, w1)) / (double)A->P.W;
+  const double jv = ((double)pj + words_f64(w2, w3)) / (double)A->P.H;
+  double dx = 0.0, dy = 0.0;
+  // UnitDisk (randomness.rs:21-34): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
+  for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
+    ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
+    double tx[RPK_TRIES], ty[RPK_TRIES];
+#pragma unroll
+    for (int j = 0; j < RPK_TRIES; j++) {
+      tx[j] = ring_sym(rng, a + 4u * j);
+      ty[j] = ring_sym(rng, a + 4u * j + 2u);
+    }
+    bool done = false;
+#pragma unroll
+    for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+      const double qx = tx[j], qy = ty[j];
+      if (qx * qx + qy * qy < 1.0) { dx = qx; dy = qy; rng.pos = a + 4u * (j + 1); done = true; }
+    }
+    if (done) break;
+  }
+  A = kargs();
+  // tan(fov/2) is computed on the host (render.rs:33 is a per-camera constant; same libm as the reference)
+  const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
+  const V3 lo = v3(lens * dx, lens * dy, 0.0);
+  const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
+  double m[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
+  d = matvec(m, dl);
+  o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
+}
+
+}  // namespace rpk

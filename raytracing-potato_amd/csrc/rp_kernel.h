@@ -124,6 +124,20 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
 
+// Stage-split engine (rp_wavefront.hip): the path-slot pool of a workspace, structure-of-arrays in device
+// memory, and the host loop of trace / shade passes (synchronous: it polls the ray-queue length every
+// `poll` iterations through the pinned word host_count).
+struct WfBuffers {
+  double *ray, *tp, *sum, *hit;  // 6, 3, 3, 3 doubles per slot
+  int32_t* prim;                 // 1 per slot
+  uint32_t *st, *queue, *wc;     // 7 words per slot, 2 queues of P slot ids, 4 counters
+  uint32_t* host_count;          // pinned host word
+  uint32_t P, poll;
+};
+int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
+                     uint32_t* queue, const WfBuffers& b, int trace_grid, void* stream);
+int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
+
 // Closest-hit query kernel (one ray per thread).
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,
                      uint64_t* counters, void* stream);

@@ -27,6 +27,7 @@ RP_COUNTERS_LEN = 4  # device counter block: rays, samples, pixels, status (incl
 RP_SAMPLES_PER_STREAM = 32
 RP_COMM_ID_BYTES = 128
 RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
+RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 
 
 class rp_hittable(Structure):
@@ -84,7 +85,7 @@ class rp_scene_options(Structure):
     _fields_ = [("builder", c_uint32), ("max_leaf", c_uint32), ("cost_traverse", c_double),
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
-                ("reserved", c_uint32 * 4)]
+                ("engine", c_uint32), ("wf_slots", c_uint32), ("reserved", c_uint32 * 2)]
 
 
 class rp_stats(Structure):

@@ -16,12 +16,14 @@ from .scene import RenderParams, Scene, shard_slot_count
 def scene_options(**kw) -> F.rp_scene_options:
     """rp_scene_options with the library defaults (rp_scene_options_init), fields overridden by keyword:
     builder ("auto" | "host" | "gpu" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
-    self_check, trav_threshold, tile_order, probe_n."""
+    self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
         if k == "builder" and isinstance(v, str):
             v = {"auto": F.RP_BUILDER_AUTO, "host": F.RP_BUILDER_HOST, "gpu": F.RP_BUILDER_DEVICE}[v]
+        if k == "engine" and isinstance(v, str):
+            v = {"megakernel": F.RP_ENGINE_MEGAKERNEL, "wavefront": F.RP_ENGINE_WAVEFRONT}[v]
         if not hasattr(o, k) or k == "reserved":
             raise KeyError(f"unknown scene option {k!r}")
         setattr(o, k, v)
