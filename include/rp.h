@@ -203,7 +203,7 @@ typedef struct rp_scene_options {
   uint32_t tile_order;      /* 0 = cost-ordered tiles (probe launch + sort), 1 = plain shard order */
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
   uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
-  uint32_t wf_slots;        /* wavefront engine: path slots per resident lane (0 -> 4) */
+  uint32_t wf_slots;        /* wavefront engine: paths in flight per resident lane (0 -> 2) */
   uint32_t reserved[2];
 } rp_scene_options;
 

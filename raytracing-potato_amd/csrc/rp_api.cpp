@@ -154,7 +154,7 @@ namespace {
 
 void ws_release(rp_workspace* w) {
   for (void* p : {(void*)w->wf.ray, (void*)w->wf.tp, (void*)w->wf.sum, (void*)w->wf.hit, (void*)w->wf.prim,
-                  (void*)w->wf.st, (void*)w->wf.queue, (void*)w->wf.wc})
+                  (void*)w->wf.st, (void*)w->wf.wc})
     dfree(p);
   if (w->wf.host_count) (void)hipHostFree(w->wf.host_count);
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
@@ -187,8 +187,8 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
     }
     b.P = (uint32_t)P;
     b.poll = 8;
-    if (!dalloc(&b.ray, 6 * P) || !dalloc(&b.tp, 3 * P) || !dalloc(&b.sum, 3 * P) || !dalloc(&b.hit, 3 * P) ||
-        !dalloc(&b.prim, P) || !dalloc(&b.st, 7 * P) || !dalloc(&b.queue, 2 * P) || !dalloc(&b.wc, 4) ||
+    if (!dalloc(&b.ray, 2 * 6 * P) || !dalloc(&b.tp, 2 * 3 * P) || !dalloc(&b.sum, 2 * 3 * P) ||
+        !dalloc(&b.hit, 3 * P) || !dalloc(&b.prim, P) || !dalloc(&b.st, 2 * 7 * P) || !dalloc(&b.wc, 4) ||
         hipHostMalloc(reinterpret_cast<void**>(&b.host_count), sizeof(uint32_t)) != hipSuccess) {
       ws_release(w);
       return fail(RP_ENOMEM, "hipMalloc wavefront path slots");
@@ -267,7 +267,7 @@ rp_scene_options default_options() {
   o.tile_order = 0;
   o.probe_n = rpk::PROBE_LATTICE_N;
   o.engine = RP_ENGINE_MEGAKERNEL;
-  o.wf_slots = 4;
+  o.wf_slots = 2;
   return o;
 }
 

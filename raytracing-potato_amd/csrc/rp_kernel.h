@@ -128,9 +128,9 @@ int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
 // memory, and the host loop of trace / shade passes (synchronous: it polls the ray-queue length every
 // `poll` iterations through the pinned word host_count).
 struct WfBuffers {
-  double *ray, *tp, *sum, *hit;  // 6, 3, 3, 3 doubles per slot
-  int32_t* prim;                 // 1 per slot
-  uint32_t *st, *queue, *wc;     // 7 words per slot, 2 queues of P slot ids, 4 counters
+  double *ray, *tp, *sum, *hit;  // two state buffers of 6, 3, 3 doubles per path; hits 3 doubles per path
+  int32_t* prim;                 // 1 per path
+  uint32_t *st, *wc;             // two state buffers of 7 words per path, 4 counters
   uint32_t* host_count;          // pinned host word
   uint32_t P, poll;
 };

@@ -75,36 +75,38 @@ RPK_INLINE uint4 rng_jitter(WRng& r, uint32_t s) {
   return v;
 }
 
-// ---- slot state ---------------------------------------------------------------------------------------
-// st word layout (SoA, P entries each): ST_S sample index in the unit | FIRST_BIT, ST_DEPTH bounces left,
-// ST_POS keystream word (POS_NEW: the slot holds no unit yet), ST_PIPJ pixel i | j << 16, ST_BATCH, ST_SLOT
-// the unit's output slot, ST_HITS samples whose first ray hit.
+// ---- path state ---------------------------------------------------------------------------------------
+// The paths in flight are kept in QUEUE ORDER: a shade pass reads entry i of the input state and appends
+// the paths that go on to the output state at consecutive positions (wave-aggregated atomic), so every
+// state access of both passes is coalesced; the trace pass reads the ray of entry q and writes its hit at
+// q.  Two state buffers alternate.  st words (SoA, P entries each): ST_S sample index in the unit |
+// FIRST_BIT, ST_DEPTH bounces left, ST_POS keystream word (POS_NEW: the entry holds no unit yet), ST_PIPJ
+// pixel i | j << 16, ST_BATCH, ST_SLOT the unit's output slot, ST_HITS samples whose first ray hit.
 enum { ST_S = 0, ST_DEPTH, ST_POS, ST_PIPJ, ST_BATCH, ST_SLOT, ST_HITS, ST_N };
 static constexpr uint32_t FIRST_BIT = 0x80000000u, POS_NEW = 0xFFFFFFFFu;
 enum { WC_N0 = 0, WC_N1 = 1, WC_FETCH = 2, WC_N = 4 };
 
+struct WfState {
+  double* ray;  // 6 x P: o.x o.y o.z d.x d.y d.z
+  double* tp;   // 3 x P: path throughput
+  double* sum;  // 3 x P: the unit's sample sum
+  uint32_t* st; // ST_N x P
+};
 struct WfArgs {
-  double* ray;      // 6 x P: o.x o.y o.z d.x d.y d.z
-  double* tp;       // 3 x P: path throughput
-  double* sum;      // 3 x P: the unit's sample sum
-  double* hit;      // 3 x P: t, u, v of the closest hit
-  int32_t* prim;    // P: closest primitive (-1 = miss)
-  uint32_t* st;     // ST_N x P
-  uint32_t* queue;  // 2 x P: the two ray queues (slot ids)
-  uint32_t* wc;     // WC_N counters: queue lengths, the trace pass's fetch index
+  WfState in, out;  // the pass reads `in`, a shade pass appends to `out`
+  double* hit;      // 3 x P: t, u, v of the closest hit of input entry q
+  int32_t* prim;    // P: its primitive (-1 = miss)
+  uint32_t* wc;     // WC_N counters: the two state buffers' lengths, the trace pass's fetch index
   uint32_t P;
-  uint32_t in;      // queue this pass reads (0 / 1)
+  uint32_t nin;     // WC_N0 / WC_N1: the counter of `in` (the other one counts `out`)
 };
 
 __global__ void __launch_bounds__(256) wf_init_kernel(const WfArgs w) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i < w.P) {
-    w.st[ST_POS * (uint64_t)w.P + i] = POS_NEW;
-    w.queue[i] = i;
-  }
+  if (i < w.P) w.in.st[ST_POS * (uint64_t)w.P + i] = POS_NEW;
   if (i == 0) {
-    w.wc[WC_N0] = w.P;
-    w.wc[WC_N1] = 0;
+    w.wc[w.nin] = w.P;
+    w.wc[w.nin ^ 1u] = 0;
     w.wc[WC_FETCH] = 0;
   }
 }
@@ -114,21 +116,19 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
   __shared__ uint32_t ring[32 * BLOCK];
   const uint32_t tid = threadIdx.x;
   const uint32_t i = blockIdx.x * BLOCK + tid;
-  const uint32_t out = w.in ^ 1u;
   if (blockIdx.x == 0 && tid == 0) w.wc[WC_FETCH] = 0;  // the next trace pass fetches from its start
-  const uint32_t n = w.wc[w.in];
+  const uint32_t n = w.wc[w.nin];
   const bool live = i < n;
   const uint64_t P = w.P;
-  uint32_t slot = live ? w.queue[w.in * P + i] : 0u;
   uint32_t s = 0, depth = 0, pos = POS_NEW, pipj = 0, batch = 0, oslot = 0, hits = 0;
   if (live) {
-    s = w.st[ST_S * P + slot];
-    depth = w.st[ST_DEPTH * P + slot];
-    pos = w.st[ST_POS * P + slot];
-    pipj = w.st[ST_PIPJ * P + slot];
-    batch = w.st[ST_BATCH * P + slot];
-    oslot = w.st[ST_SLOT * P + slot];
-    hits = w.st[ST_HITS * P + slot];
+    s = w.in.st[ST_S * P + i];
+    depth = w.in.st[ST_DEPTH * P + i];
+    pos = w.in.st[ST_POS * P + i];
+    pipj = w.in.st[ST_PIPJ * P + i];
+    batch = w.in.st[ST_BATCH * P + i];
+    oslot = w.in.st[ST_SLOT * P + i];
+    hits = w.in.st[ST_HITS * P + i];
   }
   KArgsPtr A = kargs();
   WRng rng;
@@ -141,19 +141,19 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
     seed_key(unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch), rng.key);
     rng.pos = pos;
     rng.end = pos >> 4;
-    o = v3(w.ray[slot], w.ray[P + slot], w.ray[2 * P + slot]);
-    d = v3(w.ray[3 * P + slot], w.ray[4 * P + slot], w.ray[5 * P + slot]);
-    tx = w.tp[slot];
-    ty = w.tp[P + slot];
-    tz = w.tp[2 * P + slot];
-    sx = w.sum[slot];
-    sy = w.sum[P + slot];
-    sz = w.sum[2 * P + slot];
+    o = v3(w.in.ray[i], w.in.ray[P + i], w.in.ray[2 * P + i]);
+    d = v3(w.in.ray[3 * P + i], w.in.ray[4 * P + i], w.in.ray[5 * P + i]);
+    tx = w.in.tp[i];
+    ty = w.in.tp[P + i];
+    tz = w.in.tp[2 * P + i];
+    sx = w.in.sum[i];
+    sy = w.in.sum[P + i];
+    sz = w.in.sum[2 * P + i];
     HitRec hr;
-    hr.t = w.hit[slot];
-    hr.u = w.hit[P + slot];
-    hr.v = w.hit[2 * P + slot];
-    hr.prim = w.prim[slot];
+    hr.t = w.hit[i];
+    hr.u = w.hit[P + i];
+    hr.v = w.hit[2 * P + i];
+    hr.prim = w.prim[i];
     const bool first = (s & FIRST_BIT) != 0u;
     s &= ~FIRST_BIT;
     const KScene S = load_scene(A);
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
       }
     }
   }
-  if (fetch) {  // the slot's next unit (pixel, sample batch) from the frame's queue
+  if (fetch) {  // the path's next unit (pixel, sample batch) from the frame's queue; none left: it ends
     uint32_t pi = 0, pj = 0;
     if (fetch_pixel<false>(oslot, pi, pj, batch)) {
       pipj = pi | (pj << 16);
@@ -203,8 +203,6 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
       rng.pos = 0;
       rng.end = 0;
       start = true;
-    } else {
-      pos = POS_NEW;  // no unit left: the slot goes idle (not queued)
     }
   }
   if (start) {  // camera sample s of the unit (main.rs:75-76): jitter + Camera::shoot
@@ -215,29 +213,26 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
     append = true;
   }
   if (append) {
-    const uint32_t k = atomicAdd(&w.wc[out], 1u);
-    w.queue[out * P + k] = slot;
-    w.ray[slot] = o.x;
-    w.ray[P + slot] = o.y;
-    w.ray[2 * P + slot] = o.z;
-    w.ray[3 * P + slot] = d.x;
-    w.ray[4 * P + slot] = d.y;
-    w.ray[5 * P + slot] = d.z;
-    w.tp[slot] = tx;
-    w.tp[P + slot] = ty;
-    w.tp[2 * P + slot] = tz;
-    w.sum[slot] = sx;
-    w.sum[P + slot] = sy;
-    w.sum[2 * P + slot] = sz;
-    w.st[ST_S * P + slot] = s;
-    w.st[ST_DEPTH * P + slot] = depth;
-    w.st[ST_POS * P + slot] = rng.pos;
-    w.st[ST_PIPJ * P + slot] = pipj;
-    w.st[ST_BATCH * P + slot] = batch;
-    w.st[ST_SLOT * P + slot] = oslot;
-    w.st[ST_HITS * P + slot] = hits;
-  } else if (live && pos == POS_NEW) {
-    w.st[ST_POS * P + slot] = POS_NEW;
+    const uint32_t k = atomicAdd(&w.wc[w.nin ^ 1u], 1u);
+    w.out.ray[k] = o.x;
+    w.out.ray[P + k] = o.y;
+    w.out.ray[2 * P + k] = o.z;
+    w.out.ray[3 * P + k] = d.x;
+    w.out.ray[4 * P + k] = d.y;
+    w.out.ray[5 * P + k] = d.z;
+    w.out.tp[k] = tx;
+    w.out.tp[P + k] = ty;
+    w.out.tp[2 * P + k] = tz;
+    w.out.sum[k] = sx;
+    w.out.sum[P + k] = sy;
+    w.out.sum[2 * P + k] = sz;
+    w.out.st[ST_S * P + k] = s;
+    w.out.st[ST_DEPTH * P + k] = depth;
+    w.out.st[ST_POS * P + k] = rng.pos;
+    w.out.st[ST_PIPJ * P + k] = pipj;
+    w.out.st[ST_BATCH * P + k] = batch;
+    w.out.st[ST_SLOT * P + k] = oslot;
+    w.out.st[ST_HITS * P + k] = hits;
   }
   // per-wave counts (ballot popcounts) into the frame's counters
   const uint64_t n_rays = (uint64_t)__popcll(__ballot(traced));
@@ -252,8 +247,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
 }
 
 // ---- trace pass ---------------------------------------------------------------------------------------
-// Persistent: every lane takes the next queued slot as soon as its ray is done.  A wave refills its idle
-// lanes when at least WF_REFILL of them wait (the ray setup runs with many lanes) or when none traverse.
+// Persistent: every lane takes the next queued ray as soon as its ray is done.  A wave refills its idle
+// lanes when at least RPK_WF_REFILL of them wait (the ray setup runs with many lanes) or when none
+// traverse; the refilling lanes get consecutive entries (wave-aggregated atomic), so the ray loads coalesce.
 #ifndef RPK_WF_REFILL
 #define RPK_WF_REFILL 16
 #endif
@@ -262,11 +258,11 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
   extern __shared__ uint32_t lds_stack[];
   lds_u32* stk = (lds_u32*)(lds_stack + threadIdx.x);
   const uint32_t tid = threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) w.wc[w.in ^ 1u] = 0;  // the next shade pass appends from 0
-  const uint32_t n = w.wc[w.in];
+  if (blockIdx.x == 0 && tid == 0) w.wc[w.nin ^ 1u] = 0;  // the next shade pass appends from 0
+  const uint32_t n = w.wc[w.nin];
   const uint64_t P = w.P;
   bool have = false, drained = false, overflow = false;
-  uint32_t slot = 0;
+  uint32_t q = 0;
   V3 o = v3(0.0, 0.0, 0.0), d = v3(0.0, 0.0, 1.0);
   Ray32 r;
   TravState ts;
@@ -280,11 +276,10 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
     const uint64_t idle = __ballot(!have);
     if (!drained && idle != 0 && ((uint32_t)__popcll(idle) >= RPK_WF_REFILL || __ballot(have) == 0)) {
       if (!have) {
-        const uint32_t q = atomicAdd(&w.wc[WC_FETCH], 1u);
+        q = atomicAdd(&w.wc[WC_FETCH], 1u);
         if (q < n) {
-          slot = w.queue[w.in * P + q];
-          o = v3(w.ray[slot], w.ray[P + slot], w.ray[2 * P + slot]);
-          d = v3(w.ray[3 * P + slot], w.ray[4 * P + slot], w.ray[5 * P + slot]);
+          o = v3(w.in.ray[q], w.in.ray[P + q], w.in.ray[2 * P + q]);
+          d = v3(w.in.ray[3 * P + q], w.in.ray[4 * P + q], w.in.ray[5 * P + q]);
           const KScene S = load_scene(kargs());
           setup_ray32(o, d, RAY_EPSILON, r);
           trav_init(S, INF, ts);
@@ -304,10 +299,10 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
       const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + tid) * (S.stack_depth - S.lds_depth) : 0u;
       trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
       if (trav_done(ts)) {
-        w.hit[slot] = ts.best;
-        w.hit[P + slot] = ts.bu;
-        w.hit[2 * P + slot] = ts.bv;
-        w.prim[slot] = ts.bestp;
+        w.hit[q] = ts.best;
+        w.hit[P + q] = ts.bu;
+        w.hit[2 * P + q] = ts.bv;
+        w.prim[q] = ts.bestp;
         have = false;
       }
     }
@@ -327,30 +322,38 @@ int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* 
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
   a.queue = queue;
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
+  WfState sb[2];
+  for (int k = 0; k < 2; k++) {
+    sb[k].ray = b.ray + (uint64_t)k * 6 * b.P;
+    sb[k].tp = b.tp + (uint64_t)k * 3 * b.P;
+    sb[k].sum = b.sum + (uint64_t)k * 3 * b.P;
+    sb[k].st = b.st + (uint64_t)k * ST_N * b.P;
+  }
   WfArgs w;
-  w.ray = b.ray;
-  w.tp = b.tp;
-  w.sum = b.sum;
   w.hit = b.hit;
   w.prim = b.prim;
-  w.st = b.st;
-  w.queue = b.queue;
   w.wc = b.wc;
   w.P = b.P;
-  w.in = 0;
+  uint32_t cur = 0;  // the state buffer holding the paths to shade / trace next
+  auto set = [&](uint32_t c) {
+    w.in = sb[c];
+    w.out = sb[c ^ 1u];
+    w.nin = c;
+  };
+  set(cur);
   const unsigned sgrid = (unsigned)((b.P + BLOCK - 1) / BLOCK);
   hipLaunchKernelGGL(wf_init_kernel, dim3(sgrid), dim3(256), 0, st, w);
-  hipLaunchKernelGGL(wf_shade_kernel, dim3(sgrid), dim3(BLOCK), 0, st, a, w);  // slots fetch their first units
+  hipLaunchKernelGGL(wf_shade_kernel, dim3(sgrid), dim3(BLOCK), 0, st, a, w);  // paths fetch their first units
+  cur ^= 1u;
   const size_t lds = (size_t)s.lds_depth * BLOCK * sizeof(uint32_t);
   const bool spill = s.lds_depth < s.stack_depth;
-  uint32_t cur = 1;
   uint32_t* h_n = b.host_count;
-  // every iteration advances each queued path by one ray, and a slot's units run back to back: a frame
-  // needs at most (units per slot + 1) x samples per unit x (max_bounce + 1) iterations (a safety bound)
+  // every iteration advances each queued path by one ray, and a path's units run back to back: a frame
+  // needs at most (units per path + 2) x samples per unit x (max_bounce + 1) iterations (a safety bound)
   const uint64_t bound = (p.n_queue / b.P + 2) * (uint64_t)p.spp_batch * (p.max_bounce + 1) + 64;
   for (uint32_t it = 1;; it++) {
     if (it > bound) return (int)hipErrorUnknown;
-    w.in = cur;
+    set(cur);
     if (spill) hipLaunchKernelGGL(wf_trace_kernel<true>, dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
     else hipLaunchKernelGGL(wf_trace_kernel<false>, dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
     hipLaunchKernelGGL(wf_shade_kernel, dim3(sgrid), dim3(BLOCK), 0, st, a, w);
