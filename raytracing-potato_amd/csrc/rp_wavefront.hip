@@ -29,13 +29,17 @@ struct WRng {
   uint32_t end;     // one past the newest block held
 };
 
-RPK_INLINE void wr_gen(WRng& r, uint32_t b) {
-  uint32_t w[16];
-  chacha12(r.key, b, w);
-  lds_u32* dst = r.ring + (b & 1u) * 16u * BLOCK;
+// Out of line: every draw site would otherwise inline a 2.5 KB ChaCha12 (instruction-cache pressure).
+static __device__ __attribute__((noinline)) void wr_block(const uint32_t* key, uint32_t b, lds_u32* ring) {
+  uint32_t k[8], w[16];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = key[i];
+  chacha12(k, b, w);
+  lds_u32* dst = ring + (b & 1u) * 16u * BLOCK;
 #pragma unroll
   for (int i = 0; i < 16; i++) dst[i * BLOCK] = w[i];
 }
+RPK_INLINE void wr_gen(WRng& r, uint32_t b) { wr_block(r.key, b, r.ring); }
 // every block up to last_blk is made (the draw sites ensure the blocks of the words they read; a try
 // spans at most two consecutive blocks, the window)
 RPK_INLINE void ring_ensure(WRng& r, uint32_t last_blk) {
