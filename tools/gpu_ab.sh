@@ -30,14 +30,5 @@ for cfg in ${CONFIGS:-C3}; do
       > gpurun_out/${TAG}_${cfg}_pmc_sq.json 2> gpurun_out/${TAG}_${cfg}_pmc_sq.err || { ok=1; break; }
   fi
 done
-if [ $ok = 0 ] && [ -n "$PCSAMP" ]; then
-  echo pcsamp >> $P
-  timeout -k 10 60 rocprofv3 --help > gpurun_out/${TAG}_rocprof_help.txt 2>&1 || true
-  timeout -s KILL 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method ${PCSAMP} --pc-sampling-unit ${PCUNIT:-time} \
-    --pc-sampling-interval ${PCINT:-1000} -d gpurun_out/${TAG}_pcs -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --spp ${PCSPP:-64} --no-cpu-baseline \
-    > gpurun_out/${TAG}_pcs.json 2> gpurun_out/${TAG}_pcs.err
-  echo "pcsamp rc $?" >> $P
-fi
 echo "done $ok" >> $P
 exit $ok
