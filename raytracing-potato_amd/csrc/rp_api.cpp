@@ -377,6 +377,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
     ps.root = 0;
     ps.max_depth = gt.max_depth;
     ps.n_leaves = gt.n_leaves;
+    ps.qbound = gt.qbound;
     n_tree_nodes = gt.n_nodes;
     n_tree_prims = pin.prims.size();
     if (opt.self_check) {
@@ -391,6 +392,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
       chk.root = 0;
       chk.max_depth = gt.max_depth;
       chk.n_leaves = gt.n_leaves;
+      chk.qbound = gt.qbound;
       if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
     }
   } else if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
@@ -416,6 +418,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->ks.root = ps.root;
   s->ks.always_first = ps.always_first;  // 0 / 0 for a device-built tree
   s->ks.n_always = ps.n_always;
+  s->ks.qbound = ps.qbound;
   // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
   // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;

@@ -2,6 +2,7 @@
 #include "rp_bvh.h"
 
 #include <algorithm>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -156,16 +157,13 @@ struct Builder {
   }
 };
 
-// f64 -> f32 rounded towards -inf / +inf (conservative box bounds)
-float down32(double x) {
-  float f = (float)x;
-  if ((double)f > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-  return f;
-}
-float up32(double x) {
-  float f = (float)x;
-  if ((double)f < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
-  return f;
+// The quantization frame of a wide node from its exact box (rp_layout.h qframe); an axis without a finite
+// extent (NaN geometry only) gets the frame at 0.
+void node_frame(const Box& b, rpl::Node4& n) {
+  for (int a = 0; a < 3; a++) {
+    const bool ok = std::isfinite(b.lo[a]) && std::isfinite(b.hi[a]) && b.lo[a] <= b.hi[a];
+    rpl::qframe(ok ? b.lo[a] : 0.0, ok ? b.hi[a] : 0.0, n.o[a], n.s[a]);
+  }
 }
 
 // Collapse the binary tree into 4-wide nodes: each wide node takes its binary node's two children and
@@ -196,19 +194,22 @@ struct Collapser {
       }
     }
     uint32_t entries[4];
-    for (int c = 0; c < 4; c++) {
+    {
       rpl::Node4& n = out[self];
-      if ((size_t)c >= kids.size()) {
-        n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = std::numeric_limits<float>::infinity();
-        n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = -std::numeric_limits<float>::infinity();
-        entries[c] = rpl::ENTRY_EMPTY;
-        continue;
+      Box nb;
+      nb.reset();
+      for (int32_t k : kids) nb.grow(bin[k].box);
+      node_frame(nb, n);
+      for (int c = 0; c < 4; c++) {
+        if ((size_t)c >= kids.size()) {
+          rpl::empty_child(n, c);
+          entries[c] = rpl::ENTRY_EMPTY;
+          continue;
+        }
+        const BinNode& k = bin[kids[c]];
+        rpl::quantize_child(n, c, k.box.lo, k.box.hi);
+        entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
       }
-      const BinNode& k = bin[kids[c]];
-      n.lo_x[c] = down32(k.box.lo[0]); n.hi_x[c] = up32(k.box.hi[0]);
-      n.lo_y[c] = down32(k.box.lo[1]); n.hi_y[c] = up32(k.box.hi[1]);
-      n.lo_z[c] = down32(k.box.lo[2]); n.hi_z[c] = up32(k.box.hi[2]);
-      entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
     }
     for (int c = 0; c < 4; c++)
       if ((size_t)c < kids.size() && !bin[kids[c]].leaf()) entries[c] = emit(kids[c], depth + 1);
@@ -435,6 +436,14 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     }
   }
   const uint32_t n_tree = (uint32_t)refs.size();
+  double amax = 0.0;
+  for (const Ref& r : refs)
+    for (int k = 0; k < 3; k++) amax = std::fmax(amax, std::fmax(std::fabs(r.box.lo[k]), std::fabs(r.box.hi[k])));
+  if (!(amax <= rpl::COORD_MAX)) {
+    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized tree";
+    return RP_EINVAL;
+  }
+  out.qbound = rpl::qbound(amax);
   std::vector<uint32_t> order;
   order.reserve(n);
   std::vector<BinNode> bin;
@@ -442,9 +451,9 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   Builder B{opt, refs, bin, order};
   if (n_tree == 0) {
     rpl::Node4 root{};
+    for (int a = 0; a < 3; a++) rpl::qframe(0.0, 0.0, root.o[a], root.s[a]);
     for (int c = 0; c < 4; c++) {
-      root.lo_x[c] = root.lo_y[c] = root.lo_z[c] = std::numeric_limits<float>::infinity();
-      root.hi_x[c] = root.hi_y[c] = root.hi_z[c] = -std::numeric_limits<float>::infinity();
+      rpl::empty_child(root, c);
       root.child[c] = rpl::ENTRY_EMPTY;
     }
     out.nodes.push_back(root);
@@ -545,78 +554,92 @@ int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err) {
     out.cmin[k] = std::numeric_limits<double>::infinity();
     out.cmax[k] = -std::numeric_limits<double>::infinity();
   }
+  out.amax = 0.0;
   for (uint32_t i = 0; i < n; i++) {
     pack_prim(d, vbase, i, out.prims[i], out.refs[i]);
     const Box b = hittable_box(d, d->hittables[i]);
     for (int k = 0; k < 3; k++) {
       out.boxes[6 * (size_t)i + k] = b.lo[k];
       out.boxes[6 * (size_t)i + 3 + k] = b.hi[k];
+      out.amax = std::fmax(out.amax, std::fmax(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
       const double c = 0.5 * (b.lo[k] + b.hi[k]);
       out.cmin[k] = std::fmin(out.cmin[k], c);
       out.cmax[k] = std::fmax(out.cmax[k], c);
     }
   }
+  if (!(out.amax <= rpl::COORD_MAX)) {
+    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized tree";
+    return RP_EINVAL;
+  }
   return RP_OK;
 }
 
 int check(const PackedScene& s, std::string& err) {
-  // Every primitive referenced exactly once; every f32 child box contains its subtree (exact f64
-  // primitive boxes); the tree is acyclic and no deeper than max_depth.
+  // Every primitive referenced exactly once; every node frame exact and inside qbound (rp_layout.h); every
+  // quantized child box contains its subtree's exact f64 primitive boxes; acyclic, no deeper than max_depth.
   std::vector<uint8_t> used(s.prims.size(), 0);
   std::vector<uint8_t> visited(s.nodes.size(), 0);
   size_t np = 0;
-  auto prim_box = [&](const rpl::Prim& p, double lo[3], double hi[3]) {
+  auto prim_box = [&](const rpl::Prim& p, Box& b) {
     if (p.kind == rpl::PRIM_SPHERE) {
-      for (int q = 0; q < 3; q++) { lo[q] = p.g[q] - p.g[3]; hi[q] = p.g[q] + p.g[3]; }
+      for (int q = 0; q < 3; q++) { b.lo[q] = p.g[q] - p.g[3]; b.hi[q] = p.g[q] + p.g[3]; }
     } else {
       for (int q = 0; q < 3; q++) {
-        // b = a - (a - b) up to one rounding: widen by an ulp-scale slack for the check only
-        double a = p.g[q], b = a - p.g[3 + q], c = a - p.g[6 + q];
+        // b = a - (a - b) up to one rounding: shrink by an ulp-scale slack for the check only
+        double a = p.g[q], bq = a - p.g[3 + q], c = a - p.g[6 + q];
         double slack = 4.0 * std::numeric_limits<double>::epsilon() * (std::fabs(a) + std::fabs(p.g[3 + q]) + std::fabs(p.g[6 + q]));
-        lo[q] = std::fmin(std::fmin(a, b), c) + slack;
-        hi[q] = std::fmax(std::fmax(a, b), c) - slack;
+        b.lo[q] = std::fmin(std::fmin(a, bq), c) + slack;
+        b.hi[q] = std::fmax(std::fmax(a, bq), c) - slack;
       }
     }
   };
-  // returns false on error; accumulates the subtree box
-  struct Item { uint32_t entry; uint32_t depth; int parent; int slot; };
-  std::vector<Item> st{{s.root, 0, -1, -1}};
-  while (!st.empty()) {
-    Item it = st.back();
-    st.pop_back();
-    const rpl::Node4* parent = it.parent >= 0 ? &s.nodes[(size_t)it.parent] : nullptr;
-    auto inside = [&](const double lo[3], const double hi[3]) {
-      if (!parent) return true;
-      int c = it.slot;
-      return lo[0] >= parent->lo_x[c] && lo[1] >= parent->lo_y[c] && lo[2] >= parent->lo_z[c] &&
-             hi[0] <= parent->hi_x[c] && hi[1] <= parent->hi_y[c] && hi[2] <= parent->hi_z[c];
-    };
-    if (it.entry & rpl::ENTRY_LEAF) {
-      uint32_t first = it.entry & rpl::LEAF_FIRST_MASK, cnt = ((it.entry >> rpl::LEAF_SHIFT) & 7u) + 1;
+  if (!(s.qbound > 0.0)) { err = "qbound not set"; return RP_EINTERNAL; }
+  // subtree box of `entry` into `out`; false (err set) on the first violation
+  std::function<bool(uint32_t, uint32_t, Box&)> walk = [&](uint32_t entry, uint32_t depth, Box& out) -> bool {
+    out.reset();
+    if (entry & rpl::ENTRY_LEAF) {
+      uint32_t first = entry & rpl::LEAF_FIRST_MASK, cnt = ((entry >> rpl::LEAF_SHIFT) & 7u) + 1;
       for (uint32_t k = first; k < first + cnt; k++) {
-        if (k >= s.prims.size() || used[k]) { err = "primitive referenced twice or out of range"; return RP_EINTERNAL; }
+        if (k >= s.prims.size() || used[k]) { err = "primitive referenced twice or out of range"; return false; }
         used[k] = 1;
         np++;
-        double lo[3], hi[3];
-        prim_box(s.prims[k], lo, hi);
-        if (!inside(lo, hi)) { err = "primitive outside its leaf box"; return RP_EINTERNAL; }
+        Box b;
+        prim_box(s.prims[k], b);
+        out.grow(b);
       }
-      continue;
+      return true;
     }
-    if (it.entry >= s.nodes.size()) { err = "node index out of range"; return RP_EINTERNAL; }
-    if (visited[it.entry]) { err = "node visited twice"; return RP_EINTERNAL; }
-    visited[it.entry] = 1;
-    if (it.depth > s.max_depth) { err = "depth exceeds max_depth"; return RP_EINTERNAL; }
-    const rpl::Node4& n = s.nodes[it.entry];
+    if (entry >= s.nodes.size()) { err = "node index out of range"; return false; }
+    if (visited[entry]) { err = "node visited twice"; return false; }
+    visited[entry] = 1;
+    if (depth > s.max_depth) { err = "depth exceeds max_depth"; return false; }
+    const rpl::Node4& n = s.nodes[entry];
+    for (int a = 0; a < 3; a++) {
+      if (!(n.s[a] >= 0x1p-60f) || !std::isfinite(n.o[a]) || !(std::fabs((double)n.o[a]) <= s.qbound) ||
+          !(255.0 * (double)n.s[a] <= s.qbound)) {
+        err = "node frame outside qbound";
+        return false;
+      }
+    }
+    const uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
+    const uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
     for (int c = 0; c < 4; c++) {
       if (n.child[c] == rpl::ENTRY_EMPTY) continue;
-      if (parent) {
-        const double lo[3] = {n.lo_x[c], n.lo_y[c], n.lo_z[c]}, hi[3] = {n.hi_x[c], n.hi_y[c], n.hi_z[c]};
-        (void)lo; (void)hi;  // child boxes are built from exact f64 subtree boxes, checked at the leaves
+      Box sub;
+      if (!walk(n.child[c], depth + 1, sub)) return false;
+      for (int a = 0; a < 3; a++) {
+        if (!(sub.lo[a] <= sub.hi[a])) continue;  // nothing finite below on this axis
+        if (!(rpl::plane_q(n.o[a], n.s[a], L[a][c]) <= sub.lo[a]) || !(rpl::plane_q(n.o[a], n.s[a], H[a][c]) >= sub.hi[a])) {
+          err = "quantized child box does not contain its subtree";
+          return false;
+        }
       }
-      st.push_back({n.child[c], it.depth + 1, (int)it.entry, c});
+      out.grow(sub);
     }
-  }
+    return true;
+  };
+  Box all;
+  if (!walk(s.root, 0, all)) return RP_EINTERNAL;
   size_t expect = s.prims.size() - s.n_always;  // the always-tested tail is outside the tree
   if (np != expect && !(np == 0 && s.prims.size() == 1)) {
     err = "primitive count mismatch";

@@ -43,6 +43,7 @@ struct PackedScene {
   uint32_t max_depth = 0;             // deepest wide node (root = 0)
   uint32_t always_first = 0, n_always = 0;  // prims[always_first, +n_always): outside the tree, tested first
   uint64_t n_leaves = 0;
+  double qbound = 0.0;  // rp_layout.h qbound: >= |o| and 255 s of every node frame
 };
 
 // Checks every index the reference would bounds-check (or loop on).  Returns RP_OK or RP_EINVAL.
@@ -58,6 +59,7 @@ struct PrimInput {
   std::vector<rpl::PrimRef> refs;
   std::vector<double> boxes;  // 6 per primitive
   double cmin[3], cmax[3];
+  double amax;                // largest |coordinate| of the boxes (NaN ignored)
 };
 int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err);
 
@@ -76,6 +78,7 @@ struct GpuTree {
   rpl::PrimRef* d_prim_refs = nullptr;
   uint64_t n_nodes = 0, n_leaves = 0;
   uint32_t max_depth = 0;
+  double qbound = 0.0;
 };
 
 // LBVH (Karras 2012) + wide collapse on the current device.  Needs >= 2 primitives.

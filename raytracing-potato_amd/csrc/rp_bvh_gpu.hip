@@ -196,24 +196,34 @@ __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur
     kids[best] = left[open];
     kids[nk++] = right[open];
   }
+  Box6 kb[4];
+  Box6 nb;
+  for (int a = 0; a < 3; a++) {
+    nb.lo[a] = __builtin_huge_val();
+    nb.hi[a] = -__builtin_huge_val();
+  }
+  for (uint32_t k = 0; k < nk; k++) {
+    const uint32_t c = kids[k];
+    kb[k] = (c & BIN_LEAF) ? leaf_boxes[order[c & ~BIN_LEAF]] : node_boxes[c];
+    for (int a = 0; a < 3; a++) {
+      nb.lo[a] = fmin(nb.lo[a], kb[k].lo[a]);
+      nb.hi[a] = fmax(nb.hi[a], kb[k].hi[a]);
+    }
+  }
+  // quantization frame of the wide node (rp_layout.h qframe; rp_bvh.cpp node_frame)
   rpl::Node4 nd;
+  for (int a = 0; a < 3; a++) {
+    const bool ok = isfinite(nb.lo[a]) && isfinite(nb.hi[a]) && nb.lo[a] <= nb.hi[a];
+    rpl::qframe(ok ? nb.lo[a] : 0.0, ok ? nb.hi[a] : 0.0, nd.o[a], nd.s[a]);
+  }
   for (uint32_t k = 0; k < 4; k++) {
-    nd.pad[k] = 0;
     if (k >= nk) {
-      nd.lo_x[k] = nd.lo_y[k] = nd.lo_z[k] = __builtin_huge_valf();
-      nd.hi_x[k] = nd.hi_y[k] = nd.hi_z[k] = -__builtin_huge_valf();
+      rpl::empty_child(nd, (int)k);
       nd.child[k] = rpl::ENTRY_EMPTY;
       continue;
     }
     const uint32_t c = kids[k];
-    const Box6 b = (c & BIN_LEAF) ? leaf_boxes[order[c & ~BIN_LEAF]] : node_boxes[c];
-    // f64 -> f32 rounded outward (conservative child boxes, rp_layout.h)
-    nd.lo_x[k] = __double2float_rd(b.lo[0]);
-    nd.hi_x[k] = __double2float_ru(b.hi[0]);
-    nd.lo_y[k] = __double2float_rd(b.lo[1]);
-    nd.hi_y[k] = __double2float_ru(b.hi[1]);
-    nd.lo_z[k] = __double2float_rd(b.lo[2]);
-    nd.hi_z[k] = __double2float_ru(b.hi[2]);
+    rpl::quantize_child(nd, (int)k, kb[k].lo, kb[k].hi);
     const uint32_t cnt = bin_count(c, first, last);
     if (cnt <= max_leaf) {
       const uint32_t lo = (c & BIN_LEAF) ? (c & ~BIN_LEAF) : first[c];
@@ -372,6 +382,7 @@ int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::st
     std::swap(d_fa, d_fb);
   }
   out.max_depth = depth;
+  out.qbound = rpl::qbound(in.amax);
   hipLaunchKernelGGL(permute_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_order, d_prims_in, d_refs_in,
                      out.d_prims, out.d_prim_refs);
   RPG_CHECK("permute");

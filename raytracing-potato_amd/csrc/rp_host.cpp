@@ -412,8 +412,9 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba) {
 }
 
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray) {
-  // CPU model of rp_kernel.hip's traversal over the same packed 4-wide tree: conservative f32 child
-  // box tests (fma form + slack, rcp emulated by a correctly rounded 1/x), near-first order, exact f64
+  // CPU model of rp_device.h's traversal over the same packed 4-wide tree: quantized child boxes tested
+  // in f32 (t = fma(q, s inv, fma(o, inv, -oinv)) + slack, rcp emulated by a correctly rounded 1/x, the
+  // min/max slab form instead of the device's octant selection: the same values), near-first order, exact f64
   // primitive tests.  per_ray: n x 3 {wide nodes visited, primitive tests, closest hittable id or
   // 2^64-1}.  tests/test_bvh.py checks the closest hits against brute force.
   std::string err;
@@ -435,9 +436,12 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
       inv[k] = std::fmin(std::fmax(1.0f / (float)d[k], -0x1p64f), 0x1p64f);
       oinv[k] = o32 * inv[k];
       const double e = std::fabs(o[k] - (double)o32);
-      D = std::fmax(D, (e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv[k]) * 0x1p-23);
+      D = std::fmax(D, (e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv[k]) * 0x1p-23 +
+                           ((std::fabs(inv[k]) == 0x1p64f && o32 == 0.0f)
+                                ? 0.0
+                                : std::fabs((double)inv[k]) * (2.0 * ps.qbound + std::fabs((double)o32)) * 0x1p-23 * (1.0 + 0x1p-20)));
     }
-    const float slack = up(3.0 * D * (1.0 + 0x1p-20) + 0x1p-126), tmin32 = down(tmin);
+    const float slack = up(3.0 * D * (1.0 + 0x1p-20) + 0x1p-100), tmin32 = down(tmin);
     double best = q[7];
     float best32 = up(best);
     int64_t bestp = -1;
@@ -491,11 +495,17 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
         const rpl::Node4& nd = ps.nodes[cur];
         float tn[4];
         uint32_t cc[4];
+        float A[3], B[3];
+        for (int k = 0; k < 3; k++) {
+          A[k] = nd.s[k] * inv[k];
+          B[k] = std::fma(nd.o[k], inv[k], -oinv[k]);
+        }
         for (int c = 0; c < 4; c++) {
-          const float lo[3] = {nd.lo_x[c], nd.lo_y[c], nd.lo_z[c]}, hi[3] = {nd.hi_x[c], nd.hi_y[c], nd.hi_z[c]};
+          const float lo[3] = {(float)nd.lo_x[c], (float)nd.lo_y[c], (float)nd.lo_z[c]};
+          const float hi[3] = {(float)nd.hi_x[c], (float)nd.hi_y[c], (float)nd.hi_z[c]};
           float tnear = tmin32, tfar = best32;
           for (int k = 0; k < 3; k++) {
-            const float a = std::fma(lo[k], inv[k], -oinv[k]), b = std::fma(hi[k], inv[k], -oinv[k]);
+            const float a = std::fma(lo[k], A[k], B[k]), b = std::fma(hi[k], A[k], B[k]);
             tnear = std::fmax(tnear, std::fmin(a, b));
             tfar = std::fmin(tfar, std::fmax(a, b));
           }

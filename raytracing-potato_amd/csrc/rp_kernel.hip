@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         newray = false;
       }
       Ray32 r;
-      setup_ray32(o, d, RAY_EPSILON, r);
+      setup_ray32(o, d, RAY_EPSILON, S.qbound, r);
       for (;;) {
         if (alive && !tdone) {
           DREG(DREG_STEP)

@@ -3,29 +3,110 @@
 //
 // Layout rationale (DESIGN.md "Data layout in HBM"): traversal is one ray per lane, so neighbouring
 // lanes read unrelated nodes; what matters is that one lane's node fetch is a few wide (16 B) loads
-// from one 128 B record.  Each wide node stores all four children's boxes (the parent tests them with
-// one fetch), grouped per axis (SoA within the record), and primitives are stored contiguously in leaf
+// from one 64 B record.  Each wide node stores all four children's boxes (the parent tests them with
+// one fetch), quantized against the node's own frame, and primitives are stored contiguously in leaf
 // order with the triangle operands pre-subtracted exactly as hittable.rs:71-72 computes them.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 namespace rpl {
 
-// 4-wide BVH node: 128 B, one cache line pair-aligned record per lane fetch.  The four child boxes
-// are stored per axis (SoA within the record: 6 x float4 loads) in f32, rounded OUTWARD from the exact
-// f64 boxes, and tested with a conservative slab test (rp_kernel.hip) so no primitive the exact f64
-// test would accept is ever culled.  Child entries:
+// 4-wide BVH node: 64 B, four 16 B loads per lane fetch.  The four child boxes are quantized to 8 bits
+// per plane in a per-node frame (per axis an f32 origin o and step s: plane(q) = o + q * s, exact in f64,
+// q = 0..255), rounded OUTWARD from the exact f64 boxes, and tested with a conservative slab test
+// (rp_device.h trav_step) so no primitive the exact f64 test would accept is ever culled.
+//   16 B chunks: {o.x, o.y, o.z, s.x} {s.y, s.z, lo_x, hi_x} {lo_y, hi_y, lo_z, hi_z} {child[4]}
+// The traversal kernel is bound by the vector-memory data path (one TA/TD cycle per lane per load
+// instruction): halving the node from 7 to 4 loads per visit is the lever; the
+// dequantization (v_cvt_f32_ubyte + the same one FMA per plane) costs ALU that was idle.
+// Child entries:
 //   inner node : node index (bit 31 clear)
 //   leaf       : ENTRY_LEAF | (count - 1) << LEAF_SHIFT | first primitive   (count 1..8)
-//   empty slot : ENTRY_EMPTY
+//   empty slot : ENTRY_EMPTY (its plane bytes are meaningless; the traversal masks it by the entry)
 struct alignas(16) Node4 {
-  float lo_x[4], hi_x[4];
-  float lo_y[4], hi_y[4];
-  float lo_z[4], hi_z[4];
+  float o[3];  // frame origin per axis
+  float s[3];  // frame step per axis
+  uint8_t lo_x[4], hi_x[4];
+  uint8_t lo_y[4], hi_y[4];
+  uint8_t lo_z[4], hi_z[4];
   uint32_t child[4];
-  uint32_t pad[4];
 };
-static_assert(sizeof(Node4) == 128, "Node4 must be 128 B");
+static_assert(sizeof(Node4) == 64, "Node4 must be 64 B");
+
+#if defined(__HIPCC__)
+#define RPL_HD __host__ __device__
+#else
+#define RPL_HD
+#endif
+
+// Node frames.  qframe(lo, hi) picks the frame of a node box [lo, hi] along one axis (finite, lo <= hi):
+//   o <= lo and o + 255 s >= hi;
+//   o is a multiple of 2^(E_s - 8) (E_s = floor(log2 s)) or, far from 0, of its own ulp (>= 2^(E_s - 8)),
+//   and |o| < 2^(E_s + 29), so o + q s is a multiple of 2^(E_s - 23) below 2^(E_s + 30): exact in f64;
+//   s >= (hi - lo) (1 + 2^-7) / 255 leaves room for o's rounding below lo;  s >= 2^-60.
+// plane_q(o, s, q) is that exact value; q_down / q_up the conservative quantization of a child's bounds.
+RPL_HD inline float f32_rd(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -__builtin_huge_valf());
+  return f;
+}
+RPL_HD inline float f32_ru(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, __builtin_huge_valf());
+  return f;
+}
+RPL_HD inline double plane_q(float o, float s, uint32_t q) { return (double)o + (double)q * (double)s; }
+RPL_HD inline void qframe(double lo, double hi, float& o, float& s) {
+  const float o0 = f32_rd(lo);
+  double need = fmax((hi - lo) * (1.0 + 0x1p-7), hi - (double)o0) / 255.0 * (1.0 + 0x1p-40);
+  need = fmax(fmax(need, fabs((double)o0) * 0x1p-28), 0x1p-60);
+  s = f32_ru(need);
+  int e = 0;
+  (void)frexp((double)s, &e);  // s = m 2^e, m in [0.5, 1): E_s = e - 1
+  if (fabs(lo) < ldexp(1.0, e + 15)) {
+    const double g = ldexp(1.0, e - 9);
+    o = (float)(floor(lo / g) * g);
+  } else {
+    o = o0;
+  }
+  while (plane_q(o, s, 255u) < hi) s = nextafterf(s, __builtin_huge_valf());  // not expected to run
+}
+RPL_HD inline uint32_t q_down(double x, float o, float s) {  // largest q with plane(q) <= x (0 if none)
+  double f = floor((x - (double)o) / (double)s);
+  uint32_t q = f <= 0.0 ? 0u : (f >= 255.0 ? 255u : (uint32_t)f);
+  while (q > 0u && plane_q(o, s, q) > x) q--;
+  while (q < 255u && plane_q(o, s, q + 1u) <= x) q++;
+  return q;
+}
+RPL_HD inline uint32_t q_up(double x, float o, float s) {  // smallest q with plane(q) >= x (255 if none)
+  double c = ceil((x - (double)o) / (double)s);
+  uint32_t q = c <= 0.0 ? 0u : (c >= 255.0 ? 255u : (uint32_t)c);
+  while (q < 255u && plane_q(o, s, q) < x) q++;
+  while (q > 0u && plane_q(o, s, q - 1u) >= x) q--;
+  return q;
+}
+// Frames are built from the primitive boxes of the tree, so every |o| and 255 s stays below
+// qbound(amax) (amax = the largest |coordinate| of those boxes): the traversal's slack uses it
+// (rp_device.h setup_ray32).  Coordinates beyond 2^54 are refused (rp_bvh.cpp build).
+RPL_HD inline double qbound(double amax) { return 4.0 * amax + 0x1p-50; }
+constexpr double COORD_MAX = 0x1p54;
+
+// Quantize child c of node n from its exact f64 box (lo[3], hi[3]); a non-finite bound (NaN geometry: never
+// hit) takes the whole frame.
+RPL_HD inline void quantize_child(Node4& n, int c, const double lo[3], const double hi[3]) {
+  uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
+  uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
+  for (int a = 0; a < 3; a++) {
+    const bool ok = lo[a] == lo[a] && hi[a] == hi[a];
+    L[a][c] = ok ? (uint8_t)q_down(lo[a], n.o[a], n.s[a]) : (uint8_t)0;
+    H[a][c] = ok ? (uint8_t)q_up(hi[a], n.o[a], n.s[a]) : (uint8_t)255;
+  }
+}
+RPL_HD inline void empty_child(Node4& n, int c) {
+  n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = 255;
+  n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = 0;
+}
 
 constexpr uint32_t ENTRY_LEAF = 0x80000000u;
 constexpr uint32_t ENTRY_EMPTY = 0xFFFFFFFFu;

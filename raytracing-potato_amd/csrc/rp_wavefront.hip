@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
           o = v3(w.in.ray[q], w.in.ray[P + q], w.in.ray[2 * P + q]);
           d = v3(w.in.ray[3 * P + q], w.in.ray[4 * P + q], w.in.ray[5 * P + q]);
           const KScene S = load_scene(kargs());
-          setup_ray32(o, d, RAY_EPSILON, r);
+          setup_ray32(o, d, RAY_EPSILON, S.qbound, r);
           trav_init(S, INF, ts);
           double best = ts.best;
           for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++)
