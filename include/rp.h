@@ -192,6 +192,9 @@ enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2 };
  * lanes) and the stage-split engine (trace and shade passes over a pool of path slots; its renders
  * synchronise the host: the pass loop polls the ray queue). */
 enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
+/* Wide-node formats: 128 B f32 child boxes, or 64 B child boxes quantized to 8 bits per plane in a per-node
+ * f32 frame (half the node bytes, more ALU per visit).  AUTO = F32 below 2^17 hittables, Q8 above. */
+enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = host binned SAH below 2^20 hittables, device LBVH above */
   uint32_t max_leaf;        /* primitives per leaf, 1..8 (0 -> 4) */
@@ -204,7 +207,8 @@ typedef struct rp_scene_options {
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
   uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
   uint32_t wf_slots;        /* wavefront engine: paths in flight per resident lane (0 -> 2) */
-  uint32_t reserved[2];
+  uint32_t node_format;     /* RP_NODES_* */
+  uint32_t reserved;
 } rp_scene_options;
 
 typedef struct rp_stats {

@@ -49,13 +49,19 @@ void rph_lookat(const double position[3], const double target[3], const double u
 int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba);
 
 /* Self-check of the acceleration-structure builder used by librp.so on a scene (CPU only):
- * validates the scene, builds the tree and checks its invariants.  stats (nullable, 4 values):
- * {nodes, leaves, max_depth, primitives}. */
-int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats);
+ * validates the scene, builds the host tree in `node_format` (RP_NODES_*, AUTO = librp.so's size rule)
+ * and checks its invariants.  stats (nullable, 4 values): {nodes, leaves, max_depth, primitives}. */
+int rph_bvh_selfcheck(const rp_scene_desc* desc, uint32_t node_format, uint64_t* stats);
 
-/* CPU model of the device traversal over the same packed tree (diagnostics): for n rays (layout of
- * rp_intersect) writes n x 3 {node records visited, primitive tests, closest hittable id or 2^64-1}. */
-int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray);
+/* CPU model of the device traversal over the same packed tree in `node_format` (diagnostics): for n rays
+ * (layout of rp_intersect) writes n x 3 {node records visited, primitive tests, closest hittable id or
+ * 2^64-1}. */
+int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
+                            uint64_t* per_ray);
+
+/* Hash (FNV-1a) of the packed host tree (node records and leaf-ordered primitive references) built with
+ * `threads` build threads (0 = the machine's, at most 16): the tree does not depend on the thread count. */
+int rph_bvh_tree_hash(const rp_scene_desc* desc, uint32_t node_format, uint32_t threads, uint64_t* hash);
 
 /* rand 0.8 StdRng (ChaCha12, rand_chacha 0.3 stream: 64-bit block counter, zero nonce) keyed by the 32-byte
  * seed (StdRng::from_seed; seed_from_u64 seeds come from its PCG32 expansion): n consecutive next_u64

@@ -116,7 +116,7 @@ struct rp_scene {
   int device = 0;
   rpk::KScene ks{};
   rp_scene_options opt{};
-  rpl::Node4* d_nodes = nullptr;
+  void* d_nodes = nullptr;  // rpl::Node4 or rpl::Node4Q (ks.node_format)
   rpl::Prim* d_prims = nullptr;
   rpl::PrimRef* d_prim_refs = nullptr;
   double* d_vnrm = nullptr;
@@ -289,6 +289,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
   if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
   if (o.wf_slots > 64) return fail(RP_EINVAL, "options.wf_slots must be 1..64");
+  if (o.node_format > RP_NODES_Q8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
   return RP_OK;
 }
 
@@ -330,6 +331,10 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
   return RP_OK;
 }
 
+size_t rp_node_bytes(uint32_t node_format) {
+  return node_format == rpl::NODES_Q8 ? sizeof(rpl::Node4Q) : sizeof(rpl::Node4);
+}
+
 int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* opt_in, rp_scene** out) {
   if (!out) return fail(RP_EINVAL, "out is NULL");
   *out = nullptr;
@@ -356,6 +361,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   bo.max_leaf = opt.max_leaf;
   bo.cost_traverse = opt.cost_traverse;
   bo.always_max = (uint32_t)opt.always_max;
+  bo.node_format = opt.node_format;  // RP_NODES_AUTO (0) resolved by the builder
   rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(rc, err);
 
@@ -365,12 +371,14 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->opt = opt;
   s->num_cu = prop.multiProcessorCount;
   auto bail = [&](int code) { rp_scene_destroy(s); return code; };
-  uint64_t n_tree_nodes = ps.nodes.size(), n_tree_prims = ps.prims.size();
+  uint64_t n_tree_nodes = ps.n_nodes(), n_tree_prims = ps.prims.size();
+  uint32_t node_format = ps.node_format;
   if (use_gpu) {
     rpb::PrimInput pin;
     if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
+    node_format = opt.node_format ? opt.node_format : rpb::auto_node_format(desc->n_hittables, pin.amax);
     rpg::GpuTree gt;
-    if ((rc = rpg::build_gpu(pin, opt.max_leaf, gt, err))) return bail(fail(rc, err));
+    if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, gt, err))) return bail(fail(rc, err));
     s->d_nodes = gt.d_nodes;
     s->d_prims = gt.d_prims;
     s->d_prim_refs = gt.d_prim_refs;
@@ -378,15 +386,24 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
     ps.max_depth = gt.max_depth;
     ps.n_leaves = gt.n_leaves;
     ps.qbound = gt.qbound;
+    ps.node_format = node_format;
     n_tree_nodes = gt.n_nodes;
     n_tree_prims = pin.prims.size();
     if (opt.self_check) {
       // the structural self-check of the host builder on the device-built tree (tests)
       rpb::PackedScene chk;
-      chk.nodes.resize(n_tree_nodes);
+      chk.node_format = node_format;
+      void* host_nodes;
+      if (node_format == rpl::NODES_Q8) {
+        chk.qnodes.resize(n_tree_nodes);
+        host_nodes = chk.qnodes.data();
+      } else {
+        chk.nodes.resize(n_tree_nodes);
+        host_nodes = chk.nodes.data();
+      }
       chk.prims.resize(n_tree_prims);
       chk.prim_refs.resize(n_tree_prims);
-      RP_HIP(hipMemcpy(chk.nodes.data(), s->d_nodes, sizeof(rpl::Node4) * n_tree_nodes, hipMemcpyDeviceToHost));
+      RP_HIP(hipMemcpy(host_nodes, s->d_nodes, rp_node_bytes(node_format) * n_tree_nodes, hipMemcpyDeviceToHost));
       RP_HIP(hipMemcpy(chk.prims.data(), s->d_prims, sizeof(rpl::Prim) * n_tree_prims, hipMemcpyDeviceToHost));
       RP_HIP(hipMemcpy(chk.prim_refs.data(), s->d_prim_refs, sizeof(rpl::PrimRef) * n_tree_prims, hipMemcpyDeviceToHost));
       chk.root = 0;
@@ -395,7 +412,9 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
       chk.qbound = gt.qbound;
       if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
     }
-  } else if ((rc = upload(ps.nodes, &s->d_nodes)) || (rc = upload(ps.prims, &s->d_prims)) ||
+  } else if ((rc = node_format == rpl::NODES_Q8 ? upload(ps.qnodes, (rpl::Node4Q**)&s->d_nodes)
+                                                    : upload(ps.nodes, (rpl::Node4**)&s->d_nodes)) ||
+             (rc = upload(ps.prims, &s->d_prims)) ||
              (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
     return bail(rc);
   }
@@ -419,6 +438,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->ks.always_first = ps.always_first;  // 0 / 0 for a device-built tree
   s->ks.n_always = ps.n_always;
   s->ks.qbound = ps.qbound;
+  s->ks.node_format = node_format;
   // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
   // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
@@ -428,7 +448,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
   s->max_depth = ps.max_depth;
-  s->device_bytes = sizeof(rpl::Node4) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
+  s->device_bytes = rp_node_bytes(node_format) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
@@ -437,18 +457,18 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // forces a depth (>= 17) for tests and tuning.
   s->ks.lds_depth = s->ks.stack_depth;
   int bpc = 0;
-  if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, &bpc) != 0 || bpc < 1) bpc = 1;
+  if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   int bpc_spill = 0;
-  if (rpk::render_blocks_per_cu(17, true, &bpc_spill) == 0 && bpc_spill > bpc) {
+  if (rpk::render_blocks_per_cu(17, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
     uint32_t L = s->ks.stack_depth - 1;
     int b = 0;
-    while (L > 17 && (rpk::render_blocks_per_cu(L, true, &b) != 0 || b < bpc_spill)) L--;
+    while (L > 17 && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
     s->ks.lds_depth = L;
     bpc = bpc_spill;
   }
   if (opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
     s->ks.lds_depth = opt.lds_depth;
-    if (rpk::render_blocks_per_cu(opt.lds_depth, true, &bpc) != 0 || bpc < 1) bpc = 1;
+    if (rpk::render_blocks_per_cu(opt.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   }
   s->blocks_per_cu = bpc;
   if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);

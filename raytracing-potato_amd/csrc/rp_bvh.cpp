@@ -2,6 +2,9 @@
 #include "rp_bvh.h"
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
+#include <thread>
 #include <functional>
 #include <cmath>
 #include <cstring>
@@ -10,6 +13,31 @@
 namespace rpb {
 
 namespace {
+
+// Running min / max of an accumulator that is never NaN (it starts at +-inf): a NaN operand leaves it
+// unchanged, as fmin / fmax would.  Branch-free (minsd / maxsd): the libm calls gcc emits for std::fmin
+// without -ffinite-math-only, and then a branchy inline form, were most of the host SAH build time.
+inline double min_(double acc, double v) { return v < acc ? v : acc; }
+inline double max_(double acc, double v) { return v > acc ? v : acc; }
+
+// Threads of the host build: the machine's, at most 16 (a GPU box's share of its host).
+unsigned build_threads() {
+  const unsigned h = std::thread::hardware_concurrency();
+  return h == 0 ? 1u : std::min(h, 16u);
+}
+
+// f(begin, end) over [0, n) in `threads` contiguous chunks (inline below min_items items).
+template <class F>
+void parallel_for(size_t n, unsigned threads, F f, size_t min_items = 1u << 16) {
+  if (threads <= 1 || n < min_items) { f((size_t)0, n); return; }
+  std::vector<std::thread> th;
+  const size_t chunk = (n + threads - 1) / threads;
+  for (unsigned t = 0; t < threads; t++) {
+    const size_t b = t * chunk, e = std::min(n, b + chunk);
+    if (b < e) th.emplace_back([=] { f(b, e); });
+  }
+  for (auto& x : th) x.join();
+}
 
 struct Box {
   double lo[3], hi[3];
@@ -22,8 +50,8 @@ struct Box {
   // AABB::union (utility.rs:130-135): exact min/max, so parents contain children bit-exactly.
   void grow(const Box& b) {
     for (int k = 0; k < 3; k++) {
-      lo[k] = std::fmin(lo[k], b.lo[k]);
-      hi[k] = std::fmax(hi[k], b.hi[k]);
+      lo[k] = min_(lo[k], b.lo[k]);
+      hi[k] = max_(hi[k], b.hi[k]);
     }
   }
   double area() const {
@@ -53,52 +81,108 @@ struct Builder {
   std::vector<BinNode>& bin;
   std::vector<uint32_t>& order;  // leaf-ordered hittable ids
   uint64_t n_leaves = 0;
+  unsigned par = 1;  // threads for the centroid-bounds and binning passes of large ranges (ParallelBuild::top)
 
-  // Returns the split position m in (b, e) or b when the range should be a leaf.
-  uint32_t split(uint32_t b, uint32_t e, const Box& box) {
+  // Returns the split position m in (b, e) or b when the range should be a leaf; for a split, lb / rb are
+  // the exact boxes of [b, m) and [m, e).  One binning pass over the range for all three axes (then the
+  // partition); the child boxes are unions of the chosen side's bins (exact min/max: the same values as a
+  // pass over the children).
+  uint32_t split(uint32_t b, uint32_t e, const Box& box, Box& lb, Box& rb) {
     uint32_t n = e - b;
+    // large ranges: both passes split over `par` threads, partial bounds and bins merged (min / max / sums
+    // are order-independent, so the merged values are the serial pass's)
+    const unsigned P = (par > 1 && n >= (1u << 18)) ? par : 1u;
+    const size_t chunk = (n + P - 1) / P;
+    auto run = [&](auto&& f) {
+      if (P == 1) { f(0u, b, e); return; }
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < P; t++) {
+        const uint32_t cb_ = b + (uint32_t)std::min<size_t>(n, t * chunk), ce = b + (uint32_t)std::min<size_t>(n, (t + 1) * chunk);
+        th.emplace_back([&f, t, cb_, ce] { f(t, cb_, ce); });
+      }
+      for (auto& x : th) x.join();
+    };
+    std::vector<Box> cbp(P);
+    run([&](unsigned t, uint32_t lo, uint32_t hi) {
+      Box c;
+      c.reset();
+      for (uint32_t i = lo; i < hi; i++)
+        for (int k = 0; k < 3; k++) {
+          c.lo[k] = min_(c.lo[k], refs[i].c[k]);
+          c.hi[k] = max_(c.hi[k], refs[i].c[k]);
+        }
+      cbp[t] = c;
+    });
     Box cb;
     cb.reset();
-    for (uint32_t i = b; i < e; i++)
-      for (int k = 0; k < 3; k++) {
-        cb.lo[k] = std::fmin(cb.lo[k], refs[i].c[k]);
-        cb.hi[k] = std::fmax(cb.hi[k], refs[i].c[k]);
-      }
+    for (const Box& c : cbp) cb.grow(c);
     const uint32_t NB = std::max(2u, std::min(opt.bins, n));
+    double scale[3];
+    bool live[3];
+    for (int ax = 0; ax < 3; ax++) {
+      const double ext = cb.hi[ax] - cb.lo[ax];
+      live[ax] = ext > 0.0;
+      scale[ax] = live[ax] ? (double)NB / ext : 0.0;
+    }
+    bb_.resize(3 * (size_t)NB);
+    bn_.resize(3 * (size_t)NB);
+    right_area_.resize(NB);
+    right_n_.resize(NB);
+    for (uint32_t k = 0; k < 3 * NB; k++) { bb_[k].reset(); bn_[k] = 0; }
+    auto bin_of = [&](const Ref& r, int ax) {
+      int k = (int)((r.c[ax] - cb.lo[ax]) * scale[ax]);
+      return std::min<int>(std::max(k, 0), (int)NB - 1);
+    };
+    if ((live[0] || live[1] || live[2]) && P == 1) {
+      for (uint32_t i = b; i < e; i++)
+        for (int ax = 0; ax < 3; ax++) {
+          if (!live[ax]) continue;
+          const int k = ax * (int)NB + bin_of(refs[i], ax);
+          bb_[k].grow(refs[i].box);
+          bn_[k]++;
+        }
+    } else if (live[0] || live[1] || live[2]) {
+      std::vector<std::vector<Box>> pb(P, std::vector<Box>(3 * (size_t)NB));
+      std::vector<std::vector<uint32_t>> pn(P, std::vector<uint32_t>(3 * (size_t)NB, 0u));
+      run([&](unsigned t, uint32_t lo, uint32_t hi) {
+        for (Box& x : pb[t]) x.reset();
+        for (uint32_t i = lo; i < hi; i++)
+          for (int ax = 0; ax < 3; ax++) {
+            if (!live[ax]) continue;
+            const int k = ax * (int)NB + bin_of(refs[i], ax);
+            pb[t][k].grow(refs[i].box);
+            pn[t][k]++;
+          }
+      });
+      for (unsigned t = 0; t < P; t++)
+        for (uint32_t k = 0; k < 3 * NB; k++) {
+          bb_[k].grow(pb[t][k]);
+          bn_[k] += pn[t][k];
+        }
+    }
     double best_cost = std::numeric_limits<double>::infinity();
     int best_axis = -1;
     uint32_t best_bin = 0;
-    std::vector<Box> bb(NB);
-    std::vector<uint32_t> bn(NB);
-    std::vector<double> right_area(NB);
-    std::vector<uint32_t> right_n(NB);
     for (int ax = 0; ax < 3; ax++) {
-      double ext = cb.hi[ax] - cb.lo[ax];
-      if (!(ext > 0.0)) continue;
-      double scale = (double)NB / ext;
-      for (uint32_t k = 0; k < NB; k++) { bb[k].reset(); bn[k] = 0; }
-      for (uint32_t i = b; i < e; i++) {
-        int k = (int)((refs[i].c[ax] - cb.lo[ax]) * scale);
-        k = std::min<int>(std::max(k, 0), (int)NB - 1);
-        bb[k].grow(refs[i].box);
-        bn[k]++;
-      }
+      if (!live[ax]) continue;
+      const Box* bb = &bb_[ax * NB];
+      const uint32_t* bn = &bn_[ax * NB];
       Box acc;
       acc.reset();
       uint32_t cnt = 0;
       for (int k = (int)NB - 1; k >= 1; k--) {
         acc.grow(bb[k]);
         cnt += bn[k];
-        right_area[k] = acc.area();
-        right_n[k] = cnt;
+        right_area_[k] = acc.area();
+        right_n_[k] = cnt;
       }
       acc.reset();
       cnt = 0;
       for (uint32_t k = 0; k + 1 < NB; k++) {
         acc.grow(bb[k]);
         cnt += bn[k];
-        if (cnt == 0 || right_n[k + 1] == 0) continue;
-        double cost = acc.area() * cnt + right_area[k + 1] * right_n[k + 1];
+        if (cnt == 0 || right_n_[k + 1] == 0) continue;
+        double cost = acc.area() * cnt + right_area_[k + 1] * right_n_[k + 1];
         if (cost < best_cost) { best_cost = cost; best_axis = ax; best_bin = k; }
       }
     }
@@ -108,15 +192,15 @@ struct Builder {
       double split_cost = opt.cost_traverse +
                           (parent_area > 0.0 ? opt.cost_intersect * best_cost / parent_area : opt.cost_intersect * n);
       if (n <= opt.max_leaf && leaf_cost <= split_cost) return b;
-      double ext = cb.hi[best_axis] - cb.lo[best_axis];
-      double scale = (double)NB / ext;
-      auto mid = std::partition(refs.begin() + b, refs.begin() + e, [&](const Ref& r) {
-        int k = (int)((r.c[best_axis] - cb.lo[best_axis]) * scale);
-        k = std::min<int>(std::max(k, 0), (int)NB - 1);
-        return (uint32_t)k <= best_bin;
-      });
+      auto mid = std::partition(refs.begin() + b, refs.begin() + e,
+                                [&](const Ref& r) { return (uint32_t)bin_of(r, best_axis) <= best_bin; });
       uint32_t m = (uint32_t)(mid - refs.begin());
-      if (m > b && m < e) return m;
+      if (m > b && m < e) {
+        lb.reset();
+        rb.reset();
+        for (uint32_t k = 0; k < NB; k++) (k <= best_bin ? lb : rb).grow(bb_[best_axis * NB + k]);
+        return m;
+      }
     }
     if (n <= opt.max_leaf) return b;
     // Degenerate centroids (or a failed partition): object median on the longest centroid axis.
@@ -128,6 +212,10 @@ struct Builder {
       if (x.c[ax] != y.c[ax]) return x.c[ax] < y.c[ax];
       return x.id < y.id;
     });
+    lb.reset();
+    rb.reset();
+    for (uint32_t i = b; i < m; i++) lb.grow(refs[i].box);
+    for (uint32_t i = m; i < e; i++) rb.grow(refs[i].box);
     return m;
   }
 
@@ -136,7 +224,8 @@ struct Builder {
     const int32_t self = (int32_t)bin.size();
     bin.emplace_back();
     bin[self].box = box;
-    const uint32_t m = split(b, e, box);
+    Box lb, rb;
+    const uint32_t m = split(b, e, box, lb, rb);
     if (m == b) {
       bin[self].first = (uint32_t)order.size();
       bin[self].count = e - b;
@@ -144,22 +233,159 @@ struct Builder {
       n_leaves++;
       return self;
     }
-    Box lb, rb;
-    lb.reset();
-    rb.reset();
-    for (uint32_t i = b; i < m; i++) lb.grow(refs[i].box);
-    for (uint32_t i = m; i < e; i++) rb.grow(refs[i].box);
     const int32_t l = build(b, m, lb);
     const int32_t r = build(m, e, rb);
     bin[self].left = l;
     bin[self].right = r;
     return self;
   }
+
+  std::vector<Box> bb_;  // split() scratch: NB bins per axis
+  std::vector<uint32_t> bn_, right_n_;
+  std::vector<double> right_area_;
+};
+
+// Parallel form of Builder::build with the identical result.  The top of the tree is split serially-in-
+// parallel (the two halves of a large range on two threads) down to ranges of at most `task` primitives;
+// those subtrees are built by independent Builders on a thread pool; the pieces are then spliced in the
+// serial builder's depth-first order (self, left, right), so node numbers, leaf order and the tree are
+// exactly Builder::build's (the split of a range depends only on the range's contents).
+struct TopNode {
+  Box box;
+  uint32_t b = 0, e = 0;
+  int kind = 0;  // 0 inner, 1 leaf (a range split() kept whole), 2 task (built by a Builder later)
+  std::unique_ptr<TopNode> left, right;
+  size_t task = 0;
+};
+
+struct ParallelBuild {
+  const BuildOptions& opt;
+  std::vector<Ref>& refs;
+  uint32_t task_max;
+  unsigned threads;
+
+  struct Task {
+    uint32_t b, e;
+    Box box;
+    std::vector<BinNode> bin;
+    std::vector<uint32_t> order;
+    uint64_t n_leaves = 0;
+  };
+  std::vector<Task> tasks;
+
+  void top(TopNode& t, uint32_t b, uint32_t e, const Box& box, unsigned par) {
+    t.box = box;
+    t.b = b;
+    t.e = e;
+    if (e - b <= task_max) { t.kind = 2; return; }
+    std::vector<BinNode> scratch_bin;
+    std::vector<uint32_t> scratch_order;
+    Builder B{opt, refs, scratch_bin, scratch_order};
+    B.par = par;
+    Box lb, rb;
+    const uint32_t m = B.split(b, e, box, lb, rb);
+    if (m == b) { t.kind = 1; return; }
+    t.left.reset(new TopNode());
+    t.right.reset(new TopNode());
+    if (par > 1) {
+      std::thread th([&] { top(*t.left, b, m, lb, par / 2); });
+      top(*t.right, m, e, rb, par - par / 2);
+      th.join();
+    } else {
+      top(*t.left, b, m, lb, 1);
+      top(*t.right, m, e, rb, 1);
+    }
+  }
+
+  void collect(TopNode& t) {
+    if (t.kind == 2) {
+      t.task = tasks.size();
+      tasks.push_back(Task{t.b, t.e, t.box, {}, {}, 0});
+    } else if (t.kind == 0) {
+      collect(*t.left);
+      collect(*t.right);
+    }
+  }
+
+  // Depth-first numbering of the spliced tree: top nodes are written here, each task's block of nodes and
+  // leaf-order entries is reserved at its offsets (copied afterwards, in parallel).
+  struct Place { size_t task; int32_t node; uint32_t order, refb; };
+  int32_t splice(const TopNode& t, std::vector<BinNode>& bin, uint32_t& n_order, uint64_t& n_leaves,
+                 std::vector<Place>& places) {
+    const int32_t self = (int32_t)bin.size();
+    if (t.kind == 2) {
+      const Task& k = tasks[t.task];
+      places.push_back(Place{t.task, self, n_order, 0});
+      bin.resize(bin.size() + k.bin.size());
+      n_order += (uint32_t)k.order.size();
+      n_leaves += k.n_leaves;
+      return self;
+    }
+    bin.emplace_back();
+    bin[self].box = t.box;
+    if (t.kind == 1) {
+      bin[self].first = n_order;
+      bin[self].count = t.e - t.b;
+      n_order += t.e - t.b;
+      n_leaves++;
+      places.push_back(Place{~(size_t)0, self, bin[self].first, t.b});  // leaf kept whole: ids of refs[b, e)
+      return self;
+    }
+    const int32_t l = splice(*t.left, bin, n_order, n_leaves, places);
+    const int32_t r = splice(*t.right, bin, n_order, n_leaves, places);
+    bin[self].left = l;
+    bin[self].right = r;
+    return self;
+  }
+
+  uint64_t run(uint32_t n, const Box& all, std::vector<BinNode>& bin, std::vector<uint32_t>& order) {
+    TopNode root;
+    top(root, 0, n, all, threads);
+    collect(root);
+    std::atomic<size_t> next{0};
+    auto worker = [&] {
+      for (size_t i; (i = next.fetch_add(1)) < tasks.size();) {
+        Task& k = tasks[i];
+        k.bin.reserve(2 * (size_t)(k.e - k.b));
+        Builder B{opt, refs, k.bin, k.order};
+        B.build(k.b, k.e, k.box);
+        k.n_leaves = B.n_leaves;
+      }
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < threads; t++) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    uint64_t n_leaves = 0;
+    uint32_t n_order = 0;
+    std::vector<Place> places;
+    splice(root, bin, n_order, n_leaves, places);
+    order.resize(n_order);
+    parallel_for(places.size(), std::min<unsigned>(threads, (unsigned)places.size()), [&](size_t b, size_t e) {
+      for (size_t i = b; i < e; i++) {
+        const Place& p = places[i];
+        if (p.task == ~(size_t)0) {
+          const BinNode& leaf = bin[p.node];
+          for (uint32_t k = 0; k < leaf.count; k++) order[p.order + k] = refs[p.refb + k].id;
+          continue;
+        }
+        const Task& k = tasks[p.task];
+        for (size_t j = 0; j < k.bin.size(); j++) {
+          BinNode n = k.bin[j];
+          if (n.leaf()) n.first += p.order;
+          else { n.left += p.node; n.right += p.node; }
+          bin[p.node + j] = n;
+        }
+        std::copy(k.order.begin(), k.order.end(), order.begin() + p.order);
+      }
+    }, 2);
+    return n_leaves;
+  }
 };
 
 // The quantization frame of a wide node from its exact box (rp_layout.h qframe); an axis without a finite
 // extent (NaN geometry only) gets the frame at 0.
-void node_frame(const Box& b, rpl::Node4& n) {
+void node_frame(const Box& b, rpl::Node4Q& n) {
   for (int a = 0; a < 3; a++) {
     const bool ok = std::isfinite(b.lo[a]) && std::isfinite(b.hi[a]) && b.lo[a] <= b.hi[a];
     rpl::qframe(ok ? b.lo[a] : 0.0, ok ? b.hi[a] : 0.0, n.o[a], n.s[a]);
@@ -168,52 +394,103 @@ void node_frame(const Box& b, rpl::Node4& n) {
 
 // Collapse the binary tree into 4-wide nodes: each wide node takes its binary node's two children and
 // repeatedly opens the inner child of largest surface area until it has 4 children (Wald et al.).
+// The wide nodes are written in the scene's node format (child boxes from the exact f64 boxes), numbered
+// depth-first (a node, then its inner children's subtrees in child order).  With par > 1 the inner
+// children's subtrees are collapsed on threads into local arrays and appended in child order: the same
+// numbering and records as the serial collapse.
 struct Collapser {
   const std::vector<BinNode>& bin;
-  std::vector<rpl::Node4>& out;
+  uint32_t fmt;
+  unsigned par = 1;
+  std::vector<rpl::Node4> nodes;
+  std::vector<rpl::Node4Q> qnodes;
   uint32_t max_depth = 0;
+
+  uint32_t size() const { return (uint32_t)(fmt == rpl::NODES_Q8 ? qnodes.size() : nodes.size()); }
+  uint32_t* child(uint32_t i) { return fmt == rpl::NODES_Q8 ? qnodes[i].child : nodes[i].child; }
+  uint32_t add() {
+    if (fmt == rpl::NODES_Q8) qnodes.emplace_back();
+    else nodes.emplace_back();
+    return size() - 1;
+  }
+  // appends another collapse's nodes, shifting its inner-node entries by the current size
+  void append(Collapser& o) {
+    const uint32_t base = size();
+    if (fmt == rpl::NODES_Q8) qnodes.insert(qnodes.end(), o.qnodes.begin(), o.qnodes.end());
+    else nodes.insert(nodes.end(), o.nodes.begin(), o.nodes.end());
+    for (uint32_t i = base; i < size(); i++)
+      for (int c = 0; c < 4; c++)
+        if (!(child(i)[c] & rpl::ENTRY_LEAF)) child(i)[c] += base;
+  }
 
   uint32_t emit(int32_t bi, uint32_t depth) {
     if (depth > max_depth) max_depth = depth;
-    const uint32_t self = (uint32_t)out.size();
-    out.emplace_back();
-    std::vector<int32_t> kids;
+    const uint32_t self = add();
+    int32_t kids[4];
+    int nk = 0;
     if (bin[bi].leaf()) {
-      kids.push_back(bi);  // root that is a single leaf
+      kids[nk++] = bi;  // root that is a single leaf
     } else {
-      kids = {bin[bi].left, bin[bi].right};
-      while (kids.size() < 4) {
+      kids[nk++] = bin[bi].left;
+      kids[nk++] = bin[bi].right;
+      while (nk < 4) {
         int best = -1;
         double area = -1.0;
-        for (size_t k = 0; k < kids.size(); k++)
-          if (!bin[kids[k]].leaf() && bin[kids[k]].box.area() > area) { area = bin[kids[k]].box.area(); best = (int)k; }
+        for (int k = 0; k < nk; k++)
+          if (!bin[kids[k]].leaf() && bin[kids[k]].box.area() > area) { area = bin[kids[k]].box.area(); best = k; }
         if (best < 0) break;
         const int32_t open = kids[best];
         kids[best] = bin[open].left;
-        kids.push_back(bin[open].right);
+        kids[nk++] = bin[open].right;
+      }
+    }
+    if (fmt == rpl::NODES_Q8) {
+      rpl::Node4Q& n = qnodes[self];
+      Box nb;
+      nb.reset();
+      for (int k = 0; k < nk; k++) nb.grow(bin[kids[k]].box);
+      node_frame(nb, n);
+      for (int c = 0; c < 4; c++) {
+        if (c < nk) rpl::quantize_child(n, c, bin[kids[c]].box.lo, bin[kids[c]].box.hi);
+        else rpl::empty_child(n, c);
+      }
+    } else {
+      rpl::Node4& n = nodes[self];
+      for (int c = 0; c < 4; c++) {
+        if (c < nk) rpl::f32_child(n, c, bin[kids[c]].box.lo, bin[kids[c]].box.hi);
+        else rpl::f32_empty(n, c);
       }
     }
     uint32_t entries[4];
-    {
-      rpl::Node4& n = out[self];
-      Box nb;
-      nb.reset();
-      for (int32_t k : kids) nb.grow(bin[k].box);
-      node_frame(nb, n);
-      for (int c = 0; c < 4; c++) {
-        if ((size_t)c >= kids.size()) {
-          rpl::empty_child(n, c);
-          entries[c] = rpl::ENTRY_EMPTY;
-          continue;
-        }
-        const BinNode& k = bin[kids[c]];
-        rpl::quantize_child(n, c, k.box.lo, k.box.hi);
-        entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
-      }
+    int inner = 0;
+    for (int c = 0; c < 4; c++) {
+      if (c >= nk) { entries[c] = rpl::ENTRY_EMPTY; continue; }
+      const BinNode& k = bin[kids[c]];
+      entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
+      inner += !k.leaf();
     }
-    for (int c = 0; c < 4; c++)
-      if ((size_t)c < kids.size() && !bin[kids[c]].leaf()) entries[c] = emit(kids[c], depth + 1);
-    for (int c = 0; c < 4; c++) out[self].child[c] = entries[c];
+    if (par > 1 && inner >= 2) {
+      std::vector<std::unique_ptr<Collapser>> sub;
+      std::vector<std::thread> th;
+      for (int c = 0; c < nk; c++) {
+        if (bin[kids[c]].leaf()) continue;
+        sub.emplace_back(new Collapser{bin, fmt, std::max(1u, par / (unsigned)inner), {}, {}, 0});
+        Collapser* sc = sub.back().get();
+        const int32_t kb = kids[c];
+        th.emplace_back([sc, kb] { sc->emit(kb, 0); });
+      }
+      for (auto& t : th) t.join();
+      for (int c = 0, j = 0; c < nk; c++) {
+        if (bin[kids[c]].leaf()) continue;
+        entries[c] = size();
+        max_depth = std::max(max_depth, depth + 1 + sub[j]->max_depth);
+        append(*sub[j++]);
+      }
+    } else {
+      for (int c = 0; c < nk; c++)
+        if (!bin[kids[c]].leaf()) entries[c] = emit(kids[c], depth + 1);
+    }
+    for (int c = 0; c < 4; c++) child(self)[c] = entries[c];
     return self;
   }
 };
@@ -327,8 +604,12 @@ static bool texture_reads_uv(const rp_scene_desc* d, uint32_t t, int depth = 0) 
   return false;
 }
 
+static void pack_prim(const rp_scene_desc* d, const std::vector<uint64_t>& vbase, uint32_t id, rpl::Prim& p,
+                      rpl::PrimRef& pr);
+
 int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std::string& err) {
   out = PackedScene();
+  const unsigned threads = opt.threads ? opt.threads : build_threads();
   // ---- shading tables
   std::vector<uint64_t> vbase(d->n_meshes + 1, 0);
   for (uint32_t i = 0; i < d->n_meshes; i++) vbase[i + 1] = vbase[i] + d->meshes[i].n_vertices;
@@ -337,10 +618,11 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   out.vuv.resize(2 * vbase[d->n_meshes] + 2);
   for (uint32_t i = 0; i < d->n_meshes; i++) {
     const rp_mesh& m = d->meshes[i];
-    if (m.n_vertices) {
-      std::memcpy(&out.vnrm[3 * vbase[i]], m.normals, sizeof(double) * 3 * m.n_vertices);
-      std::memcpy(&out.vuv[2 * vbase[i]], m.uvs, sizeof(double) * 2 * m.n_vertices);
-    }
+    // vertex runs in parallel chunks (C5: 30 M vertices, 1.2 GB)
+    parallel_for(m.n_vertices, threads, [&](size_t b, size_t e) {
+      std::memcpy(&out.vnrm[3 * (vbase[i] + b)], m.normals + 3 * b, sizeof(double) * 3 * (e - b));
+      std::memcpy(&out.vuv[2 * (vbase[i] + b)], m.uvs + 2 * b, sizeof(double) * 2 * (e - b));
+    });
   }
   for (uint32_t i = 0; i < d->n_materials; i++) {
     const rp_material& s = d->materials[i];
@@ -394,6 +676,7 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
 
   if (opt.tables_only) return RP_OK;
+  if (opt.node_format > rpl::NODES_Q8) { err = "unknown node format"; return RP_EINVAL; }
 
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is
   //      independent of visit order except exact-t ties)
@@ -403,11 +686,13 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   if ((uint64_t)n * sizeof(rpl::Prim) > 0xFFFFFFFFull) { err = "too many hittables for 32-bit device offsets"; return RP_EINVAL; }
   if (opt.max_leaf < 1 || opt.max_leaf > rpl::LEAF_MAX) { err = "max_leaf out of range"; return RP_EINVAL; }
   std::vector<Ref> refs(n);
-  for (uint32_t i = 0; i < n; i++) {
-    refs[i].box = hittable_box(d, d->hittables[i]);
-    for (int k = 0; k < 3; k++) refs[i].c[k] = 0.5 * (refs[i].box.lo[k] + refs[i].box.hi[k]);
-    refs[i].id = i;
-  }
+  parallel_for(n, threads, [&](size_t b, size_t e) {
+    for (size_t i = b; i < e; i++) {
+      refs[i].box = hittable_box(d, d->hittables[i]);
+      for (int k = 0; k < 3; k++) refs[i].c[k] = 0.5 * (refs[i].box.lo[k] + refs[i].box.hi[k]);
+      refs[i].id = (uint32_t)i;
+    }
+  });
   // always-tested primitives (BuildOptions::always_max): out of the tree, appended after its leaves
   std::vector<uint32_t> always;
   if (opt.always_max > 0 && n > 1) {
@@ -438,9 +723,10 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   const uint32_t n_tree = (uint32_t)refs.size();
   double amax = 0.0;
   for (const Ref& r : refs)
-    for (int k = 0; k < 3; k++) amax = std::fmax(amax, std::fmax(std::fabs(r.box.lo[k]), std::fabs(r.box.hi[k])));
-  if (!(amax <= rpl::COORD_MAX)) {
-    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized tree";
+    for (int k = 0; k < 3; k++) amax = max_(max_(amax, std::fabs(r.box.lo[k])), std::fabs(r.box.hi[k]));
+  out.node_format = opt.node_format ? opt.node_format : auto_node_format(d->n_hittables, amax);
+  if (out.node_format == rpl::NODES_Q8 && !(amax <= rpl::COORD_MAX)) {
+    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized nodes";
     return RP_EINVAL;
   }
   out.qbound = rpl::qbound(amax);
@@ -450,22 +736,40 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   bin.reserve(n_tree ? 2 * (size_t)n_tree : 1);
   Builder B{opt, refs, bin, order};
   if (n_tree == 0) {
-    rpl::Node4 root{};
-    for (int a = 0; a < 3; a++) rpl::qframe(0.0, 0.0, root.o[a], root.s[a]);
-    for (int c = 0; c < 4; c++) {
-      rpl::empty_child(root, c);
-      root.child[c] = rpl::ENTRY_EMPTY;
+    if (out.node_format == rpl::NODES_Q8) {
+      rpl::Node4Q root{};
+      for (int a = 0; a < 3; a++) rpl::qframe(0.0, 0.0, root.o[a], root.s[a]);
+      for (int c = 0; c < 4; c++) {
+        rpl::empty_child(root, c);
+        root.child[c] = rpl::ENTRY_EMPTY;
+      }
+      out.qnodes.push_back(root);
+    } else {
+      rpl::Node4 root{};
+      for (int c = 0; c < 4; c++) {
+        rpl::f32_empty(root, c);
+        root.child[c] = rpl::ENTRY_EMPTY;
+      }
+      out.nodes.push_back(root);
     }
-    out.nodes.push_back(root);
     out.max_depth = 0;
   } else {
     Box all;
     all.reset();
     for (auto& r : refs) all.grow(r.box);
-    B.build(0, n_tree, all);
-    out.nodes.reserve(bin.size() / 2 + 1);
-    Collapser C{bin, out.nodes};
+    // large trees: the parallel form (identical tree); tasks of ~n/256 primitives, at least 16 k
+    if (n_tree >= (1u << 16) && threads > 1) {
+      ParallelBuild P{opt, refs, std::max<uint32_t>(n_tree / 256, 1u << 14), threads, {}};
+      B.n_leaves = P.run(n_tree, all, bin, order);
+    } else {
+      B.build(0, n_tree, all);
+    }
+    Collapser C{bin, out.node_format, threads, {}, {}, 0};
+    if (out.node_format == rpl::NODES_Q8) C.qnodes.reserve(bin.size() / 2 + 1);
+    else C.nodes.reserve(bin.size() / 2 + 1);
     C.emit(0, 0);
+    out.nodes.swap(C.nodes);
+    out.qnodes.swap(C.qnodes);
     out.max_depth = C.max_depth;
   }
   out.root = 0;
@@ -474,39 +778,12 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   out.n_always = (uint32_t)always.size();
   for (uint32_t a : always) order.push_back(a);
 
-  // ---- primitives in leaf order
+  // ---- primitives in leaf order (value-initialised: a scene without primitives keeps one zero record)
   out.prims.resize(order.size() ? order.size() : 1);
-  std::memset(out.prims.data(), 0, sizeof(rpl::Prim) * out.prims.size());
   out.prim_refs.resize(out.prims.size());
-  std::memset(out.prim_refs.data(), 0, sizeof(rpl::PrimRef) * out.prim_refs.size());
-  for (size_t k = 0; k < order.size(); k++) {
-    const rp_hittable& h = d->hittables[order[k]];
-    rpl::Prim& p = out.prims[k];
-    rpl::PrimRef& pr = out.prim_refs[k];
-    pr.src = order[k];
-    if (h.kind == RP_HITTABLE_SPHERE) {
-      p.kind = rpl::PRIM_SPHERE;
-      p.material = h.material;
-      for (int c = 0; c < 3; c++) p.g[c] = h.center[c];
-      p.g[3] = h.radius;
-    } else {
-      const rp_mesh& m = d->meshes[h.mesh];
-      uint32_t i0 = m.indices[h.triangle], i1 = m.indices[h.triangle + 1], i2 = m.indices[h.triangle + 2];
-      const double* a = m.positions + 3 * (size_t)i0;
-      const double* b = m.positions + 3 * (size_t)i1;
-      const double* c = m.positions + 3 * (size_t)i2;
-      p.kind = rpl::PRIM_TRIANGLE;
-      p.material = m.material;
-      for (int k2 = 0; k2 < 3; k2++) {
-        p.g[k2] = a[k2];
-        p.g[3 + k2] = a[k2] - b[k2];  // ba, hittable.rs:71 (same IEEE subtraction as on the device)
-        p.g[6 + k2] = a[k2] - c[k2];  // ca, hittable.rs:72
-      }
-      pr.v[0] = (uint32_t)(vbase[h.mesh] + i0);
-      pr.v[1] = (uint32_t)(vbase[h.mesh] + i1);
-      pr.v[2] = (uint32_t)(vbase[h.mesh] + i2);
-    }
-  }
+  parallel_for(order.size(), threads, [&](size_t b, size_t e) {
+    for (size_t k = b; k < e; k++) pack_prim(d, vbase, order[k], out.prims[k], out.prim_refs[k]);
+  });
   return RP_OK;
 }
 
@@ -567,18 +844,14 @@ int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err) {
       out.cmax[k] = std::fmax(out.cmax[k], c);
     }
   }
-  if (!(out.amax <= rpl::COORD_MAX)) {
-    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized tree";
-    return RP_EINVAL;
-  }
   return RP_OK;
 }
 
 int check(const PackedScene& s, std::string& err) {
-  // Every primitive referenced exactly once; every node frame exact and inside qbound (rp_layout.h); every
-  // quantized child box contains its subtree's exact f64 primitive boxes; acyclic, no deeper than max_depth.
+  // Every primitive referenced exactly once; every stored child box (f32, or quantized in a frame inside
+  // qbound, rp_layout.h) contains its subtree's exact f64 primitive boxes; acyclic, no deeper than max_depth.
   std::vector<uint8_t> used(s.prims.size(), 0);
-  std::vector<uint8_t> visited(s.nodes.size(), 0);
+  std::vector<uint8_t> visited(s.n_nodes(), 0);
   size_t np = 0;
   auto prim_box = [&](const rpl::Prim& p, Box& b) {
     if (p.kind == rpl::PRIM_SPHERE) {
@@ -593,7 +866,7 @@ int check(const PackedScene& s, std::string& err) {
       }
     }
   };
-  if (!(s.qbound > 0.0)) { err = "qbound not set"; return RP_EINTERNAL; }
+  if (s.node_format == rpl::NODES_Q8 && !(s.qbound > 0.0)) { err = "qbound not set"; return RP_EINTERNAL; }
   // subtree box of `entry` into `out`; false (err set) on the first violation
   std::function<bool(uint32_t, uint32_t, Box&)> walk = [&](uint32_t entry, uint32_t depth, Box& out) -> bool {
     out.reset();
@@ -609,28 +882,45 @@ int check(const PackedScene& s, std::string& err) {
       }
       return true;
     }
-    if (entry >= s.nodes.size()) { err = "node index out of range"; return false; }
+    if (entry >= s.n_nodes()) { err = "node index out of range"; return false; }
     if (visited[entry]) { err = "node visited twice"; return false; }
     visited[entry] = 1;
     if (depth > s.max_depth) { err = "depth exceeds max_depth"; return false; }
-    const rpl::Node4& n = s.nodes[entry];
-    for (int a = 0; a < 3; a++) {
-      if (!(n.s[a] >= 0x1p-60f) || !std::isfinite(n.o[a]) || !(std::fabs((double)n.o[a]) <= s.qbound) ||
-          !(255.0 * (double)n.s[a] <= s.qbound)) {
-        err = "node frame outside qbound";
-        return false;
+    const uint32_t* child;
+    double plo[4][3], phi[4][3];  // the stored child box planes, exact in f64
+    if (s.node_format == rpl::NODES_Q8) {
+      const rpl::Node4Q& n = s.qnodes[entry];
+      for (int a = 0; a < 3; a++) {
+        if (!(n.s[a] >= 0x1p-60f) || !std::isfinite(n.o[a]) || !(std::fabs((double)n.o[a]) <= s.qbound) ||
+            !(255.0 * (double)n.s[a] <= s.qbound)) {
+          err = "node frame outside qbound";
+          return false;
+        }
       }
+      const uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
+      const uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
+      for (int c = 0; c < 4; c++)
+        for (int a = 0; a < 3; a++) {
+          plo[c][a] = rpl::plane_q(n.o[a], n.s[a], L[a][c]);
+          phi[c][a] = rpl::plane_q(n.o[a], n.s[a], H[a][c]);
+        }
+      child = n.child;
+    } else {
+      const rpl::Node4& n = s.nodes[entry];
+      for (int c = 0; c < 4; c++) {
+        plo[c][0] = n.lo_x[c]; plo[c][1] = n.lo_y[c]; plo[c][2] = n.lo_z[c];
+        phi[c][0] = n.hi_x[c]; phi[c][1] = n.hi_y[c]; phi[c][2] = n.hi_z[c];
+      }
+      child = n.child;
     }
-    const uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
-    const uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
     for (int c = 0; c < 4; c++) {
-      if (n.child[c] == rpl::ENTRY_EMPTY) continue;
+      if (child[c] == rpl::ENTRY_EMPTY) continue;
       Box sub;
-      if (!walk(n.child[c], depth + 1, sub)) return false;
+      if (!walk(child[c], depth + 1, sub)) return false;
       for (int a = 0; a < 3; a++) {
         if (!(sub.lo[a] <= sub.hi[a])) continue;  // nothing finite below on this axis
-        if (!(rpl::plane_q(n.o[a], n.s[a], L[a][c]) <= sub.lo[a]) || !(rpl::plane_q(n.o[a], n.s[a], H[a][c]) >= sub.hi[a])) {
-          err = "quantized child box does not contain its subtree";
+        if (!(plo[c][a] <= sub.lo[a]) || !(phi[c][a] >= sub.hi[a])) {
+          err = "child box does not contain its subtree";
           return false;
         }
       }

@@ -27,10 +27,14 @@ struct BuildOptions {
   // ground sphere, r = 1000 under a bunny of size ~0.2).  always_max = 0 disables.
   uint32_t always_max = 4;
   double always_ratio = 4.0;
+  uint32_t node_format = rpl::NODES_F32;  // rpl::NODES_F32 (Node4), rpl::NODES_Q8 (Node4Q) or 0 (auto_node_format)
+  uint32_t threads = 0;                   // host build threads (0 = the machine's, at most 16); same tree for any
 };
 
 struct PackedScene {
-  std::vector<rpl::Node4> nodes;      // nodes[root] is the root (always an inner record)
+  uint32_t node_format = rpl::NODES_F32;  // resolved (never 0 after a tree build)
+  std::vector<rpl::Node4> nodes;      // NODES_F32: nodes[root] is the root (always an inner record)
+  std::vector<rpl::Node4Q> qnodes;    // NODES_Q8: the same tree in the quantized format
   std::vector<rpl::Prim> prims;       // leaf order
   std::vector<rpl::PrimRef> prim_refs;  // leaf order: vertex ids, source hittable
   std::vector<double> vnrm;           // 3 per global vertex (mesh vertices concatenated)
@@ -43,8 +47,18 @@ struct PackedScene {
   uint32_t max_depth = 0;             // deepest wide node (root = 0)
   uint32_t always_first = 0, n_always = 0;  // prims[always_first, +n_always): outside the tree, tested first
   uint64_t n_leaves = 0;
-  double qbound = 0.0;  // rp_layout.h qbound: >= |o| and 255 s of every node frame
+  double qbound = 0.0;  // rp_layout.h qbound: >= |o| and 255 s of every node frame (NODES_Q8)
+  size_t n_nodes() const { return node_format == rpl::NODES_Q8 ? qnodes.size() : nodes.size(); }
 };
+
+// The node format of RP_NODES_AUTO: the 64 B quantized node once the 128 B tree would outgrow the L2
+// (~2^17 hittables: ~60 k wide nodes, 8 MB), where halving the node bytes pays -- unless a
+// coordinate exceeds the frames' range (rp_layout.h COORD_MAX).  `amax`: the largest |coordinate| of the
+// primitive boxes.
+constexpr uint32_t Q8_MIN_PRIMS = 1u << 17;
+inline uint32_t auto_node_format(uint32_t n_hittables, double amax) {
+  return n_hittables >= Q8_MIN_PRIMS && amax <= rpl::COORD_MAX ? rpl::NODES_Q8 : rpl::NODES_F32;
+}
 
 // Checks every index the reference would bounds-check (or loop on).  Returns RP_OK or RP_EINVAL.
 int validate(const rp_scene_desc* d, std::string& err);
@@ -73,7 +87,8 @@ namespace rpg {
 
 // A tree built on the device (rp_bvh_gpu.hip): device buffers in the rp_layout.h format, owned by the caller.
 struct GpuTree {
-  rpl::Node4* d_nodes = nullptr;  // n_nodes used (capacity: one per primitive)
+  void* d_nodes = nullptr;  // rpl::Node4 or rpl::Node4Q by node_format; n_nodes used (capacity: one per primitive)
+  uint32_t node_format = rpl::NODES_F32;
   rpl::Prim* d_prims = nullptr;   // leaf order
   rpl::PrimRef* d_prim_refs = nullptr;
   uint64_t n_nodes = 0, n_leaves = 0;
@@ -82,6 +97,6 @@ struct GpuTree {
 };
 
 // LBVH (Karras 2012) + wide collapse on the current device.  Needs >= 2 primitives.
-int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::string& err);
+int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, GpuTree& out, std::string& err);
 
 }  // namespace rpg

@@ -14,6 +14,8 @@
 //      a subtree of <= max_leaf primitives -- a contiguous run of the sorted order -- becomes a leaf;
 //   6. primitive records permuted into leaf (= sorted) order; child boxes rounded outward to f32.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 #include <hipcub/hipcub.hpp>
 
 #include <string>
@@ -167,13 +169,14 @@ __device__ __forceinline__ uint32_t bin_count(uint32_t c, const uint32_t* first,
 
 // One level of the collapse: every frontier entry fills its wide node and appends its inner wide
 // children to the next frontier.
+template <uint32_t NF>
 __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur, Frontier* __restrict__ next,
                                 uint32_t* __restrict__ counters /* [0] wide nodes, [1] next frontier, [2] leaves */,
                                 uint32_t max_leaf, const Box6* __restrict__ leaf_boxes,
                                 const uint32_t* __restrict__ order, const uint32_t* __restrict__ left,
                                 const uint32_t* __restrict__ right, const uint32_t* __restrict__ first,
                                 const uint32_t* __restrict__ last, const Box6* __restrict__ node_boxes,
-                                rpl::Node4* __restrict__ nodes) {
+                                void* __restrict__ nodes) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n_cur) return;
   const Frontier f = cur[t];
@@ -210,20 +213,28 @@ __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur
       nb.hi[a] = fmax(nb.hi[a], kb[k].hi[a]);
     }
   }
-  // quantization frame of the wide node (rp_layout.h qframe; rp_bvh.cpp node_frame)
-  rpl::Node4 nd;
-  for (int a = 0; a < 3; a++) {
-    const bool ok = isfinite(nb.lo[a]) && isfinite(nb.hi[a]) && nb.lo[a] <= nb.hi[a];
-    rpl::qframe(ok ? nb.lo[a] : 0.0, ok ? nb.hi[a] : 0.0, nd.o[a], nd.s[a]);
+  // child boxes in the node format: f32 rounded outward, or quantized in the node's frame (rp_layout.h
+  // qframe; rp_bvh.cpp node_frame / Collapser)
+  typedef typename std::conditional<NF == rpl::NODES_Q8, rpl::Node4Q, rpl::Node4>::type NodeT;
+  NodeT nd;
+  if constexpr (NF == rpl::NODES_Q8) {
+    for (int a = 0; a < 3; a++) {
+      const bool ok = isfinite(nb.lo[a]) && isfinite(nb.hi[a]) && nb.lo[a] <= nb.hi[a];
+      rpl::qframe(ok ? nb.lo[a] : 0.0, ok ? nb.hi[a] : 0.0, nd.o[a], nd.s[a]);
+    }
+  } else {
+    for (int k = 0; k < 4; k++) nd.pad[k] = 0;
   }
   for (uint32_t k = 0; k < 4; k++) {
     if (k >= nk) {
-      rpl::empty_child(nd, (int)k);
+      if constexpr (NF == rpl::NODES_Q8) rpl::empty_child(nd, (int)k);
+      else rpl::f32_empty(nd, (int)k);
       nd.child[k] = rpl::ENTRY_EMPTY;
       continue;
     }
     const uint32_t c = kids[k];
-    rpl::quantize_child(nd, (int)k, kb[k].lo, kb[k].hi);
+    if constexpr (NF == rpl::NODES_Q8) rpl::quantize_child(nd, (int)k, kb[k].lo, kb[k].hi);
+    else rpl::f32_child(nd, (int)k, kb[k].lo, kb[k].hi);
     const uint32_t cnt = bin_count(c, first, last);
     if (cnt <= max_leaf) {
       const uint32_t lo = (c & BIN_LEAF) ? (c & ~BIN_LEAF) : first[c];
@@ -235,7 +246,7 @@ __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur
       next[atomicAdd(&counters[1], 1u)] = Frontier{c, w};
     }
   }
-  nodes[f.wide] = nd;
+  reinterpret_cast<NodeT*>(nodes)[f.wide] = nd;
 }
 
 __global__ void permute_kernel(uint32_t n, const uint32_t* __restrict__ order, const rpl::Prim* __restrict__ prims_in,
@@ -258,11 +269,19 @@ unsigned grid(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / 
 }  // namespace
 
 // Temporaries are freed on every path; on success the caller owns out.d_nodes / d_prims / d_prim_refs.
-int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::string& err) {
+int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, GpuTree& out, std::string& err) {
   out = GpuTree{};
   const uint32_t n = (uint32_t)in.prims.size();
   if (n < 2) {
     err = "device BVH build needs at least 2 primitives";
+    return RP_EINVAL;
+  }
+  if (node_format != rpl::NODES_F32 && node_format != rpl::NODES_Q8) {
+    err = "unknown node format";
+    return RP_EINVAL;
+  }
+  if (node_format == rpl::NODES_Q8 && !(in.amax <= rpl::COORD_MAX)) {
+    err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized nodes";
     return RP_EINVAL;
   }
   if (max_leaf < 1 || max_leaf > rpl::LEAF_MAX) {
@@ -303,7 +322,8 @@ int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::st
   alloc((void**)&d_fa, sizeof(Frontier) * n);
   alloc((void**)&d_fb, sizeof(Frontier) * n);
   // outputs: at most n - 1 wide nodes (each inner wide node has >= 2 children)
-  if (e == hipSuccess) e = hipMalloc((void**)&out.d_nodes, sizeof(rpl::Node4) * n);
+  const size_t node_bytes = node_format == rpl::NODES_Q8 ? sizeof(rpl::Node4Q) : sizeof(rpl::Node4);
+  if (e == hipSuccess) e = hipMalloc(&out.d_nodes, node_bytes * n);
   if (e == hipSuccess) e = hipMalloc((void**)&out.d_prims, sizeof(rpl::Prim) * n);
   if (e == hipSuccess) e = hipMalloc((void**)&out.d_prim_refs, sizeof(rpl::PrimRef) * n);
   void* d_sort_tmp = nullptr;
@@ -365,8 +385,12 @@ int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::st
   for (;;) {
     e = hipMemset(d_ctr + 1, 0, sizeof(uint32_t));
     if (e != hipSuccess) return cleanup(RP_EHIP, std::string("collapse: ") + hipGetErrorString(e));
-    hipLaunchKernelGGL(collapse_kernel, dim3(grid(n_cur, B)), dim3(B), 0, nullptr, d_fa, n_cur, d_fb, d_ctr, max_leaf,
-                       d_boxes, d_order, d_left, d_right, d_first, d_last, d_nboxes, out.d_nodes);
+    if (node_format == rpl::NODES_Q8)
+      hipLaunchKernelGGL(collapse_kernel<rpl::NODES_Q8>, dim3(grid(n_cur, B)), dim3(B), 0, nullptr, d_fa, n_cur, d_fb,
+                         d_ctr, max_leaf, d_boxes, d_order, d_left, d_right, d_first, d_last, d_nboxes, out.d_nodes);
+    else
+      hipLaunchKernelGGL(collapse_kernel<rpl::NODES_F32>, dim3(grid(n_cur, B)), dim3(B), 0, nullptr, d_fa, n_cur, d_fb,
+                         d_ctr, max_leaf, d_boxes, d_order, d_left, d_right, d_first, d_last, d_nboxes, out.d_nodes);
     RPG_CHECK("collapse");
     uint32_t ctr[4];
     e = hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost);
@@ -382,6 +406,7 @@ int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, GpuTree& out, std::st
     std::swap(d_fa, d_fb);
   }
   out.max_depth = depth;
+  out.node_format = node_format;
   out.qbound = rpl::qbound(in.amax);
   hipLaunchKernelGGL(permute_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_order, d_prims_in, d_refs_in,
                      out.d_prims, out.d_prim_refs);

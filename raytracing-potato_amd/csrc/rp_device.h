@@ -357,33 +357,34 @@ struct TravDiag {
 
 // ---- conservative f32 box test ------------------------------------------------------------------
 //
-// Child box planes are P = o + q s (rp_layout.h Node4: per node and axis an f32 frame origin o and step s,
-// q an 8-bit plane code; P is exact in f64 and rounded outward from the exact f64 boxes by the builder).
-// The ray enters in f32 as o32 = fl(o_ray), inv = rcp(fl(d)) (<= 1 ulp), oinv = fl(o32 * inv); per node
-// and axis A = fl(s inv) and B = fma(o, inv, -oinv), and each plane costs one FMA: t^ = fma(q, A, B).
-// Against the exact t = (P - o_ray) / d:
-//     t^ = (P inv - oinv) (1 + d3) + e,   |e| <= u (1 + u) (|q s inv| + |o inv - oinv|)
-// where the first term is the single-rounding form fma(P, inv, -oinv) with an exact P, whose error is
-//     <= 5u |t| + |o_ray - o32| |inv| (1 + 6u) + u |o32 inv|                    (u = 2^-24)
-// and, with every |o| and |q s| <= qbound (rp_layout.h), |e| <= u (1 + u) |inv| (2 qbound + |o32|) + u^2 |o32 inv|
-// (e = 0 when inv = +-2^64, the clamp below, and o32 = 0: A and B are exact).
-// With D = max over axes of all the absolute terms, a box whose exact interval meets [t_min, best] at
-// some t* > 0 satisfies  tnear^ <= t*(1 + 5u) + D  and  tfar^ >= t*(1 - 5u) - D  (the near planes behind
-// the origin and tmin32 <= t* do not raise tnear^; every far plane lies at or beyond t*).  The test
+// Conservative f32 slab test.  The ray enters in f32 as o32 = fl(o_ray), inv = rcp(fl(d)) (<= 1 ulp),
+// oinv = fl(o32 * inv).  Plane coordinates P are exact: f32 values rounded outward from the exact f64 boxes
+// (Node4), or P = o + q s in a node frame (Node4Q: f32 o and s, 8-bit q, exact in f64).
+//   Node4:  t^ = fma(P, inv, -oinv)
+//   Node4Q: per node and axis A = fl(s inv), B = fma(o, inv, -oinv), and t^ = fma(q, A, B) =
+//           (P inv - oinv)(1 + d3) + e,  |e| <= u (1 + u)(|q s inv| + |o inv - oinv|)
+// The single-rounding form fma(P, inv, -oinv) errs by <= 5u |t| + |o_ray - o32| |inv| (1 + 6u) + u |o32 inv|
+// against the exact t = (P - o_ray) / d (u = 2^-24); with every |o| and |q s| <= qbound (rp_layout.h),
+// |e| <= u (1 + u) |inv| (2 qbound + |o32|) + u^2 |o32 inv|, and e = 0 when inv = +-2^64 (the clamp below)
+// and o32 = 0 (A and B exact).  With D = max over axes of the absolute terms, a box whose exact interval
+// meets [t_min, best] at some t* > 0 satisfies  tnear^ <= t*(1 + 5u) + D  and  tfar^ >= t*(1 - 5u) - D  (the
+// near planes behind the origin and tmin32 <= t* do not raise tnear^; every far plane lies at or beyond t*).
+// The test
 //     fma(tnear^, 1 - 2^-19, -slack) <= tfar^                    (slack >= 3D)
 // then passes every such box: its exact left side is <= t*(1+5u)(1-2^-19) + D - slack <= t*(1-5u) - 2D
 // - 22u t*, which leaves 22u t* + D to absorb the FMA's rounding (<= u (tnear^ + slack)).  It may pass a
-// few more boxes, never fewer: no primitive the reference's f64 test reaches is culled.  Empty slots are
-// masked by their entry (ENTRY_EMPTY).  Slopes are clamped to |inv| <= 2^64 (axis-parallel rays) and
-// frames to |o|, 255 s <= 2^56 (rp_layout.h COORD_MAX), so every A, B and t^ is finite; an A that
-// underflows to a subnormal or zero errs by < 2^-118, inside the 2^-100 slack floor.
+// few more boxes, never fewer: no primitive the reference's f64 test reaches is culled.  Empty slots fail
+// (Node4: lo = +inf, hi = -inf gives t_near = +inf; Node4Q: masked by their entry).  Slopes are clamped to
+// |inv| <= 2^64 (axis-parallel rays) and frames to |o|, 255 s <= 2^56 (rp_layout.h COORD_MAX), so every
+// A, B and t^ is finite; an A that underflows errs by < 2^-118, inside the 2^-100 slack floor.
 struct Ray32 {
   float ix, iy, iz;     // rcp(fl(d))
   float oix, oiy, oiz;  // fl(o32 * inv)
   float slack;          // >= 3D (per ray)
   float tmin;           // t_min rounded down
-  uint32_t sx, sy, sz;  // v_perm_b32 selector per axis: picks the near plane codes (lo_* or hi_*, by the
-                        // sign of the slope) out of the {hi, lo} word pair, the far codes out of {lo, hi}
+  uint32_t sx, sy, sz;  // per axis, by the sign of the slope: Node4 = byte offset of the near plane row
+                        // (lo_* or hi_*; the far row is the other); Node4Q = v_perm_b32 selector picking the
+                        // near plane codes out of the {hi, lo} word pair (the far codes out of {lo, hi})
 };
 
 // next representable float towards +inf / -inf (finite inputs; the callers only step values that
@@ -403,6 +404,7 @@ RPK_INLINE float f32_up(double x) {
   return (double)f < x ? next_up(f) : f;
 }
 
+template <uint32_t NF>
 RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
   const float ox = (float)o.x, oy = (float)o.y, oz = (float)o.z;
   // |inv| clamped to 2^64: a zero direction component gives a huge finite slope instead of inf, so the
@@ -416,21 +418,28 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
   r.oiz = oz * r.iz;
   // |o - o32| is exact in f64 (Sterbenz); an axis with no origin rounding contributes no origin term
   const double ex = fabs(o.x - (double)ox), ey = fabs(o.y - (double)oy), ez = fabs(o.z - (double)oz);
-  // the frame term (e above) vanishes on an axis-parallel axis through 0 (inv = +-2^64, o32 = 0): A = s inv
-  // and B = o inv are then exact
   const double k = 1.0 + 0x1p-20, u = 0x1p-23, q2 = 2.0 * qbound;
-  const auto fr = [&](float inv, float o32) {
-    return (fabsf(inv) == 0x1p64f && o32 == 0.0f) ? 0.0 : fabs((double)inv) * (q2 + fabs((double)o32)) * u * k;
+  const auto fr = [&](float inv, float o32) {  // the Node4Q frame term e (see above)
+    return (NF != rpl::NODES_Q8 || (fabsf(inv) == 0x1p64f && o32 == 0.0f))
+               ? 0.0
+               : fabs((double)inv) * (q2 + fabs((double)o32)) * u * k;
   };
   double D = 0.0;
   D = fmax(D, (ex == 0.0 ? 0.0 : ex * fabs((double)r.ix) * k) + fabs((double)r.oix) * u + fr(r.ix, ox));
   D = fmax(D, (ey == 0.0 ? 0.0 : ey * fabs((double)r.iy) * k) + fabs((double)r.oiy) * u + fr(r.iy, oy));
   D = fmax(D, (ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)r.oiz) * u + fr(r.iz, oz));
-  r.slack = f32_up(3.0 * D * k + 0x1p-100);
+  r.slack = f32_up(3.0 * D * k + (NF == rpl::NODES_Q8 ? 0x1p-100 : 0x1p-126));
   r.tmin = f32_down(tmin);
-  r.sx = r.ix < 0.0f ? 0x07060504u : 0x03020100u;
-  r.sy = r.iy < 0.0f ? 0x07060504u : 0x03020100u;
-  r.sz = r.iz < 0.0f ? 0x07060504u : 0x03020100u;
+  if (NF == rpl::NODES_Q8) {
+    r.sx = r.ix < 0.0f ? 0x07060504u : 0x03020100u;
+    r.sy = r.iy < 0.0f ? 0x07060504u : 0x03020100u;
+    r.sz = r.iz < 0.0f ? 0x07060504u : 0x03020100u;
+  } else {
+    // Node4: lo_x at 0, hi_x at 16, lo_y at 32, hi_y at 48, lo_z at 64, hi_z at 80
+    r.sx = r.ix < 0.0f ? 16u : 0u;
+    r.sy = r.iy < 0.0f ? 48u : 32u;
+    r.sz = r.iz < 0.0f ? 80u : 64u;
+  }
 }
 
 // Closest hit over the 4-wide BVH (the reference's Hittable::Bvh::hit, bvh.rs:121-124 / hit_node
@@ -548,7 +557,7 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride
 
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
-template <bool SPILL>
+template <bool SPILL, uint32_t NF>
 RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
@@ -559,36 +568,61 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
   while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
     DREG(DREG_NODE)
-    // Near/far planes chosen per ray by the slope signs (octant): one v_perm_b32 per axis and side picks
-    // the four children's near (far) plane codes out of the {lo, hi} code words, so each child costs one
-    // max3 + max for t_near and one min3 + min for t_far.  For a valid box this is the same pair of values
-    // the min/max slab form picks (t^ is monotone in q).
-    // 32-bit byte offsets from the (wave-uniform) node base: scalar-base + vector-offset addressing
+    // Near/far planes chosen per ray by the slope signs (octant), so each child costs one max3 + max for
+    // t_near and one min3 + min for t_far: for a valid box the same pair of values the min/max slab form
+    // picks (t^ is monotone in the plane coordinate).  Node4 picks the near/far rows by address; Node4Q
+    // picks the four children's near (far) plane codes out of the {lo, hi} code words with one v_perm_b32
+    // per axis and side.  32-bit byte offsets from the (wave-uniform) node base: scalar-base +
+    // vector-offset addressing.
     const char* nb = reinterpret_cast<const char*>(S.nodes);
-    const uint32_t no = cur << 6;
-    const float4 c0 = *reinterpret_cast<const float4*>(nb + no);           // o.x o.y o.z s.x
-    const uint4 c1 = *reinterpret_cast<const uint4*>(nb + (no + 16u));     // s.y s.z lo_x hi_x
-    const uint4 c2 = *reinterpret_cast<const uint4*>(nb + (no + 32u));     // lo_y hi_y lo_z hi_z
-    const uint4 ch = *reinterpret_cast<const uint4*>(nb + (no + 48u));
+    f2 NX[2], FX[2], NY[2], FY[2], NZ[2], FZ[2];
+    uint4 ch;
+    if constexpr (NF == rpl::NODES_Q8) {
+      const uint32_t no = cur << 6;
+      const float4 c0 = *reinterpret_cast<const float4*>(nb + no);        // o.x o.y o.z s.x
+      const uint4 c1 = *reinterpret_cast<const uint4*>(nb + (no + 16u));  // s.y s.z lo_x hi_x
+      const uint4 c2 = *reinterpret_cast<const uint4*>(nb + (no + 32u));  // lo_y hi_y lo_z hi_z
+      ch = *reinterpret_cast<const uint4*>(nb + (no + 48u));
+      // per axis: A = s inv, B = fma(o, inv, -oinv); plane t^ = fma(q, A, B)
+      const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
+      const float Bx = fmaf(c0.x, r.ix, -r.oix), By = fmaf(c0.y, r.iy, -r.oiy), Bz = fmaf(c0.z, r.iz, -r.oiz);
+      const uint32_t qnx = __builtin_amdgcn_perm(c1.w, c1.z, r.sx), qfx = __builtin_amdgcn_perm(c1.z, c1.w, r.sx);
+      const uint32_t qny = __builtin_amdgcn_perm(c2.y, c2.x, r.sy), qfy = __builtin_amdgcn_perm(c2.x, c2.y, r.sy);
+      const uint32_t qnz = __builtin_amdgcn_perm(c2.w, c2.z, r.sz), qfz = __builtin_amdgcn_perm(c2.z, c2.w, r.sz);
+      // children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the same per-element
+      // rounding as fmaf; byte b of a code word converts with v_cvt_f32_ubyte<b>
+      const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az}, bx = {Bx, Bx}, by = {By, By}, bz = {Bz, Bz};
+#define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        NX[q] = pk_fma(RPK_Q2(qnx, q), ax, bx);
+        FX[q] = pk_fma(RPK_Q2(qfx, q), ax, bx);
+        NY[q] = pk_fma(RPK_Q2(qny, q), ay, by);
+        FY[q] = pk_fma(RPK_Q2(qfy, q), ay, by);
+        NZ[q] = pk_fma(RPK_Q2(qnz, q), az, bz);
+        FZ[q] = pk_fma(RPK_Q2(qfz, q), az, bz);
+      }
+#undef RPK_Q2
+    } else {
+      const uint32_t no = cur << 7;
+      const float4 nx = *reinterpret_cast<const float4*>(nb + (no + r.sx));
+      const float4 fx = *reinterpret_cast<const float4*>(nb + (no + (r.sx ^ 16u)));
+      const float4 ny = *reinterpret_cast<const float4*>(nb + (no + r.sy));
+      const float4 fy = *reinterpret_cast<const float4*>(nb + (no + (r.sy ^ 16u)));
+      const float4 nz = *reinterpret_cast<const float4*>(nb + (no + r.sz));
+      const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.sz ^ 16u)));
+      ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
+      const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+      const f2 nox = {-r.oix, -r.oix}, noy = {-r.oiy, -r.oiy}, noz = {-r.oiz, -r.oiz};
+      NX[0] = pk_fma(f2{nx.x, nx.y}, ix, nox); NX[1] = pk_fma(f2{nx.z, nx.w}, ix, nox);
+      FX[0] = pk_fma(f2{fx.x, fx.y}, ix, nox); FX[1] = pk_fma(f2{fx.z, fx.w}, ix, nox);
+      NY[0] = pk_fma(f2{ny.x, ny.y}, iy, noy); NY[1] = pk_fma(f2{ny.z, ny.w}, iy, noy);
+      FY[0] = pk_fma(f2{fy.x, fy.y}, iy, noy); FY[1] = pk_fma(f2{fy.z, fy.w}, iy, noy);
+      NZ[0] = pk_fma(f2{nz.x, nz.y}, iz, noz); NZ[1] = pk_fma(f2{nz.z, nz.w}, iz, noz);
+      FZ[0] = pk_fma(f2{fz.x, fz.y}, iz, noz); FZ[1] = pk_fma(f2{fz.z, fz.w}, iz, noz);
+    }
     float tn[4];
     uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
-    // per axis: A = s inv, B = fma(o, inv, -oinv); plane t^ = fma(q, A, B)
-    const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
-    const float Bx = fmaf(c0.x, r.ix, -r.oix), By = fmaf(c0.y, r.iy, -r.oiy), Bz = fmaf(c0.z, r.iz, -r.oiz);
-    const uint32_t qnx = __builtin_amdgcn_perm(c1.w, c1.z, r.sx), qfx = __builtin_amdgcn_perm(c1.z, c1.w, r.sx);
-    const uint32_t qny = __builtin_amdgcn_perm(c2.y, c2.x, r.sy), qfy = __builtin_amdgcn_perm(c2.x, c2.y, r.sy);
-    const uint32_t qnz = __builtin_amdgcn_perm(c2.w, c2.z, r.sz), qfz = __builtin_amdgcn_perm(c2.z, c2.w, r.sz);
-    // slab planes of children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the
-    // same per-element rounding as fmaf; byte b of a code word converts with v_cvt_f32_ubyte<b>
-    const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az}, bx = {Bx, Bx}, by = {By, By}, bz = {Bz, Bz};
-#define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
-    const f2 NX[2] = {pk_fma(RPK_Q2(qnx, 0), ax, bx), pk_fma(RPK_Q2(qnx, 1), ax, bx)};
-    const f2 FX[2] = {pk_fma(RPK_Q2(qfx, 0), ax, bx), pk_fma(RPK_Q2(qfx, 1), ax, bx)};
-    const f2 NY[2] = {pk_fma(RPK_Q2(qny, 0), ay, by), pk_fma(RPK_Q2(qny, 1), ay, by)};
-    const f2 FY[2] = {pk_fma(RPK_Q2(qfy, 0), ay, by), pk_fma(RPK_Q2(qfy, 1), ay, by)};
-    const f2 NZ[2] = {pk_fma(RPK_Q2(qnz, 0), az, bz), pk_fma(RPK_Q2(qnz, 1), az, bz)};
-    const f2 FZ[2] = {pk_fma(RPK_Q2(qfz, 0), az, bz), pk_fma(RPK_Q2(qfz, 1), az, bz)};
-#undef RPK_Q2
     f2 TN[2], TF[2];
 #pragma unroll
     for (int q = 0; q < 2; q++) {
@@ -602,7 +636,8 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
 #pragma unroll
       for (int e = 0; e < 2; e++) {
         const int c = 2 * q + e;
-        tn[c] = (lhs[e] <= TF[q][e] && cc[c] != rpl::ENTRY_EMPTY) ? TN[q][e] : __builtin_huge_valf();
+        const bool hit = lhs[e] <= TF[q][e] && (NF != rpl::NODES_Q8 || cc[c] != rpl::ENTRY_EMPTY);
+        tn[c] = hit ? TN[q][e] : __builtin_huge_valf();
       }
     }
     // sort (tn, entry) ascending: misses (+inf) go last
@@ -692,13 +727,14 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
   ts.leaf = leaf;
 }
 
+template <uint32_t NF>
 RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V3 d, double tmin, double tmax,
                          HitRec& hr, bool& overflow, TravDiag* td = nullptr) {
   Ray32 r;
-  setup_ray32(o, d, tmin, S.qbound, r);
+  setup_ray32<NF>(o, d, tmin, S.qbound, r);
   TravState t;
   trav_begin(S, o, d, tmin, tmax, t);
-  while (!trav_done(t)) trav_step<false>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
+  while (!trav_done(t)) trav_step<false, NF>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
   hr.u = t.bu;
   hr.v = t.bv;
@@ -1072,6 +1108,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.always_first = A->S.always_first;
   S.n_always = A->S.n_always;
   S.qbound = A->S.qbound;
+  S.node_format = A->S.node_format;
   S.stack_depth = A->S.stack_depth;
   S.lds_depth = A->S.lds_depth;
   S.spill = A->S.spill;

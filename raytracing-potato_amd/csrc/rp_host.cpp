@@ -411,7 +411,8 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba) {
   return RP_OK;
 }
 
-int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint64_t* per_ray) {
+int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
+                            uint64_t* per_ray) {
   // CPU model of rp_device.h's traversal over the same packed 4-wide tree: quantized child boxes tested
   // in f32 (t = fma(q, s inv, fma(o, inv, -oinv)) + slack, rcp emulated by a correctly rounded 1/x, the
   // min/max slab form instead of the device's octant selection: the same values), near-first order, exact f64
@@ -421,8 +422,11 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   int rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(err);
   rpb::PackedScene ps;
-  rc = rpb::build(desc, rpb::BuildOptions(), ps, err);
+  rpb::BuildOptions bo;
+  bo.node_format = node_format;
+  rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(err);
+  const bool q8 = ps.node_format == rpl::NODES_Q8;
   auto down = [](double x) { float f = (float)x; if ((double)f > x) f = std::nextafter(f, -INFINITY); return f; };
   auto up = [](double x) { float f = (float)x; if ((double)f < x) f = std::nextafter(f, INFINITY); return f; };
   for (uint64_t r = 0; r < n; r++) {
@@ -437,7 +441,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
       oinv[k] = o32 * inv[k];
       const double e = std::fabs(o[k] - (double)o32);
       D = std::fmax(D, (e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv[k]) * 0x1p-23 +
-                           ((std::fabs(inv[k]) == 0x1p64f && o32 == 0.0f)
+                           ((!q8 || (std::fabs(inv[k]) == 0x1p64f && o32 == 0.0f))
                                 ? 0.0
                                 : std::fabs((double)inv[k]) * (2.0 * ps.qbound + std::fabs((double)o32)) * 0x1p-23 * (1.0 + 0x1p-20)));
     }
@@ -492,26 +496,47 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
     for (;;) {
       while (!(cur & rpl::ENTRY_LEAF)) {
         visits++;
-        const rpl::Node4& nd = ps.nodes[cur];
+        float lo4[4][3], hi4[4][3];
+        const uint32_t* child;
+        if (q8) {
+          const rpl::Node4Q& nd = ps.qnodes[cur];
+          float A[3], B[3];
+          for (int k = 0; k < 3; k++) {
+            A[k] = nd.s[k] * inv[k];
+            B[k] = std::fma(nd.o[k], inv[k], -oinv[k]);
+          }
+          const uint8_t* L[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
+          const uint8_t* H[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
+          // plane t values directly: t = fma(q, A, B) (the device's dequantized form)
+          for (int c = 0; c < 4; c++)
+            for (int k = 0; k < 3; k++) {
+              lo4[c][k] = std::fma((float)L[k][c], A[k], B[k]);
+              hi4[c][k] = std::fma((float)H[k][c], A[k], B[k]);
+            }
+          child = nd.child;
+        } else {
+          const rpl::Node4& nd = ps.nodes[cur];
+          const float* lo[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
+          const float* hi[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
+          for (int c = 0; c < 4; c++)
+            for (int k = 0; k < 3; k++) {
+              lo4[c][k] = std::fma(lo[k][c], inv[k], -oinv[k]);
+              hi4[c][k] = std::fma(hi[k][c], inv[k], -oinv[k]);
+            }
+          child = nd.child;
+        }
         float tn[4];
         uint32_t cc[4];
-        float A[3], B[3];
-        for (int k = 0; k < 3; k++) {
-          A[k] = nd.s[k] * inv[k];
-          B[k] = std::fma(nd.o[k], inv[k], -oinv[k]);
-        }
         for (int c = 0; c < 4; c++) {
-          const float lo[3] = {(float)nd.lo_x[c], (float)nd.lo_y[c], (float)nd.lo_z[c]};
-          const float hi[3] = {(float)nd.hi_x[c], (float)nd.hi_y[c], (float)nd.hi_z[c]};
           float tnear = tmin32, tfar = best32;
           for (int k = 0; k < 3; k++) {
-            const float a = std::fma(lo[k], A[k], B[k]), b = std::fma(hi[k], A[k], B[k]);
+            const float a = lo4[c][k], b = hi4[c][k];
             tnear = std::fmax(tnear, std::fmin(a, b));
             tfar = std::fmin(tfar, std::fmax(a, b));
           }
-          const bool hit = std::fma(tnear, 1.0f - 0x1p-19f, -slack) <= tfar && nd.child[c] != rpl::ENTRY_EMPTY;
+          const bool hit = std::fma(tnear, 1.0f - 0x1p-19f, -slack) <= tfar && child[c] != rpl::ENTRY_EMPTY;
           tn[c] = hit ? tnear : INFINITY;
-          cc[c] = nd.child[c];
+          cc[c] = child[c];
         }
         for (int a = 0; a < 4; a++)  // stable sort by tn (matches the device network for distinct keys)
           for (int b = a + 1; b < 4; b++)
@@ -535,12 +560,14 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   return RP_OK;
 }
 
-int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats) {
+int rph_bvh_selfcheck(const rp_scene_desc* desc, uint32_t node_format, uint64_t* stats) {
   std::string err;
   int rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(err);
   rpb::PackedScene ps;
-  rc = rpb::build(desc, rpb::BuildOptions(), ps, err);
+  rpb::BuildOptions bo;
+  bo.node_format = node_format;
+  rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(err);
   rc = rpb::check(ps, err);
   if (rc != RP_OK) {
@@ -548,11 +575,33 @@ int rph_bvh_selfcheck(const rp_scene_desc* desc, uint64_t* stats) {
     return rc;
   }
   if (stats) {
-    stats[0] = ps.nodes.size();
+    stats[0] = ps.n_nodes();
     stats[1] = ps.n_leaves;
     stats[2] = ps.max_depth;
     stats[3] = desc->n_hittables;
   }
+  return RP_OK;
+}
+
+int rph_bvh_tree_hash(const rp_scene_desc* desc, uint32_t node_format, uint32_t threads, uint64_t* hash) {
+  std::string err;
+  int rc = rpb::validate(desc, err);
+  if (rc != RP_OK) return fail(err);
+  rpb::PackedScene ps;
+  rpb::BuildOptions bo;
+  bo.node_format = node_format;
+  bo.threads = threads;
+  rc = rpb::build(desc, bo, ps, err);
+  if (rc != RP_OK) return fail(err);
+  uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over the packed records
+  auto mix = [&](const void* p, size_t n) {
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
+  };
+  if (ps.node_format == rpl::NODES_Q8) mix(ps.qnodes.data(), ps.qnodes.size() * sizeof(rpl::Node4Q));
+  else mix(ps.nodes.data(), ps.nodes.size() * sizeof(rpl::Node4));
+  mix(ps.prim_refs.data(), ps.prim_refs.size() * sizeof(rpl::PrimRef));
+  *hash = h;
   return RP_OK;
 }
 

@@ -7,7 +7,7 @@
 namespace rpk {
 
 struct KScene {
-  const rpl::Node4* nodes;
+  const void* nodes;     // rpl::Node4 or rpl::Node4Q records (node_format)
   const rpl::Prim* prims;
   const rpl::PrimRef* prim_refs;
   const double* vnrm;
@@ -18,7 +18,8 @@ struct KScene {
   rpl::Emit background;
   uint32_t root;
   uint32_t always_first, n_always;  // prims tested before the tree for every ray (rp_bvh.h BuildOptions)
-  double qbound;         // bound on every node frame's |o| and 255 s (rp_layout.h qbound): the slab slack
+  double qbound;         // Node4Q: bound on every node frame's |o| and 255 s (rp_layout.h qbound): the slab slack
+  uint32_t node_format;  // rpl::NODES_F32 / NODES_Q8: picks the kernel instantiation
   uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
   uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
@@ -123,7 +124,7 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
                           void* stream);
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
-int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
+int render_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t node_format, int* blocks);
 
 // Stage-split engine (rp_wavefront.hip): the path-slot pool of a workspace, structure-of-arrays in device
 // memory, and the host loop of trace / shade passes (synchronous: it polls the ray-queue length every
@@ -137,7 +138,7 @@ struct WfBuffers {
 };
 int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
                      uint32_t* queue, const WfBuffers& b, int trace_grid, void* stream);
-int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks);
+int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t node_format, int* blocks);
 
 // Closest-hit query kernel (one ray per thread).
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,

@@ -27,7 +27,7 @@ namespace rpk {
 #endif
 // PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
 // and timings of the frame kernel never mix with it.
-template <bool PROBE, bool SPILL>
+template <bool PROBE, bool SPILL, uint32_t NF>
 __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KArgs args) {
   extern __shared__ uint32_t lds_stack[];
   __shared__ unsigned long long blk_ctr[3];
@@ -151,14 +151,14 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         newray = false;
       }
       Ray32 r;
-      setup_ray32(o, d, RAY_EPSILON, S.qbound, r);
+      setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
       for (;;) {
         if (alive && !tdone) {
           DREG(DREG_STEP)
 #ifdef RPK_DIAG
-          trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
+          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
 #else
-          trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
 #endif
           tdone = trav_done(ts);
         }
@@ -290,6 +290,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   if (threadIdx.x < 3) atomicAdd(&ctr[CTR_RAYS + threadIdx.x], blk_ctr[threadIdx.x]);
 }
 
+template <uint32_t NF>
 __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const double* __restrict__ rays, uint64_t n,
                                                          double* __restrict__ out_hit, uint32_t* __restrict__ out_mat,
                                                          unsigned long long* __restrict__ ctr) {
@@ -301,7 +302,7 @@ __global__ void __launch_bounds__(BLOCK) intersect_kernel(const KScene S, const 
   const double tmin = q[6], tmax = q[7];
   HitRec hr;
   bool overflow = false;
-  traverse(S, (lds_u32*)(lds_stack + threadIdx.x), BLOCK, o, d, tmin, tmax, hr, overflow);
+  traverse<NF>(S, (lds_u32*)(lds_stack + threadIdx.x), BLOCK, o, d, tmin, tmax, hr, overflow);
   double* oh = out_hit + 9 * i;
   if (hr.prim >= 0) {
     Surf h;
@@ -332,10 +333,19 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   a.ctr = reinterpret_cast<unsigned long long*>(counters);
   a.queue = queue;
   a.diag = reinterpret_cast<unsigned long long*>(s.diag);
-  if (p.probe && spill) hipLaunchKernelGGL((render_kernel<true, true>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
-  else if (p.probe) hipLaunchKernelGGL((render_kernel<true, false>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
-  else if (spill) hipLaunchKernelGGL((render_kernel<false, true>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL((render_kernel<false, false>), dim3(grid), dim3(BLOCK), lds, (hipStream_t)stream, a);
+  const hipStream_t st = (hipStream_t)stream;
+#define RPK_LAUNCH(P_, S_)                                                                                   \
+  do {                                                                                                   \
+    if (s.node_format == rpl::NODES_Q8)                                                                  \
+      hipLaunchKernelGGL((render_kernel<P_, S_, rpl::NODES_Q8>), dim3(grid), dim3(BLOCK), lds, st, a);   \
+    else                                                                                                 \
+      hipLaunchKernelGGL((render_kernel<P_, S_, rpl::NODES_F32>), dim3(grid), dim3(BLOCK), lds, st, a);  \
+  } while (0)
+  if (p.probe && spill) RPK_LAUNCH(true, true);
+  else if (p.probe) RPK_LAUNCH(true, false);
+  else if (spill) RPK_LAUNCH(false, true);
+  else RPK_LAUNCH(false, false);
+#undef RPK_LAUNCH
   return (int)hipGetLastError();
 }
 
@@ -476,10 +486,14 @@ int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32
 
 uint64_t rng_slab_bytes_per_lane() { return (uint64_t)SLAB_N * sizeof(uint4); }
 
-int render_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks) {
+int render_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t nf, int* blocks) {
   const size_t lds = (size_t)lds_depth * BLOCK * sizeof(uint32_t);
-  if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true>, BLOCK, lds);
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false>, BLOCK, lds);
+  if (nf == rpl::NODES_Q8) {
+    if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true, rpl::NODES_Q8>, BLOCK, lds);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false, rpl::NODES_Q8>, BLOCK, lds);
+  }
+  if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true, rpl::NODES_F32>, BLOCK, lds);
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false, rpl::NODES_F32>, BLOCK, lds);
 }
 
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,
@@ -487,8 +501,12 @@ int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* ou
   if (n == 0) return 0;
   const size_t lds = (size_t)s.stack_depth * BLOCK * sizeof(uint32_t);
   const uint64_t grid = (n + BLOCK - 1) / BLOCK;
-  hipLaunchKernelGGL(intersect_kernel, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s, rays, n,
-                     out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
+  if (s.node_format == rpl::NODES_Q8)
+    hipLaunchKernelGGL(intersect_kernel<rpl::NODES_Q8>, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s,
+                       rays, n, out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
+  else
+    hipLaunchKernelGGL(intersect_kernel<rpl::NODES_F32>, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s,
+                       rays, n, out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
   return (int)hipGetLastError();
 }
 

@@ -3,8 +3,8 @@
 //
 // Layout rationale (DESIGN.md "Data layout in HBM"): traversal is one ray per lane, so neighbouring
 // lanes read unrelated nodes; what matters is that one lane's node fetch is a few wide (16 B) loads
-// from one 64 B record.  Each wide node stores all four children's boxes (the parent tests them with
-// one fetch), quantized against the node's own frame, and primitives are stored contiguously in leaf
+// from one 128 B (or 64 B) record.  Each wide node stores all four children's boxes (the parent tests them
+// with one fetch), and primitives are stored contiguously in leaf
 // order with the triangle operands pre-subtracted exactly as hittable.rs:71-72 computes them.
 #pragma once
 #include <math.h>
@@ -12,19 +12,33 @@
 
 namespace rpl {
 
-// 4-wide BVH node: 64 B, four 16 B loads per lane fetch.  The four child boxes are quantized to 8 bits
-// per plane in a per-node frame (per axis an f32 origin o and step s: plane(q) = o + q * s, exact in f64,
-// q = 0..255), rounded OUTWARD from the exact f64 boxes, and tested with a conservative slab test
-// (rp_device.h trav_step) so no primitive the exact f64 test would accept is ever culled.
-//   16 B chunks: {o.x, o.y, o.z, s.x} {s.y, s.z, lo_x, hi_x} {lo_y, hi_y, lo_z, hi_z} {child[4]}
-// The traversal kernel is bound by the vector-memory data path (one TA/TD cycle per lane per load
-// instruction): halving the node from 7 to 4 loads per visit is the lever; the
-// dequantization (v_cvt_f32_ubyte + the same one FMA per plane) costs ALU that was idle.
-// Child entries:
+// Two 4-wide node formats, chosen per scene (rp_scene_options.node_format; rp_api.cpp picks by size):
+//
+// Node4 (128 B, cache-resident trees): the four child boxes per axis (SoA within the record: 6 float4
+// loads + the children) in f32, rounded OUTWARD from the exact f64 boxes.
+//
+// Node4Q (64 B, large trees): the child boxes quantized to 8 bits per plane in a per-node frame (per axis an
+// f32 origin o and step s: plane(q) = o + q * s, exact in f64, q = 0..255), rounded outward from the exact
+// f64 boxes.  16 B chunks: {o.x, o.y, o.z, s.x} {s.y, s.z, lo_x, hi_x} {lo_y, hi_y, lo_z, hi_z} {child[4]}.
+// Four loads per visit instead of seven; the dequantization (v_perm + v_cvt_f32_ubyte per plane, the same
+// one FMA) costs ALU.  Measured: C5 (10 M triangles, SAH tree) -4.4 % frame time,
+// C3 (bunny, L2-resident) +0.7 %.
+//
+// Both are tested with a conservative slab test (rp_device.h trav_step) so no primitive the exact f64
+// test would accept is ever culled.  Child entries:
 //   inner node : node index (bit 31 clear)
 //   leaf       : ENTRY_LEAF | (count - 1) << LEAF_SHIFT | first primitive   (count 1..8)
-//   empty slot : ENTRY_EMPTY (its plane bytes are meaningless; the traversal masks it by the entry)
+//   empty slot : ENTRY_EMPTY (Node4: lo = +inf, hi = -inf; Node4Q: plane bytes meaningless, masked by the entry)
 struct alignas(16) Node4 {
+  float lo_x[4], hi_x[4];
+  float lo_y[4], hi_y[4];
+  float lo_z[4], hi_z[4];
+  uint32_t child[4];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Node4) == 128, "Node4 must be 128 B");
+
+struct alignas(16) Node4Q {
   float o[3];  // frame origin per axis
   float s[3];  // frame step per axis
   uint8_t lo_x[4], hi_x[4];
@@ -32,7 +46,9 @@ struct alignas(16) Node4 {
   uint8_t lo_z[4], hi_z[4];
   uint32_t child[4];
 };
-static_assert(sizeof(Node4) == 64, "Node4 must be 64 B");
+static_assert(sizeof(Node4Q) == 64, "Node4Q must be 64 B");
+
+enum : uint32_t { NODES_F32 = 1, NODES_Q8 = 2 };  // = RP_NODES_F32 / RP_NODES_Q8 (include/rp.h)
 
 #if defined(__HIPCC__)
 #define RPL_HD __host__ __device__
@@ -40,12 +56,7 @@ static_assert(sizeof(Node4) == 64, "Node4 must be 64 B");
 #define RPL_HD
 #endif
 
-// Node frames.  qframe(lo, hi) picks the frame of a node box [lo, hi] along one axis (finite, lo <= hi):
-//   o <= lo and o + 255 s >= hi;
-//   o is a multiple of 2^(E_s - 8) (E_s = floor(log2 s)) or, far from 0, of its own ulp (>= 2^(E_s - 8)),
-//   and |o| < 2^(E_s + 29), so o + q s is a multiple of 2^(E_s - 23) below 2^(E_s + 30): exact in f64;
-//   s >= (hi - lo) (1 + 2^-7) / 255 leaves room for o's rounding below lo;  s >= 2^-60.
-// plane_q(o, s, q) is that exact value; q_down / q_up the conservative quantization of a child's bounds.
+// f64 -> f32 rounded towards -inf / +inf; Node4 child boxes rounded outward
 RPL_HD inline float f32_rd(double x) {
   float f = (float)x;
   if ((double)f > x) f = nextafterf(f, -__builtin_huge_valf());
@@ -56,6 +67,22 @@ RPL_HD inline float f32_ru(double x) {
   if ((double)f < x) f = nextafterf(f, __builtin_huge_valf());
   return f;
 }
+RPL_HD inline void f32_child(Node4& n, int c, const double lo[3], const double hi[3]) {
+  n.lo_x[c] = f32_rd(lo[0]); n.hi_x[c] = f32_ru(hi[0]);
+  n.lo_y[c] = f32_rd(lo[1]); n.hi_y[c] = f32_ru(hi[1]);
+  n.lo_z[c] = f32_rd(lo[2]); n.hi_z[c] = f32_ru(hi[2]);
+}
+RPL_HD inline void f32_empty(Node4& n, int c) {
+  n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = __builtin_huge_valf();
+  n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = -__builtin_huge_valf();
+}
+
+// Node frames.  qframe(lo, hi) picks the frame of a node box [lo, hi] along one axis (finite, lo <= hi):
+//   o <= lo and o + 255 s >= hi;
+//   o is a multiple of 2^(E_s - 8) (E_s = floor(log2 s)) or, far from 0, of its own ulp (>= 2^(E_s - 8)),
+//   and |o| < 2^(E_s + 29), so o + q s is a multiple of 2^(E_s - 23) below 2^(E_s + 30): exact in f64;
+//   s >= (hi - lo) (1 + 2^-7) / 255 leaves room for o's rounding below lo;  s >= 2^-60.
+// plane_q(o, s, q) is that exact value; q_down / q_up the conservative quantization of a child's bounds.
 RPL_HD inline double plane_q(float o, float s, uint32_t q) { return (double)o + (double)q * (double)s; }
 RPL_HD inline void qframe(double lo, double hi, float& o, float& s) {
   const float o0 = f32_rd(lo);
@@ -94,7 +121,7 @@ constexpr double COORD_MAX = 0x1p54;
 
 // Quantize child c of node n from its exact f64 box (lo[3], hi[3]); a non-finite bound (NaN geometry: never
 // hit) takes the whole frame.
-RPL_HD inline void quantize_child(Node4& n, int c, const double lo[3], const double hi[3]) {
+RPL_HD inline void quantize_child(Node4Q& n, int c, const double lo[3], const double hi[3]) {
   uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
   uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
   for (int a = 0; a < 3; a++) {
@@ -103,7 +130,7 @@ RPL_HD inline void quantize_child(Node4& n, int c, const double lo[3], const dou
     H[a][c] = ok ? (uint8_t)q_up(hi[a], n.o[a], n.s[a]) : (uint8_t)255;
   }
 }
-RPL_HD inline void empty_child(Node4& n, int c) {
+RPL_HD inline void empty_child(Node4Q& n, int c) {
   n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = 255;
   n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = 0;
 }

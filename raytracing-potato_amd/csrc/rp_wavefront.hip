@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
 #ifndef RPK_WF_REFILL
 #define RPK_WF_REFILL 16
 #endif
-template <bool SPILL>
+template <bool SPILL, uint32_t NF>
 __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const WfArgs w) {
   extern __shared__ uint32_t lds_stack[];
   lds_u32* stk = (lds_u32*)(lds_stack + threadIdx.x);
@@ -285,7 +285,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
           o = v3(w.in.ray[q], w.in.ray[P + q], w.in.ray[2 * P + q]);
           d = v3(w.in.ray[3 * P + q], w.in.ray[4 * P + q], w.in.ray[5 * P + q]);
           const KScene S = load_scene(kargs());
-          setup_ray32(o, d, RAY_EPSILON, S.qbound, r);
+          setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
           trav_init(S, INF, ts);
           double best = ts.best;
           for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++)
@@ -301,7 +301,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
     if (have) {
       const KScene S = load_scene(kargs());
       const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + tid) * (S.stack_depth - S.lds_depth) : 0u;
-      trav_step<SPILL>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+      trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
       if (trav_done(ts)) {
         w.hit[q] = ts.best;
         w.hit[P + q] = ts.bu;
@@ -358,8 +358,13 @@ int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* 
   for (uint32_t it = 1;; it++) {
     if (it > bound) return (int)hipErrorUnknown;
     set(cur);
-    if (spill) hipLaunchKernelGGL(wf_trace_kernel<true>, dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
-    else hipLaunchKernelGGL(wf_trace_kernel<false>, dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+    if (s.node_format == rpl::NODES_Q8) {
+      if (spill) hipLaunchKernelGGL((wf_trace_kernel<true, rpl::NODES_Q8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+      else hipLaunchKernelGGL((wf_trace_kernel<false, rpl::NODES_Q8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+    } else {
+      if (spill) hipLaunchKernelGGL((wf_trace_kernel<true, rpl::NODES_F32>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+      else hipLaunchKernelGGL((wf_trace_kernel<false, rpl::NODES_F32>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+    }
     hipLaunchKernelGGL(wf_shade_kernel, dim3(sgrid), dim3(BLOCK), 0, st, a, w);
     cur ^= 1u;
     if (it % b.poll == 0) {  // host poll: stop once no ray is queued
@@ -372,10 +377,14 @@ int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* 
   return (int)hipGetLastError();
 }
 
-int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, int* blocks) {
+int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t nf, int* blocks) {
   const size_t lds = (size_t)lds_depth * BLOCK * sizeof(uint32_t);
-  if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<true>, BLOCK, lds);
-  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<false>, BLOCK, lds);
+  if (nf == rpl::NODES_Q8) {
+    if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<true, rpl::NODES_Q8>, BLOCK, lds);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<false, rpl::NODES_Q8>, BLOCK, lds);
+  }
+  if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<true, rpl::NODES_F32>, BLOCK, lds);
+  return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<false, rpl::NODES_F32>, BLOCK, lds);
 }
 
 }  // namespace rpk

@@ -28,6 +28,7 @@ RP_SAMPLES_PER_STREAM = 32
 RP_COMM_ID_BYTES = 128
 RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
 RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
+RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8 = 0, 1, 2
 
 
 class rp_hittable(Structure):
@@ -85,7 +86,7 @@ class rp_scene_options(Structure):
     _fields_ = [("builder", c_uint32), ("max_leaf", c_uint32), ("cost_traverse", c_double),
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
-                ("engine", c_uint32), ("wf_slots", c_uint32), ("reserved", c_uint32 * 2)]
+                ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("reserved", c_uint32)]
 
 
 class rp_stats(Structure):
@@ -122,7 +123,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
               "rp_render_multi"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
-                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_last_error",
+                "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64"]
 
 
@@ -217,8 +218,9 @@ def host() -> ctypes.CDLL:
     lib.rph_lookat.argtypes = [c_double * 3, c_double * 3, c_double * 3, c_double * 9]
     lib.rph_lookat.restype = None
     lib.rph_sky_panorama.argtypes = [c_uint32, c_uint32, c_void_p]
-    lib.rph_bvh_selfcheck.argtypes = [POINTER(rp_scene_desc), POINTER(c_uint64)]
-    lib.rph_bvh_traversal_stats.argtypes = [POINTER(rp_scene_desc), c_void_p, c_uint64, c_void_p]
+    lib.rph_bvh_selfcheck.argtypes = [POINTER(rp_scene_desc), c_uint32, POINTER(c_uint64)]
+    lib.rph_bvh_traversal_stats.argtypes = [POINTER(rp_scene_desc), c_void_p, c_uint64, c_uint32, c_void_p]
+    lib.rph_bvh_tree_hash.argtypes = [POINTER(rp_scene_desc), c_uint32, c_uint32, POINTER(c_uint64)]
     lib.rph_last_error.restype = c_char_p
     lib.rph_stdrng_u64.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p]
     _host = lib

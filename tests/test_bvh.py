@@ -6,19 +6,25 @@ import numpy as np
 import pytest
 
 
-def _selfcheck(scene):
+FORMATS = [1, 2]  # RP_NODES_F32, RP_NODES_Q8
+
+
+def _selfcheck(scene, node_format=0):
     from rtpotato import _ffi as F
     d = scene.desc()
     st = (ctypes.c_uint64 * 4)()
-    rc = F.host().rph_bvh_selfcheck(d.ptr(), st)
+    rc = F.host().rph_bvh_selfcheck(d.ptr(), node_format, st)
     return rc, list(st), (F.host().rph_last_error() or b"").decode()
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("name", ["bunny", "bunny_full", "glass_bunny", "three_balls", "more_balls", "two_balls",
                                   "earth", "one_triangle"])
-def test_catalogue_trees_valid(name):
+def test_catalogue_trees_valid(name, fmt):
+    """Both node formats: every stored child box (f32, or 8-bit planes in the node's frame) contains the
+    exact f64 boxes of its subtree (rpb::check)."""
     from rtpotato import scenes
-    rc, st, err = _selfcheck(scenes.CATALOGUE[name]())
+    rc, st, err = _selfcheck(scenes.CATALOGUE[name](), fmt)
     assert rc == 0, err
     nodes, leaves, depth, prims = st
     assert leaves >= 1 and prims == len(scenes.CATALOGUE[name]().root)
@@ -32,7 +38,8 @@ def test_bunny_tree_shape():
     assert prims == 4969 and nodes < 4969 and depth < 40
 
 
-def test_degenerate_geometry():
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_degenerate_geometry(fmt):
     """Coincident centroids (identical triangles) force the object-median fallback; a lone primitive
     becomes a root leaf next to an empty slot."""
     from rtpotato.scene import (Absorb, Emit, Hittable, Material, Mesh, Scatter, Scene, SceneData, hittables,
@@ -43,16 +50,17 @@ def test_degenerate_geometry():
     pos = np.tile(np.array([[0.0, 0, 0], [1, 0, 0], [0, 1, 0]]), (n, 1))
     mesh = Mesh(pos, np.zeros_like(pos), np.zeros((3 * n, 2)), np.arange(3 * n, dtype=np.uint32))
     sc = Scene(cam, SceneData(mat, [], [mesh]), Hittable.Triangle(mesh.iter_triangles(), 0), Emit.SkyGradient)
-    rc, st, err = _selfcheck(sc)
+    rc, st, err = _selfcheck(sc, fmt)
     assert rc == 0, err
     one = Scene(cam, SceneData(mat, [], []), Hittable.Sphere((0, 0, 0), 1.0, 0), Emit.SkyGradient)
-    rc, st, err = _selfcheck(one)
+    rc, st, err = _selfcheck(one, fmt)
     assert rc == 0 and st[0] == 1 and st[1] == 1, (st, err)
 
 
-def test_random_mesh_tree_valid():
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_random_mesh_tree_valid(fmt):
     from rtpotato import scenes
-    rc, st, err = _selfcheck(scenes.random_mesh(20000))
+    rc, st, err = _selfcheck(scenes.random_mesh(20000), fmt)
     assert rc == 0, err
     assert st[3] == 20000
 
@@ -122,18 +130,20 @@ def _rays_for(scene, n, seed, adversarial=True):
     return rays
 
 
+@pytest.mark.parametrize("fmt", FORMATS)
 @pytest.mark.parametrize("name", ["bunny_full", "more_balls", "one_triangle", "two_balls"])
-def test_conservative_f32_traversal_finds_reference_hits(oracle, name):
-    """The device traversal model (4-wide tree, conservative f32 child boxes, fma slab form) returns the
-    same closest primitive as the oracle's reference traversal (median-split tree, exact f64 boxes) on
-    random and adversarial rays -- the f32 boxes never cull a primitive the f64 test would hit."""
+def test_conservative_f32_traversal_finds_reference_hits(oracle, name, fmt):
+    """The device traversal model (4-wide tree, conservative f32 child boxes or 8-bit quantized ones, fma
+    slab form) returns the same closest primitive as the oracle's reference traversal (median-split tree,
+    exact f64 boxes) on random and adversarial rays -- the stored boxes never cull a primitive the f64 test
+    would hit."""
     from rtpotato import _ffi as F
     from rtpotato import scenes
     scene = scenes.CATALOGUE[name]()
     rays = _rays_for(scene, 40000, 3)
     d = scene.desc()
     out = np.zeros((len(rays), 3), dtype=np.uint64)
-    F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), out.ctypes.data))
+    F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt, out.ctypes.data))
     os_ = oracle.OracleScene(d.addr(), d)
     hits, mats, _ = os_.intersect(rays)
     ref_hit = np.isfinite(hits[:, 0])
@@ -154,14 +164,15 @@ def test_wide_tree_is_shallow():
     import ctypes
     d = scenes.bunny_full().desc()
     st = (ctypes.c_uint64 * 4)()
-    assert F.host().rph_bvh_selfcheck(d.ptr(), st) == 0
+    assert F.host().rph_bvh_selfcheck(d.ptr(), 0, st) == 0
     nodes, leaves, depth, prims = list(st)
     # 4 971 hittables: the 4-wide SAH tree (node cost 0.7 of a primitive test, rp_bvh.h) has ~1 700 nodes
     # at depth 8; the reference's binary median tree has 9 937 nodes at depth 14
     assert depth <= 12 and nodes < 2000, list(st)
 
 
-def test_giant_primitives_tested_first():
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_giant_primitives_tested_first(fmt):
     """The host builder keeps primitives whose box dwarfs the rest of the scene out of the tree and tests
     them first for every ray (rp_bvh.h BuildOptions::always_max): in the C3 scene the ground sphere
     (r = 1000) is tested by every ray, including rays that miss every box of the tree; in earth (one
@@ -175,8 +186,55 @@ def test_giant_primitives_tested_first():
         rays[:1000, 0:3] = np.array([0.0, 5.0, 0.0])
         d = scene.desc()
         out = np.zeros((len(rays), 3), dtype=np.uint64)
-        F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), out.ctypes.data))
+        F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt, out.ctypes.data))
         if always:
             assert (out[:, 1] >= 1).all()
         else:
             assert (out[:1000, 1] == 0).all()
+
+
+def test_quantized_nodes_cost_few_extra_visits():
+    """The 8-bit child boxes are rounded outward to a grid of 1/255 of the node's extent: the same closest hits,
+    at most a few percent more node visits and primitive tests than the f32 boxes (bunny and a 200 k mesh)."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    for scene in (scenes.bunny_full(), scenes.random_mesh(200_000)):
+        rays = _rays_for(scene, 20000, 5, adversarial=False)
+        d = scene.desc()
+        res = []
+        for fmt in FORMATS:
+            out = np.zeros((len(rays), 3), dtype=np.uint64)
+            F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt, out.ctypes.data))
+            res.append(out)
+        assert (res[0][:, 2] == res[1][:, 2]).all()
+        assert res[1][:, 0].mean() <= 1.05 * res[0][:, 0].mean()
+        assert res[1][:, 1].mean() <= 1.10 * res[0][:, 1].mean()
+
+
+def test_quantized_frames_refuse_huge_coordinates():
+    """Node frames need |coordinate| <= 2^54 (rp_layout.h COORD_MAX): larger scenes are refused, not mis-culled."""
+    from rtpotato import _ffi as F
+    from rtpotato.scene import Camera, Emit, Hittable, Material, Scatter, Absorb, Scene, SceneData, Transformation
+    cam = Camera(1.0, 1.0, 1.0, 0.0, Transformation.lookat((0, 0, 3), (0, 0, 0), (0, 1, 0)))
+    mat = [Material.new(Scatter.Lambert, Absorb.Albedo((0.5, 0.5, 0.5)), Emit.None_)]
+    far = Scene(cam, SceneData(mat, [], []), Hittable.Sphere((0, 0, 0), 1e17, 0), Emit.SkyGradient)
+    rc, _, err = _selfcheck(far, 2)
+    assert rc == F.RP_EINVAL and "2^54" in err
+    for fmt in (0, 1):  # auto falls back to the f32 nodes
+        rc, _, err = _selfcheck(far, fmt)
+        assert rc == 0, err
+
+
+@pytest.mark.parametrize("fmt", FORMATS)
+def test_parallel_host_build_is_deterministic(fmt):
+    """The host SAH build splits the top of the tree across threads and builds the subtrees on a pool; the
+    spliced tree (node records, leaf order) is the single-threaded build's bit for bit."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    d = scenes.random_mesh(150_000).desc()
+    hs = []
+    for threads in (1, 3, 8):
+        h = ctypes.c_uint64()
+        F.check_host(F.host().rph_bvh_tree_hash(d.ptr(), fmt, threads, ctypes.byref(h)))
+        hs.append(h.value)
+    assert hs[0] == hs[1] == hs[2], hs

@@ -173,10 +173,12 @@ def test_render_device_torch(gpu):
     assert int(ctr[0]) == st["rays"] and int(ctr[3]) == 0
 
 
+@pytest.mark.parametrize("fmt", ["f32", "q8"])
 @pytest.mark.parametrize("builder", ["host", "gpu"])
-def test_intersect_rays(gpu, builder):
+def test_intersect_rays(gpu, builder, fmt):
     """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle --
-    over the host SAH tree and the device-built LBVH (rp_scene_options.builder)."""
+    over the host SAH tree and the device-built LBVH (rp_scene_options.builder), with f32 or 8-bit quantized
+    child boxes (rp_scene_options.node_format)."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     rng = np.random.default_rng(5)
@@ -193,7 +195,7 @@ def test_intersect_rays(gpu, builder):
     rays[400:600, 7] = rng.uniform(0.1, 3.0, size=200)
     rays[600:700, 0] = 0.0
     rays[600:700, 3] = 0.0
-    with gpu.DeviceScene(scene, options={"builder": builder, "self_check": 1}) as ds:
+    with gpu.DeviceScene(scene, options={"builder": builder, "self_check": 1, "node_format": fmt}) as ds:
         hits, mats = ds.intersect(rays)
     d_ = scene.desc()
     os_ = O.OracleScene(d_.addr(), d_)
@@ -282,14 +284,15 @@ def test_workspaces_frames_in_flight(gpu):
         wss[0].close()  # explicit destroy before the scene; the other one is destroyed with the scene
 
 
+@pytest.mark.parametrize("fmt", ["f32", "q8"])
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000), ("three_balls", None)])
-def test_device_bvh_builder(gpu, name, arg):
-    """Scenes over the device-built tree (rp_bvh_gpu.hip: LBVH + wide collapse), with the host builder's
-    structural self-check on the downloaded tree (options.self_check): same image and ray counts as the
-    oracle."""
+def test_device_bvh_builder(gpu, name, arg, fmt):
+    """Scenes over the device-built tree (rp_bvh_gpu.hip: LBVH + wide collapse) in both node formats, with
+    the host builder's structural self-check on the downloaded tree (options.self_check): same image and ray
+    counts as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
-    opt = {"builder": "gpu", "self_check": 1}
+    opt = {"builder": "gpu", "self_check": 1, "node_format": fmt}
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
     with gpu.DeviceScene(sc, options=opt) as ds:
         info = ds.info()
@@ -297,15 +300,16 @@ def test_device_bvh_builder(gpu, name, arg):
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
+@pytest.mark.parametrize("fmt", ["f32", "q8"])
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
-def test_spilled_traversal_stack(gpu, name, arg):
+def test_spilled_traversal_stack(gpu, name, arg, fmt):
     """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
     deep trees such as C5's use): forced here with options.lds_depth = 17, so nearly every traversal spills
     -- same image as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
-    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 17})
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 17, "node_format": fmt})
 
 
 @pytest.mark.parametrize("always_max", [0, 4])
@@ -319,3 +323,13 @@ def test_always_tested_primitives(gpu, always_max):
     for name in ("bunny_full", "two_balls"):
         sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
         _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"always_max": int(always_max)})
+
+
+@pytest.mark.parametrize("name", ["bunny_full", "more_balls", "two_balls", "earth", "variants"])
+def test_quantized_nodes_scenes(gpu, name):
+    """The 64 B quantized node format (options.node_format = q8, the default above 2^17 hittables) on the
+    small catalogue scenes, whose default is the f32 format: same image and ray counts as the oracle."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"node_format": "q8"})

@@ -2,7 +2,7 @@
 triangles): rp_scene_create time with the host binned SAH and with the device LBVH, tree statistics, and
 a 4-spp C5 frame over each tree.  Diagnostic only.
 
-    python tools/bvh_build_time.py [--tris 10000000] [--spp 4]
+    python tools/bvh_build_time.py [--tris 10000000] [--spp 4] [--builders gpu,host:q8,host@2:f32,...]
 """
 import argparse
 import json
@@ -32,10 +32,13 @@ def main():
     DeviceScene(scenes.configure(scenes.random_mesh(1000), 64, 64)).close()  # HIP runtime + code objects
     print(f"[bvh] mesh ready {out['mesh_seconds']}s", file=sys.stderr, flush=True)
     for spec in a.builders.split(","):
-        b, _, leaf = spec.partition("@")  # builder[@max_leaf]
+        spec_, _, fmt = spec.partition(":")  # builder[@max_leaf][:node_format]
+        b, _, leaf = spec_.partition("@")
         opt = {"builder": b}
         if leaf:
             opt["max_leaf"] = int(leaf)
+        if fmt:
+            opt["node_format"] = fmt
         t = time.time()
         ds = DeviceScene(sc, options=opt)
         setup = time.time() - t
