@@ -83,8 +83,6 @@ void dfree(void* p) {
 // Defaults of rp_scene_options (the measured best).
 constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
 constexpr double DEF_COST_TRAVERSE = 0.7;
-// Above this many hittables the single-threaded host SAH build dominates setup: the device LBVH builds.
-constexpr uint32_t GPU_BUILD_MIN_PRIMS = 1u << 20;
 
 }  // namespace
 
@@ -354,8 +352,9 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
 
   rpb::PackedScene ps;
   rpb::BuildOptions bo;
-  const bool gpu_build = opt.builder == RP_BUILDER_DEVICE ||
-                         (opt.builder == RP_BUILDER_AUTO && desc->n_hittables >= GPU_BUILD_MIN_PRIMS);
+  // AUTO = the host binned SAH at every size: on C5 (10 M triangles) it builds in 2.8 s with 16 threads
+  // (the device LBVH: 1.1 s) and renders 24 % faster; the LBVH stays an option.
+  const bool gpu_build = opt.builder == RP_BUILDER_DEVICE;
   const bool use_gpu = gpu_build && desc->n_hittables >= 2;  // the LBVH needs two primitives
   bo.tables_only = use_gpu;
   bo.max_leaf = opt.max_leaf;
@@ -376,7 +375,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   if (use_gpu) {
     rpb::PrimInput pin;
     if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
-    node_format = opt.node_format ? opt.node_format : rpb::auto_node_format(desc->n_hittables, pin.amax);
+    node_format = opt.node_format ? opt.node_format : rpl::NODES_F32;  // AUTO: f32 for the LBVH (rp_bvh.h)
     rpg::GpuTree gt;
     if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, gt, err))) return bail(fail(rc, err));
     s->d_nodes = gt.d_nodes;

@@ -51,11 +51,13 @@ struct PackedScene {
   size_t n_nodes() const { return node_format == rpl::NODES_Q8 ? qnodes.size() : nodes.size(); }
 };
 
-// The node format of RP_NODES_AUTO: the 64 B quantized node once the 128 B tree would outgrow the L2
-// (~2^17 hittables: ~60 k wide nodes, 8 MB), where halving the node bytes pays -- unless a
-// coordinate exceeds the frames' range (rp_layout.h COORD_MAX).  `amax`: the largest |coordinate| of the
-// primitive boxes.
-constexpr uint32_t Q8_MIN_PRIMS = 1u << 17;
+// The node format of RP_NODES_AUTO for the host SAH tree: the 64 B quantized node once the 128 B tree
+// outgrows the caches (~2^21 hittables: ~1 M wide nodes, 130 MB of f32 nodes next to 170 MB of primitives
+// against the 256 MB Infinity Cache), unless a coordinate exceeds the frames' range (rp_layout.h
+// COORD_MAX).  Measured: C5, 10 M triangles, -6 % frame time; C3 (4 971 hittables) +0.4 %.
+// The device LBVH keeps f32 (its tree has 3x fewer nodes: q8 +1.5 % on C5).  `amax`: the largest
+// |coordinate| of the primitive boxes.
+constexpr uint32_t Q8_MIN_PRIMS = 1u << 21;
 inline uint32_t auto_node_format(uint32_t n_hittables, double amax) {
   return n_hittables >= Q8_MIN_PRIMS && amax <= rpl::COORD_MAX ? rpl::NODES_Q8 : rpl::NODES_F32;
 }

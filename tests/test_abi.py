@@ -91,7 +91,7 @@ def test_scene_options_defaults_without_gpu():
     o = scene_options()
     assert (o.builder, o.max_leaf, o.cost_traverse, o.always_max, o.lds_depth, o.trav_threshold, o.tile_order,
             o.probe_n) == (0, 4, 0.7, 4, 0, 24, 0, 16)
-    assert o.node_format == 0  # RP_NODES_AUTO: f32 below 2^17 hittables, q8 above
+    assert o.node_format == 0  # RP_NODES_AUTO: q8 for host trees of >= 2^21 hittables, f32 otherwise
     o = scene_options(builder="gpu", lds_depth=17, node_format="q8")
     assert o.builder == 2 and o.lds_depth == 17 and o.node_format == 2
 

@@ -52,9 +52,10 @@ def test_c4_shard_of_8(gpu, shard):
 
 @pytest.mark.slow
 def test_c5_10m_triangles(gpu):
-    """Config C5's scene (10 M random triangles, 4096x4096) through the automatically chosen device LBVH and
-    spilling traversal stack, at 4 spp (the 256-spp frame is the bench's): the oracle's reference median-split
-    tree over all 10 M triangles re-renders 8 sampled tiles, and 20 k rays are intersected ray by ray."""
+    """Config C5's scene (10 M random triangles, 4096x4096) through the default tree (host SAH, 64 B quantized
+    nodes) and the spilling traversal stack, at 4 spp (the 256-spp frame is the bench's): the oracle's
+    reference median-split tree over all 10 M triangles re-renders 8 sampled tiles, and 20 k rays are
+    intersected ray by ray -- over the default tree and over the device LBVH in both node formats."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     scene, params = scenes.config_scene("C5")
@@ -69,7 +70,10 @@ def test_c5_10m_triangles(gpu):
         info = ds.info()
         assert info["prims"] == 10_000_000 and info["max_depth"] >= 12  # 43+ stack entries: the SPILL kernel
         rgb, _, st = ds.render(p)
-        hits, mats = ds.intersect(rays)
+        results = [ds.intersect(rays)]
+    for fmt in ("f32", "q8"):
+        with gpu.DeviceScene(scene, options={"builder": "gpu", "node_format": fmt}) as ds:
+            results.append(ds.intersect(rays))
     assert st["pixels"] == 4096 * 4096 and np.isfinite(rgb).all()
     assert 1.0 < st["rays"] / st["samples"] < 8.0
     desc = scene.desc()
@@ -77,10 +81,11 @@ def test_c5_10m_triangles(gpu):
     ref_hits, ref_mats, _ = os_.intersect(rays)
     hit = np.isfinite(ref_hits[:, 0])
     assert hit.sum() > n // 4
-    assert np.array_equal(np.isfinite(hits[:, 0]), hit)
-    same = mats == ref_mats
-    assert same.all()
-    np.testing.assert_array_equal(hits[hit, :7], ref_hits[hit, :7])
+    for hits, mats in results:
+        assert np.array_equal(np.isfinite(hits[:, 0]), hit)
+        same = mats == ref_mats
+        assert same.all()
+        np.testing.assert_array_equal(hits[hit, :7], ref_hits[hit, :7])
     os_.close()
     sub = replace(p, shard=3, num_shards=2048)
     ref, _, ctr = oracle_render(scene, sub, threads=16)
