@@ -394,10 +394,12 @@ void node_frame(const Box& b, rpl::Node4Q& n) {
 
 // Collapse the binary tree into 4-wide nodes: each wide node takes its binary node's two children and
 // repeatedly opens the inner child of largest surface area until it has 4 children (Wald et al.).
-// The wide nodes are written in the scene's node format (child boxes from the exact f64 boxes), numbered
-// depth-first (a node, then its inner children's subtrees in child order).  With par > 1 the inner
-// children's subtrees are collapsed on threads into local arrays and appended in child order: the same
-// numbering and records as the serial collapse.
+// The wide nodes are written in the scene's node format (child boxes from the exact f64 boxes).
+// Numbering: the inner children of a node are consecutive records (a family), and families are laid out
+// depth-first -- a ray that enters several children of a node reads neighbouring records (the same or
+// the next cache line) instead of records a whole subtree apart.  With par > 1 the inner children's
+// subtrees are collapsed on threads into local arrays (local root at 0) whose roots are copied into the
+// family's slots and whose descendants are appended in child order: the serial numbering and records.
 struct Collapser {
   const std::vector<BinNode>& bin;
   uint32_t fmt;
@@ -408,24 +410,29 @@ struct Collapser {
 
   uint32_t size() const { return (uint32_t)(fmt == rpl::NODES_Q8 ? qnodes.size() : nodes.size()); }
   uint32_t* child(uint32_t i) { return fmt == rpl::NODES_Q8 ? qnodes[i].child : nodes[i].child; }
-  uint32_t add() {
-    if (fmt == rpl::NODES_Q8) qnodes.emplace_back();
-    else nodes.emplace_back();
-    return size() - 1;
+  uint32_t add(uint32_t n = 1) {
+    const uint32_t first = size();
+    if (fmt == rpl::NODES_Q8) qnodes.resize(qnodes.size() + n);
+    else nodes.resize(nodes.size() + n);
+    return first;
   }
-  // appends another collapse's nodes, shifting its inner-node entries by the current size
-  void append(Collapser& o) {
-    const uint32_t base = size();
-    if (fmt == rpl::NODES_Q8) qnodes.insert(qnodes.end(), o.qnodes.begin(), o.qnodes.end());
-    else nodes.insert(nodes.end(), o.nodes.begin(), o.nodes.end());
-    for (uint32_t i = base; i < size(); i++)
-      for (int c = 0; c < 4; c++)
-        if (!(child(i)[c] & rpl::ENTRY_LEAF)) child(i)[c] += base;
+  // record i of another collapse into slot `dst`, its inner entries shifted by `shift`
+  void put(uint32_t dst, Collapser& o, uint32_t i, uint32_t shift) {
+    if (fmt == rpl::NODES_Q8) qnodes[dst] = o.qnodes[i];
+    else nodes[dst] = o.nodes[i];
+    for (int c = 0; c < 4; c++)
+      if (!(child(dst)[c] & rpl::ENTRY_LEAF)) child(dst)[c] += shift;
   }
 
-  uint32_t emit(int32_t bi, uint32_t depth) {
+  uint32_t emit_root(int32_t bi) {
+    const uint32_t root = add();
+    fill(root, bi, 0);
+    return root;
+  }
+
+  // writes record `self` for binary node bi and, recursively, its descendants
+  void fill(uint32_t self, int32_t bi, uint32_t depth) {
     if (depth > max_depth) max_depth = depth;
-    const uint32_t self = add();
     int32_t kids[4];
     int nk = 0;
     if (bin[bi].leaf()) {
@@ -469,6 +476,11 @@ struct Collapser {
       entries[c] = k.leaf() ? rpl::ENTRY_LEAF | ((k.count - 1) << rpl::LEAF_SHIFT) | k.first : 0u;
       inner += !k.leaf();
     }
+    // the family: the inner children's records, consecutive
+    const uint32_t fam = inner ? add((uint32_t)inner) : 0u;
+    for (int c = 0, j = 0; c < nk; c++)
+      if (!bin[kids[c]].leaf()) entries[c] = fam + (uint32_t)j++;
+    for (int c = 0; c < 4; c++) child(self)[c] = entries[c];
     if (par > 1 && inner >= 2) {
       std::vector<std::unique_ptr<Collapser>> sub;
       std::vector<std::thread> th;
@@ -477,21 +489,23 @@ struct Collapser {
         sub.emplace_back(new Collapser{bin, fmt, std::max(1u, par / (unsigned)inner), {}, {}, 0});
         Collapser* sc = sub.back().get();
         const int32_t kb = kids[c];
-        th.emplace_back([sc, kb] { sc->emit(kb, 0); });
+        th.emplace_back([sc, kb] { sc->emit_root(kb); });
       }
       for (auto& t : th) t.join();
-      for (int c = 0, j = 0; c < nk; c++) {
-        if (bin[kids[c]].leaf()) continue;
-        entries[c] = size();
-        max_depth = std::max(max_depth, depth + 1 + sub[j]->max_depth);
-        append(*sub[j++]);
+      for (int j = 0; j < inner; j++) {
+        // local record 0 -> family slot; local records 1.. -> appended at `base` (local i -> base + i - 1)
+        Collapser& sc = *sub[j];
+        const uint32_t base = size();
+        const uint32_t n = sc.size();
+        put(fam + (uint32_t)j, sc, 0, base - 1u);
+        add(n - 1u);
+        for (uint32_t i = 1; i < n; i++) put(base + i - 1u, sc, i, base - 1u);
+        max_depth = std::max(max_depth, depth + 1 + sc.max_depth);
       }
     } else {
-      for (int c = 0; c < nk; c++)
-        if (!bin[kids[c]].leaf()) entries[c] = emit(kids[c], depth + 1);
+      for (int c = 0, j = 0; c < nk; c++)
+        if (!bin[kids[c]].leaf()) fill(fam + (uint32_t)j++, kids[c], depth + 1);
     }
-    for (int c = 0; c < 4; c++) child(self)[c] = entries[c];
-    return self;
   }
 };
 
@@ -767,7 +781,7 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     Collapser C{bin, out.node_format, threads, {}, {}, 0};
     if (out.node_format == rpl::NODES_Q8) C.qnodes.reserve(bin.size() / 2 + 1);
     else C.nodes.reserve(bin.size() / 2 + 1);
-    C.emit(0, 0);
+    C.emit_root(0);
     out.nodes.swap(C.nodes);
     out.qnodes.swap(C.qnodes);
     out.max_depth = C.max_depth;

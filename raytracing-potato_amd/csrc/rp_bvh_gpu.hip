@@ -225,6 +225,10 @@ __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur
   } else {
     for (int k = 0; k < 4; k++) nd.pad[k] = 0;
   }
+  // the inner children's wide nodes are allocated as one consecutive family (rp_bvh.cpp Collapser)
+  uint32_t n_inner = 0;
+  for (uint32_t k = 0; k < nk; k++) n_inner += bin_count(kids[k], first, last) > max_leaf;
+  uint32_t fam = n_inner ? atomicAdd(&counters[0], n_inner) : 0u;
   for (uint32_t k = 0; k < 4; k++) {
     if (k >= nk) {
       if constexpr (NF == rpl::NODES_Q8) rpl::empty_child(nd, (int)k);
@@ -241,7 +245,7 @@ __global__ void collapse_kernel(const Frontier* __restrict__ cur, uint32_t n_cur
       nd.child[k] = rpl::ENTRY_LEAF | ((cnt - 1u) << rpl::LEAF_SHIFT) | lo;
       atomicAdd(&counters[2], 1u);
     } else {
-      const uint32_t w = atomicAdd(&counters[0], 1u);
+      const uint32_t w = fam++;
       nd.child[k] = w;
       next[atomicAdd(&counters[1], 1u)] = Frontier{c, w};
     }
