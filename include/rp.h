@@ -196,6 +196,11 @@ enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
  * f32 frame (half the node bytes, more ALU per visit).  AUTO = Q8 for host-built trees of >= 2^21 hittables,
  * F32 otherwise. */
 enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2 };
+/* Tile orders: PLAIN = shard order (row-major); COST = a probe launch traces sample 0 of a lattice of pixels
+ * per tile and the costliest tiles go first (short frame tail); MORTON = Z-order of the tiles (neighbouring
+ * tiles run together: a small cache working set).  AUTO = COST while the scene fits the 256 MB Infinity
+ * Cache, MORTON above. */
+enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON = 3 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles) */
@@ -205,7 +210,7 @@ typedef struct rp_scene_options {
   uint32_t lds_depth;       /* traversal-stack entries kept in LDS (0 -> automatic; >= 17 forces a split) */
   uint32_t self_check;      /* 1: structural self-check of a device-built tree (slow; tests) */
   uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24) */
-  uint32_t tile_order;      /* 0 = cost-ordered tiles (probe launch + sort), 1 = plain shard order */
+  uint32_t tile_order;      /* RP_TILES_*: the order the unit queue hands out a shard's tiles */
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
   uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
   uint32_t wf_slots;        /* wavefront engine: paths in flight per resident lane (0 -> 2) */

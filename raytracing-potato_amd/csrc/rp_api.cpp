@@ -126,6 +126,7 @@ struct rp_scene {
   rp_workspace ws0;            // the scene's own workspace (rp_render, rp_render_device)
   int n_workspaces = 0;        // live workspaces from rp_workspace_create
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
+  uint32_t tiles_auto = RP_TILES_COST;  // the tile order of RP_TILES_AUTO (scene_create)
   uint32_t max_depth = 0;
   int num_cu = 0;
   int blocks_per_cu = 0;
@@ -282,7 +283,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.lds_depth != 0 && o.lds_depth < 17) return fail(RP_EINVAL, "options.lds_depth must be 0 or >= 17");
   if (o.trav_threshold == 0) o.trav_threshold = d.trav_threshold;
   if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
-  if (o.tile_order > 1) return fail(RP_EINVAL, "options.tile_order must be 0 or 1");
+  if (o.tile_order > RP_TILES_MORTON) return fail(RP_EINVAL, "options.tile_order must be RP_TILES_*");
   if (o.probe_n == 0) o.probe_n = d.probe_n;
   if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
   if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
@@ -450,6 +451,10 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->device_bytes = rp_node_bytes(node_format) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
                     sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
+  // Cache-resident scenes (C3: 11 MB) gain ~15 % from cost-ordered tiles (short frame tail); a scene past the
+  // 256 MB Infinity Cache (C5: 2.5 GB) loses 5-7 % to any reordering that scatters the concurrently rendered
+  // tiles over the frame, and the Z-order keeps them together.
+  s->tiles_auto = s->device_bytes > (256ull << 20) ? RP_TILES_MORTON : RP_TILES_COST;
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
   // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
   // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  options.lds_depth
@@ -536,7 +541,17 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     return (int)std::max<uint64_t>(1, std::min(want, resident));
   };
   RP_HIP(hipMemsetAsync(w->d_queue, 0, sizeof(uint32_t) * 2, st));
-  if (s->opt.tile_order == 0 && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
+  const rpk::TileGeom tg{t.tiles_x, kp.shard, kp.nshards};
+  const uint32_t tiles_y = t.tiles_y;
+  uint32_t order_mode = s->opt.tile_order;
+  if (order_mode == RP_TILES_AUTO) order_mode = s->tiles_auto;
+  if (order_mode == RP_TILES_MORTON && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX &&
+      t.tiles_x <= 256 && tiles_y <= 256) {
+    int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
+    kp.tile_order = w->d_tile_order;
+  }
+  if (order_mode == RP_TILES_COST && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
     // probe sample 0 of an n x n lattice of pixels per tile, then sort the tiles by cost (same stream,
     // no host sync)
     rpk::KParams pk = kp;
@@ -553,7 +568,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
     int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + 1, grid_for(pk.n_slots), stream);
     if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
-    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, w->d_tile_order, stream);
+    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, tg, w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }

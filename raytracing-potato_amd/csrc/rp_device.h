@@ -556,10 +556,13 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride
 }
 
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
-// parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).
-template <bool SPILL, uint32_t NF>
+// parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).  `work` (COUNT instantiations: the
+// cost probe) accumulates the lane's traversal work in WORK_* units.
+enum : uint32_t { WORK_VISIT = 2, WORK_TEST = 3, WORK_RAY = 16 };  // node visit : primitive test : shaded ray
+template <bool SPILL, uint32_t NF, bool COUNT = false>
 RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
-                          double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr) {
+                          double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr,
+                          uint32_t* work = nullptr) {
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
   double best = ts.best;
   float best32 = f32_up(best);
@@ -567,6 +570,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
   // ---- inner nodes
   while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
+    if constexpr (COUNT) *work += WORK_VISIT;
     DREG(DREG_NODE)
     // Near/far planes chosen per ray by the slope signs (octant), so each child costs one max3 + max for
     // t_near and one min3 + min for t_far: for a valid box the same pair of values the min/max slab form
@@ -703,6 +707,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
   uint32_t kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
   while (leaf != 0u) {
     DIAG(if (td) td->tests++;)
+    if constexpr (COUNT) *work += WORK_TEST;
     DREG(DREG_PRIM)
     prim_test(S, k, o, d, tmin, best, ts);
     if (++k == kend) {

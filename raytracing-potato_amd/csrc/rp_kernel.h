@@ -68,16 +68,18 @@ struct KParams {
   double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
   uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
-  uint32_t* tile_cost;         // probe: [k] rays summed over the tile's probed samples, [TILE_SORT_MAX + k]
-                               // the longest probed sample (zeroed by the caller)
+  uint32_t* tile_cost;         // probe: [k] cost (rp_device.h WORK_*: node visits, primitive tests, rays)
+                               // summed over the tile's probed samples, [TILE_SORT_MAX + k] the costliest
+                               // probed sample (zeroed by the caller)
 };
 
 // Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last
 // pixels after the queue drained) was ~23% of the C3 frame; handing out the expensive tiles first
 // (longest-processing-time-first) leaves cheap, uniform tiles for the end.  The order comes from a probe
 // launch of the same kernel (sample 0 of a 16 x 16 lattice of pixels per tile: the exact
-// paths of the frame) and a one-block sort.  Tiles holding the longest paths go first: a pixel's samples
-// run sequentially on one lane, so one expensive pixel fetched late becomes a latency-bound tail by itself.
+// paths of the frame) and a one-block sort.  Tiles holding the costliest samples go first (cost = traversal
+// work + shaded rays: on C5 the rays differ far more in node visits than in path length): a unit's samples
+// run sequentially on one lane, so one expensive unit fetched late becomes a latency-bound tail by itself.
 // Results do not depend on the order (per-pixel seeding).
 enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
 
@@ -98,9 +100,15 @@ enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
                   uint32_t* queue, int grid, void* stream);
 
-// Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (longest sample, mean rays per probed
-// pixel), ties by tile index, into order[] (shard tile indices).  One block.
-int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32_t* order, void* stream);
+// Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (costliest sample, mean cost per probed
+// pixel), log-quantized, ties by tile index, into order[] (shard tile indices).  One block.
+// With cost == NULL: the shard's tiles in Z-order of their frame-grid coordinates (tiles_x, tiles_y <= 256),
+// so tiles processed at the same time are neighbours (the scene's cache working set stays small).
+struct TileGeom {
+  uint32_t tiles_x, shard, nshards;
+};
+int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
+                     void* stream);
 
 // Final pass of a multi-batch frame: per shard slot, the batch sums added in batch order, / spp.
 int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void* stream);

@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   double& T_z = c_T[2 * BLOCK + tid];
 #endif
   uint32_t depth = 0;
+  uint32_t work = 0;  // PROBE: the probed sample's traversal work (rp_device.h WORK_*)
   bool first = true;
   Rng rng;
   rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N;
@@ -156,9 +157,9 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         if (alive && !tdone) {
           DREG(DREG_STEP)
 #ifdef RPK_DIAG
-          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
+          trav_step<SPILL, NF, PROBE>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td, &work);
 #else
-          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+          trav_step<SPILL, NF, PROBE>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, nullptr, &work);
 #endif
           tdone = trav_done(ts);
         }
@@ -204,8 +205,12 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         if (s == unit_spp(A, batch)) {  // main.rs:86-87 (for this unit's batch of samples)
           DREG(DREG_END_PIXEL)
           if (PROBE) {
-            // spp is 1 here: the sample traced max_bounce - depth scattered rays plus its last one
-            const uint32_t k = slot / A->P.probe_px, r = A->P.max_bounce - depth + (scattered_any ? 0u : 1u);
+            // spp is 1 here: the sample traced max_bounce - depth scattered rays plus its last one; its cost
+            // is their shading plus the traversal work counted in trav_step (node visits and primitive
+            // tests: C5's rays differ far more in traversal than in path length)
+            const uint32_t k = slot / A->P.probe_px, rays = A->P.max_bounce - depth + (scattered_any ? 0u : 1u);
+            const uint32_t r = work + WORK_RAY * rays;
+            work = 0;
             atomicAdd(&A->P.tile_cost[k], r);
             atomicMax(&A->P.tile_cost[TILE_SORT_MAX + k], r);
           } else if (A->P.nbatch == 1) {
@@ -446,16 +451,31 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
 // tile index.  Padding keys sort last.
 static constexpr int SORT_BLOCK = 1024;
 static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
+__device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every other bit of 16
+  v = (v | (v << 4)) & 0x0F0Fu;
+  v = (v | (v << 2)) & 0x3333u;
+  return (v | (v << 1)) & 0x5555u;
+}
+
 __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n,
-                                                               uint32_t probe_px, uint32_t np2,
+                                                               uint32_t probe_px, uint32_t np2, TileGeom g,
                                                                uint32_t* __restrict__ order) {
   __shared__ uint32_t key[TILE_SORT_MAX];
   for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
     uint32_t kk = 0xFFFFFFFFu;
-    if (i < n) {
-      const uint32_t longest = min(cost[TILE_SORT_MAX + i], 15u);
-      const uint32_t mean16 = (uint32_t)min<uint64_t>((uint64_t)cost[i] * 16u / probe_px, 16383u);
-      kk = ((((15u - longest) << 14) | (16383u - mean16)) << 14) | i;
+    if (i < n && !cost) {
+      // Z-order of the tile's (x, y) in the frame's tile grid (both < 256): nearby tiles run together
+      const uint32_t t = g.shard + i * g.nshards, tx = t % g.tiles_x, ty = t / g.tiles_x;
+      kk = (((spread8(ty) << 1) | spread8(tx)) << 14) | i;
+    } else if (i < n) {
+      // log scales of the costliest probed sample's cost and of the mean cost
+      const float mean = (float)cost[i] / (float)probe_px;
+      // quarter-octave buckets: tiles of one bucket keep their (row-major) order, so the costliest tiles
+      // go first without scattering neighbours more than the buckets do (C3: 2^(1/4) steps 248.1 ms,
+      // 2^(1/32) steps 250.1 ms, ray-count cost 254.7 ms per frame)
+      const uint32_t ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * 4.0f), 511u);
+      const uint32_t qm = min((uint32_t)(log2f(mean + 1.0f) * 4.0f), 511u);
+      kk = ((((511u - ql) << 9) | (511u - qm)) << 14) | i;
     }
     key[i] = kk;
   }
@@ -476,11 +496,13 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
   for (uint32_t i = threadIdx.x; i < n; i += SORT_BLOCK) order[i] = key[i] & 0x3FFFu;
 }
 
-int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, uint32_t* order, void* stream) {
+int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
+                     void* stream) {
   if (n == 0 || n > TILE_SORT_MAX) return (int)hipErrorInvalidValue;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
-  hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(SORT_BLOCK), 0, (hipStream_t)stream, cost, n, probe_px, np2, order);
+  hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(SORT_BLOCK), 0, (hipStream_t)stream, cost, n, probe_px, np2, g,
+                     order);
   return (int)hipGetLastError();
 }
 

@@ -333,3 +333,19 @@ def test_quantized_nodes_scenes(gpu, name):
     from rtpotato.scene import RenderParams
     sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
     _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"node_format": "q8"})
+
+
+def test_tile_orders_bitwise(gpu):
+    """The unit queue's tile order (options.tile_order: plain row-major, cost-ordered by the probe launch,
+    Z-order) changes the schedule only: the frames are identical bit for bit, sharded or not."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.bunny_full(), 96, 64)
+    for p in (RenderParams(96, 64, 40, 8, 5, 16, 16), RenderParams(96, 64, 8, 8, 5, 8, 8, shard=1, num_shards=3)):
+        frames = []
+        for order in ("plain", "cost", "morton", "auto"):
+            with gpu.DeviceScene(sc, options={"tile_order": order}) as ds:
+                rgb, _, st = ds.render(p)
+            frames.append((rgb, st["rays"]))
+        for rgb, rays in frames[1:]:
+            assert np.array_equal(rgb, frames[0][0]) and rays == frames[0][1]
