@@ -545,13 +545,16 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   const uint32_t tiles_y = t.tiles_y;
   uint32_t order_mode = s->opt.tile_order;
   if (order_mode == RP_TILES_AUTO) order_mode = s->tiles_auto;
-  if (order_mode == RP_TILES_MORTON && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX &&
-      t.tiles_x <= 256 && tiles_y <= 256) {
+  // both sorts key the tiles by their Z-order code (frame grids up to 256 x 256 tiles; larger ones keep shard
+  // order)
+  const bool sortable = t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX && t.tiles_x <= 256 &&
+                        tiles_y <= 256;
+  if (order_mode == RP_TILES_MORTON && sortable) {
     int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
-  if (order_mode == RP_TILES_COST && t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX) {
+  if (order_mode == RP_TILES_COST && sortable) {
     // probe sample 0 of an n x n lattice of pixels per tile, then sort the tiles by cost (same stream,
     // no host sync)
     rpk::KParams pk = kp;

@@ -456,26 +456,34 @@ __device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every ot
   v = (v | (v << 2)) & 0x3333u;
   return (v | (v << 1)) & 0x5555u;
 }
+__device__ __forceinline__ uint32_t compact8(uint32_t v) {  // inverse of spread8
+  v &= 0x5555u;
+  v = (v | (v >> 1)) & 0x3333u;
+  v = (v | (v >> 2)) & 0x0F0Fu;
+  return (v | (v >> 4)) & 0x00FFu;
+}
 
+// Keys: [31:28] 0 | [27:22] 63 - costliest-sample bucket | [21:16] 63 - mean-cost bucket | [15:0] Z-order code of
+// the tile's frame coordinates (both < 256), which also identifies the tile.  Ascending order = costliest
+// buckets first, Z-order inside a bucket (row-major inside a bucket measured the same on C3: 247.4 vs 247.5
+// ms); without costs (cost == NULL) plain Z-order.
 __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n,
                                                                uint32_t probe_px, uint32_t np2, TileGeom g,
                                                                uint32_t* __restrict__ order) {
   __shared__ uint32_t key[TILE_SORT_MAX];
   for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
     uint32_t kk = 0xFFFFFFFFu;
-    if (i < n && !cost) {
-      // Z-order of the tile's (x, y) in the frame's tile grid (both < 256): nearby tiles run together
+    if (i < n) {
       const uint32_t t = g.shard + i * g.nshards, tx = t % g.tiles_x, ty = t / g.tiles_x;
-      kk = (((spread8(ty) << 1) | spread8(tx)) << 14) | i;
-    } else if (i < n) {
-      // log scales of the costliest probed sample's cost and of the mean cost
-      const float mean = (float)cost[i] / (float)probe_px;
-      // quarter-octave buckets: tiles of one bucket keep their (row-major) order, so the costliest tiles
-      // go first without scattering neighbours more than the buckets do (C3: 2^(1/4) steps 248.1 ms,
-      // 2^(1/32) steps 250.1 ms, ray-count cost 254.7 ms per frame)
-      const uint32_t ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * 4.0f), 511u);
-      const uint32_t qm = min((uint32_t)(log2f(mean + 1.0f) * 4.0f), 511u);
-      kk = ((((511u - ql) << 9) | (511u - qm)) << 14) | i;
+      uint32_t ql = 0, qm = 0;
+      if (cost) {
+        // quarter-octave buckets of the costliest probed sample's cost and of the mean cost (C3: 2^(1/4)
+        // steps 248.1 ms, 2^(1/32) steps 250.1 ms, the round-1 ray-count cost 254.7 ms per frame)
+        const float mean = (float)cost[i] / (float)probe_px;
+        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * 4.0f), 63u);
+        qm = min((uint32_t)(log2f(mean + 1.0f) * 4.0f), 63u);
+      }
+      kk = ((63u - ql) << 22) | ((63u - qm) << 16) | (spread8(ty) << 1) | spread8(tx);
     }
     key[i] = kk;
   }
@@ -493,7 +501,10 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
       __syncthreads();
     }
   }
-  for (uint32_t i = threadIdx.x; i < n; i += SORT_BLOCK) order[i] = key[i] & 0x3FFFu;
+  for (uint32_t i = threadIdx.x; i < n; i += SORT_BLOCK) {
+    const uint32_t m = key[i] & 0xFFFFu, tx = compact8(m), ty = compact8(m >> 1);
+    order[i] = (ty * g.tiles_x + tx - g.shard) / g.nshards;
+  }
 }
 
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
