@@ -207,7 +207,7 @@ typedef struct rp_scene_options {
   uint32_t max_leaf;        /* primitives per leaf, 1..8 (0 -> 4) */
   double cost_traverse;     /* SAH node cost relative to a primitive test (0 -> 0.7) */
   int32_t always_max;       /* primitives tested before the tree for every ray (-1 -> 4; 0 = none) */
-  uint32_t lds_depth;       /* traversal-stack entries kept in LDS (0 -> automatic; >= 17 forces a split) */
+  uint32_t lds_depth;       /* traversal-stack entries kept in LDS (0 -> automatic; >= 8 forces a split) */
   uint32_t self_check;      /* 1: structural self-check of a device-built tree (slow; tests) */
   uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24) */
   uint32_t tile_order;      /* RP_TILES_*: the order the unit queue hands out a shard's tiles */
@@ -215,7 +215,9 @@ typedef struct rp_scene_options {
   uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
   uint32_t wf_slots;        /* wavefront engine: paths in flight per resident lane (0 -> 2) */
   uint32_t node_format;     /* RP_NODES_* */
-  uint32_t reserved;
+  uint32_t leaf_break;      /* speculative traversal: a wave moves to the leaf tests once at most this many of its
+                               lanes still look for a leaf (0 -> 8 for scenes within the 256 MB Infinity Cache,
+                               12 above; 1..64) */
 } rp_scene_options;
 
 typedef struct rp_stats {

@@ -151,12 +151,10 @@ static constexpr uint32_t SLAB_N = SLAB_COLD;
 #define RPK_RNG_CRIT 2
 #endif
 static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
-// Traversal wave-level exits (trav_step): leave the inner-node loop once at most RPK_LEAF_BREAK lanes of the
-// wave still look for a leaf (C3: 0 -> 3 is -2.7 % frame time), and the leaf loop once at most
-// RPK_PRIM_BREAK lanes still test primitives (their remaining run is parked as a leaf entry).
-#ifndef RPK_LEAF_BREAK
-#define RPK_LEAF_BREAK 3
-#endif
+// Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
+// the wave still look for a leaf (rp_scene_options.leaf_break; C3: 0 -> 3 was -2.7 % frame time, 8 is -0.8 %
+// more; C5 wants 12), and the leaf loop once at most RPK_PRIM_BREAK lanes still test primitives (their
+// remaining run is parked as a leaf entry).
 #ifndef RPK_PRIM_BREAK
 #define RPK_PRIM_BREAK 0
 #endif
@@ -688,9 +686,9 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       leaf = cur;
       cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
     }
-    // ... and once at most RPK_LEAF_BREAK lanes still look for one, the wave moves on to the leaves: the
+    // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
     // last few descents ran with most of the wave idle (those lanes resume their descent next step)
-    if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= RPK_LEAF_BREAK) break;
+    if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
 #ifdef RPK_NODE_BREAK  // experiment: leave once at most this many lanes are still descending at all
     if ((uint32_t)__popcll(__ballot(true)) <= RPK_NODE_BREAK) break;
 #endif
@@ -1114,6 +1112,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.n_always = A->S.n_always;
   S.qbound = A->S.qbound;
   S.node_format = A->S.node_format;
+  S.leaf_break = A->S.leaf_break;
   S.stack_depth = A->S.stack_depth;
   S.lds_depth = A->S.lds_depth;
   S.spill = A->S.spill;

@@ -20,6 +20,7 @@ struct KScene {
   uint32_t always_first, n_always;  // prims tested before the tree for every ray (rp_bvh.h BuildOptions)
   double qbound;         // Node4Q: bound on every node frame's |o| and 255 s (rp_layout.h qbound): the slab slack
   uint32_t node_format;  // rpl::NODES_F32 / NODES_Q8: picks the kernel instantiation
+  uint32_t leaf_break;   // trav_step leaves the inner-node loop once at most this many lanes still seek a leaf
   uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
   uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
