@@ -209,7 +209,8 @@ typedef struct rp_scene_options {
   int32_t always_max;       /* primitives tested before the tree for every ray (-1 -> 4; 0 = none) */
   uint32_t lds_depth;       /* traversal-stack entries kept in LDS (0 -> automatic; >= 8 forces a split) */
   uint32_t self_check;      /* 1: structural self-check of a device-built tree (slow; tests) */
-  uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24) */
+  uint32_t trav_threshold;  /* lanes of a wave still traversing before the finished ones shade (0 -> 24 for
+                               scenes within the 256 MB Infinity Cache, 32 above; 1..64) */
   uint32_t tile_order;      /* RP_TILES_*: the order the unit queue hands out a shard's tiles */
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
   uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */

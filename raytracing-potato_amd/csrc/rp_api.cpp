@@ -262,7 +262,7 @@ rp_scene_options default_options() {
   o.always_max = (int32_t)DEF_ALWAYS_MAX;
   o.lds_depth = 0;
   o.self_check = 0;
-  o.trav_threshold = DEF_TRAV_THRESHOLD;
+  o.trav_threshold = 0;  // auto (scene_create): DEF_TRAV_THRESHOLD, or 32 for scenes past the Infinity Cache
   o.tile_order = 0;
   o.probe_n = rpk::PROBE_LATTICE_N;
   o.engine = RP_ENGINE_MEGAKERNEL;
@@ -281,7 +281,6 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (!(o.cost_traverse > 0.0) || !std::isfinite(o.cost_traverse)) return fail(RP_EINVAL, "options.cost_traverse must be > 0");
   if (o.always_max < 0) o.always_max = d.always_max;
   if (o.lds_depth != 0 && o.lds_depth < 8) return fail(RP_EINVAL, "options.lds_depth must be 0 or >= 8");
-  if (o.trav_threshold == 0) o.trav_threshold = d.trav_threshold;
   if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
   if (o.tile_order > RP_TILES_MORTON) return fail(RP_EINVAL, "options.tile_order must be RP_TILES_*");
   if (o.probe_n == 0) o.probe_n = d.probe_n;
@@ -458,6 +457,8 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->tiles_auto = s->device_bytes > (256ull << 20) ? RP_TILES_MORTON : RP_TILES_COST;
   // the speculative-traversal exit: C3 246.3 ms at 8 (3: 248.2, 12: 248.5), C5 2,103 ms at 12 (8: 2,118, 3: 2,229)
   s->ks.leaf_break = opt.leaf_break ? opt.leaf_break : (s->device_bytes > (256ull << 20) ? 12u : 8u);
+  // lanes still traversing before the finished ones shade: C3 24 (16: +0.2 %, 32: +0.7 %), C5 32 (-1.6 %)
+  if (s->opt.trav_threshold == 0) s->opt.trav_threshold = s->device_bytes > (256ull << 20) ? 32u : DEF_TRAV_THRESHOLD;
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
   // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
   // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  options.lds_depth

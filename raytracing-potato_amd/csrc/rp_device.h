@@ -154,9 +154,9 @@ static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
 // Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
 // the wave still look for a leaf (rp_scene_options.leaf_break; C3: 0 -> 3 was -2.7 % frame time, 8 is -0.8 %
 // more; C5 wants 12), and the leaf loop once at most RPK_PRIM_BREAK lanes still test primitives (their
-// remaining run is parked as a leaf entry).
+// remaining run is parked as a leaf entry; C3 0 -> 12: -3.7 %, C5 -0.8 %; 6-16 within 0.5 %).
 #ifndef RPK_PRIM_BREAK
-#define RPK_PRIM_BREAK 0
+#define RPK_PRIM_BREAK 12
 #endif
 static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // this many lanes with room force a refill pass
 

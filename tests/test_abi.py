@@ -90,7 +90,7 @@ def test_scene_options_defaults_without_gpu():
     from rtpotato.render import scene_options
     o = scene_options()
     assert (o.builder, o.max_leaf, o.cost_traverse, o.always_max, o.lds_depth, o.trav_threshold, o.tile_order,
-            o.probe_n) == (0, 4, 0.7, 4, 0, 24, 0, 16)
+            o.probe_n) == (0, 4, 0.7, 4, 0, 0, 0, 16)
     assert o.node_format == 0  # RP_NODES_AUTO: q8 for host trees of >= 2^21 hittables, f32 otherwise
     assert o.leaf_break == 0   # auto: 8 for cache-resident scenes, 12 above 256 MB
     o = scene_options(builder="gpu", lds_depth=17, node_format="q8")
