@@ -25,6 +25,18 @@ namespace rpk {
 #else
 #define RPK_RENDER_ATTR
 #endif
+// Wave issue priority by phase (s_setprio): traversal 2 > shading 1 > keystream refill 0 -- a traversing
+// wave's next node fetch goes out sooner while VALU-heavy work fills the gaps (C3 234.7 -> 230.1 ms, C5
+// 2,039 -> 2,015 ms; traversal-only priority 231.5, priority to shading 237.6)
+#ifndef RPK_PRIO_TRAV
+#define RPK_PRIO_TRAV 2
+#endif
+#ifndef RPK_PRIO_SHADE
+#define RPK_PRIO_SHADE 1
+#endif
+#ifndef RPK_PRIO_REFILL
+#define RPK_PRIO_REFILL 0
+#endif
 // PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
 // and timings of the frame kernel never mix with it.
 template <bool PROBE, bool SPILL, uint32_t NF>
@@ -119,6 +131,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   for (;;) {
     DIAG(iters++;)
     DREG(DREG_ROUND)
+    if (RPK_PRIO_REFILL != RPK_PRIO_SHADE) __builtin_amdgcn_s_setprio(RPK_PRIO_REFILL);
     {
       KArgsPtr A = kargs();
       const uint64_t seed = fresh ? unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch) : 0ull;  // RNG contract
@@ -153,6 +166,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       }
       Ray32 r;
       setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
+      __builtin_amdgcn_s_setprio(RPK_PRIO_TRAV);  // (RPK_PRIO_* above)
       for (;;) {
         if (alive && !tdone) {
           DREG(DREG_STEP)
@@ -168,6 +182,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         if (act == 0 || (waiting != 0 && (uint32_t)__popcll(act) < thr)) break;
       }
     }
+    __builtin_amdgcn_s_setprio(RPK_PRIO_SHADE);
     DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
     if (__ballot(alive) == 0) break;
 
