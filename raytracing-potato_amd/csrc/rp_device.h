@@ -364,21 +364,24 @@ struct TravDiag {
 // The single-rounding form fma(P, inv, -oinv) errs by <= 5u |t| + |o_ray - o32| |inv| (1 + 6u) + u |o32 inv|
 // against the exact t = (P - o_ray) / d (u = 2^-24); with every |o| and |q s| <= qbound (rp_layout.h),
 // |e| <= u (1 + u) |inv| (2 qbound + |o32|) + u^2 |o32 inv|, and e = 0 when inv = +-2^64 (the clamp below)
-// and o32 = 0 (A and B exact).  With D = max over axes of the absolute terms, a box whose exact interval
-// meets [t_min, best] at some t* > 0 satisfies  tnear^ <= t*(1 + 5u) + D  and  tfar^ >= t*(1 - 5u) - D  (the
-// near planes behind the origin and tmin32 <= t* do not raise tnear^; every far plane lies at or beyond t*).
-// The test
-//     fma(tnear^, 1 - 2^-19, -slack) <= tfar^                    (slack >= 3D)
-// then passes every such box: its exact left side is <= t*(1+5u)(1-2^-19) + D - slack <= t*(1-5u) - 2D
-// - 22u t*, which leaves 22u t* + D to absorb the FMA's rounding (<= u (tnear^ + slack)).  It may pass a
-// few more boxes, never fewer: no primitive the reference's f64 test reaches is culled.  Empty slots fail
-// (Node4: lo = +inf, hi = -inf gives t_near = +inf; Node4Q: masked by their entry).  Slopes are clamped to
-// |inv| <= 2^64 (axis-parallel rays) and frames to |o|, 255 s <= 2^56 (rp_layout.h COORD_MAX), so every
-// A, B and t^ is finite; an A that underflows errs by < 2^-118, inside the 2^-100 slack floor.
+// and o32 = 0 (A and B exact).  Call D_a the absolute terms of axis a.  Each axis's planes are moved
+// outward by its own D_a, folded into the FMA's addend: near planes use nb_a = fl_down(-oinv_a - D_a), far
+// planes fb_a = fl_up(-oinv_a + D_a) (Node4Q: B_near = fma(o, inv, nb_a), B_far = fma(o, inv, fb_a), whose
+// roundings the frame term covers).  A box whose exact interval meets [t_min, best] at some t* > 0 then has
+// every near plane <= t*(1 + 6u) (those behind the origin or below tmin32 <= t* do not raise t_near) and
+// every far plane >= t*(1 - 6u), so the test
+//     fma(tnear^, 1 - 2^-19, -2^-100) <= tfar^
+// passes it (2^-19 = 32u).  It may pass a few more boxes, never fewer: no primitive the reference's f64 test
+// reaches is culled.  The error bound is per axis: a ray nearly parallel to an axis has a huge D on that
+// axis only (|inv| is huge there), which widens that slab alone -- with one scalar slack (max over the
+// axes, round 1) such a ray passed every box near the plane it runs in, up to 43 k node visits on C5.
+// Empty slots fail (Node4: lo = +inf, hi = -inf gives t_near = +inf; Node4Q: masked by their entry).  Slopes
+// are clamped to |inv| <= 2^64 (axis-parallel rays) and frames to |o|, 255 s <= 2^56 (rp_layout.h
+// COORD_MAX), so every A, B and t^ is finite; an A that underflows errs by < 2^-118, inside the 2^-100 term.
 struct Ray32 {
   float ix, iy, iz;     // rcp(fl(d))
-  float oix, oiy, oiz;  // fl(o32 * inv)
-  float slack;          // >= 3D (per ray)
+  float nbx, nby, nbz;  // near-plane addends fl_down(-oinv - D) per axis
+  float fbx, fby, fbz;  // far-plane addends fl_up(-oinv + D) per axis
   float tmin;           // t_min rounded down
   uint32_t sx, sy, sz;  // per axis, by the sign of the slope: Node4 = byte offset of the near plane row
                         // (lo_* or hi_*; the far row is the other); Node4Q = v_perm_b32 selector picking the
@@ -411,9 +414,7 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
   r.ix = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.x), -0x1p64f), 0x1p64f);
   r.iy = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.y), -0x1p64f), 0x1p64f);
   r.iz = fminf(fmaxf(__builtin_amdgcn_rcpf((float)d.z), -0x1p64f), 0x1p64f);
-  r.oix = ox * r.ix;
-  r.oiy = oy * r.iy;
-  r.oiz = oz * r.iz;
+  const float oix = ox * r.ix, oiy = oy * r.iy, oiz = oz * r.iz;
   // |o - o32| is exact in f64 (Sterbenz); an axis with no origin rounding contributes no origin term
   const double ex = fabs(o.x - (double)ox), ey = fabs(o.y - (double)oy), ez = fabs(o.z - (double)oz);
   const double k = 1.0 + 0x1p-20, u = 0x1p-23, q2 = 2.0 * qbound;
@@ -422,11 +423,15 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
                ? 0.0
                : fabs((double)inv) * (q2 + fabs((double)o32)) * u * k;
   };
-  double D = 0.0;
-  D = fmax(D, (ex == 0.0 ? 0.0 : ex * fabs((double)r.ix) * k) + fabs((double)r.oix) * u + fr(r.ix, ox));
-  D = fmax(D, (ey == 0.0 ? 0.0 : ey * fabs((double)r.iy) * k) + fabs((double)r.oiy) * u + fr(r.iy, oy));
-  D = fmax(D, (ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)r.oiz) * u + fr(r.iz, oz));
-  r.slack = f32_up(3.0 * D * k + (NF == rpl::NODES_Q8 ? 0x1p-100 : 0x1p-126));
+  const double Dx = ((ex == 0.0 ? 0.0 : ex * fabs((double)r.ix) * k) + fabs((double)oix) * u + fr(r.ix, ox)) * k;
+  const double Dy = ((ey == 0.0 ? 0.0 : ey * fabs((double)r.iy) * k) + fabs((double)oiy) * u + fr(r.iy, oy)) * k;
+  const double Dz = ((ez == 0.0 ? 0.0 : ez * fabs((double)r.iz) * k) + fabs((double)oiz) * u + fr(r.iz, oz)) * k;
+  r.nbx = f32_down(-(double)oix - Dx);
+  r.nby = f32_down(-(double)oiy - Dy);
+  r.nbz = f32_down(-(double)oiz - Dz);
+  r.fbx = f32_up(-(double)oix + Dx);
+  r.fby = f32_up(-(double)oiy + Dy);
+  r.fbz = f32_up(-(double)oiz + Dz);
   r.tmin = f32_down(tmin);
   if (NF == rpl::NODES_Q8) {
     r.sx = r.ix < 0.0f ? 0x07060504u : 0x03020100u;
@@ -587,22 +592,24 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       ch = *reinterpret_cast<const uint4*>(nb + (no + 48u));
       // per axis: A = s inv, B = fma(o, inv, -oinv); plane t^ = fma(q, A, B)
       const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
-      const float Bx = fmaf(c0.x, r.ix, -r.oix), By = fmaf(c0.y, r.iy, -r.oiy), Bz = fmaf(c0.z, r.iz, -r.oiz);
+      const float Bnx = fmaf(c0.x, r.ix, r.nbx), Bny = fmaf(c0.y, r.iy, r.nby), Bnz = fmaf(c0.z, r.iz, r.nbz);
+      const float Bfx = fmaf(c0.x, r.ix, r.fbx), Bfy = fmaf(c0.y, r.iy, r.fby), Bfz = fmaf(c0.z, r.iz, r.fbz);
       const uint32_t qnx = __builtin_amdgcn_perm(c1.w, c1.z, r.sx), qfx = __builtin_amdgcn_perm(c1.z, c1.w, r.sx);
       const uint32_t qny = __builtin_amdgcn_perm(c2.y, c2.x, r.sy), qfy = __builtin_amdgcn_perm(c2.x, c2.y, r.sy);
       const uint32_t qnz = __builtin_amdgcn_perm(c2.w, c2.z, r.sz), qfz = __builtin_amdgcn_perm(c2.z, c2.w, r.sz);
       // children (0,1) and (2,3) as packed pairs: v_pk_fma_f32 is two fused FMAs with the same per-element
       // rounding as fmaf; byte b of a code word converts with v_cvt_f32_ubyte<b>
-      const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az}, bx = {Bx, Bx}, by = {By, By}, bz = {Bz, Bz};
+      const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az};
+      const f2 bnx = {Bnx, Bnx}, bny = {Bny, Bny}, bnz = {Bnz, Bnz}, bfx = {Bfx, Bfx}, bfy = {Bfy, Bfy}, bfz = {Bfz, Bfz};
 #define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
 #pragma unroll
       for (int q = 0; q < 2; q++) {
-        NX[q] = pk_fma(RPK_Q2(qnx, q), ax, bx);
-        FX[q] = pk_fma(RPK_Q2(qfx, q), ax, bx);
-        NY[q] = pk_fma(RPK_Q2(qny, q), ay, by);
-        FY[q] = pk_fma(RPK_Q2(qfy, q), ay, by);
-        NZ[q] = pk_fma(RPK_Q2(qnz, q), az, bz);
-        FZ[q] = pk_fma(RPK_Q2(qfz, q), az, bz);
+        NX[q] = pk_fma(RPK_Q2(qnx, q), ax, bnx);
+        FX[q] = pk_fma(RPK_Q2(qfx, q), ax, bfx);
+        NY[q] = pk_fma(RPK_Q2(qny, q), ay, bny);
+        FY[q] = pk_fma(RPK_Q2(qfy, q), ay, bfy);
+        NZ[q] = pk_fma(RPK_Q2(qnz, q), az, bnz);
+        FZ[q] = pk_fma(RPK_Q2(qfz, q), az, bfz);
       }
 #undef RPK_Q2
     } else {
@@ -615,13 +622,14 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.sz ^ 16u)));
       ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
       const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
-      const f2 nox = {-r.oix, -r.oix}, noy = {-r.oiy, -r.oiy}, noz = {-r.oiz, -r.oiz};
-      NX[0] = pk_fma(f2{nx.x, nx.y}, ix, nox); NX[1] = pk_fma(f2{nx.z, nx.w}, ix, nox);
-      FX[0] = pk_fma(f2{fx.x, fx.y}, ix, nox); FX[1] = pk_fma(f2{fx.z, fx.w}, ix, nox);
-      NY[0] = pk_fma(f2{ny.x, ny.y}, iy, noy); NY[1] = pk_fma(f2{ny.z, ny.w}, iy, noy);
-      FY[0] = pk_fma(f2{fy.x, fy.y}, iy, noy); FY[1] = pk_fma(f2{fy.z, fy.w}, iy, noy);
-      NZ[0] = pk_fma(f2{nz.x, nz.y}, iz, noz); NZ[1] = pk_fma(f2{nz.z, nz.w}, iz, noz);
-      FZ[0] = pk_fma(f2{fz.x, fz.y}, iz, noz); FZ[1] = pk_fma(f2{fz.z, fz.w}, iz, noz);
+      const f2 nbx = {r.nbx, r.nbx}, nby = {r.nby, r.nby}, nbz = {r.nbz, r.nbz};
+      const f2 fbx = {r.fbx, r.fbx}, fby = {r.fby, r.fby}, fbz = {r.fbz, r.fbz};
+      NX[0] = pk_fma(f2{nx.x, nx.y}, ix, nbx); NX[1] = pk_fma(f2{nx.z, nx.w}, ix, nbx);
+      FX[0] = pk_fma(f2{fx.x, fx.y}, ix, fbx); FX[1] = pk_fma(f2{fx.z, fx.w}, ix, fbx);
+      NY[0] = pk_fma(f2{ny.x, ny.y}, iy, nby); NY[1] = pk_fma(f2{ny.z, ny.w}, iy, nby);
+      FY[0] = pk_fma(f2{fy.x, fy.y}, iy, fby); FY[1] = pk_fma(f2{fy.z, fy.w}, iy, fby);
+      NZ[0] = pk_fma(f2{nz.x, nz.y}, iz, nbz); NZ[1] = pk_fma(f2{nz.z, nz.w}, iz, nbz);
+      FZ[0] = pk_fma(f2{fz.x, fz.y}, iz, fbz); FZ[1] = pk_fma(f2{fz.z, fz.w}, iz, fbz);
     }
     float tn[4];
     uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
@@ -633,8 +641,8 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
         TN[q][e] = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
         TF[q][e] = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
       }
-      // fma(tnear, 1 - 2^-19, -slack) <= tfar (section 4.2 of DESIGN.md): one packed FMA per pair
-      const f2 lhs = pk_fma(TN[q], f2{1.0f - 0x1p-19f, 1.0f - 0x1p-19f}, f2{-r.slack, -r.slack});
+      // fma(tnear, 1 - 2^-19, -2^-100) <= tfar (section 4.2 of DESIGN.md): one packed FMA per pair
+      const f2 lhs = pk_fma(TN[q], f2{1.0f - 0x1p-19f, 1.0f - 0x1p-19f}, f2{-0x1p-100f, -0x1p-100f});
 #pragma unroll
       for (int e = 0; e < 2; e++) {
         const int c = 2 * q + e;

@@ -413,9 +413,10 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba) {
 
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
                             uint64_t* per_ray) {
-  // CPU model of rp_device.h's traversal over the same packed 4-wide tree: quantized child boxes tested
-  // in f32 (t = fma(q, s inv, fma(o, inv, -oinv)) + slack, rcp emulated by a correctly rounded 1/x, the
-  // min/max slab form instead of the device's octant selection: the same values), near-first order, exact f64
+  // CPU model of rp_device.h's traversal over the same packed 4-wide tree: child boxes tested in f32 with
+  // per-axis outward bounds (t = fma(P, inv, nb|fb), quantized: fma(q, s inv, fma(o, inv, nb|fb))), rcp
+  // emulated by a correctly rounded 1/x, the min/max slab form instead of the device's octant selection
+  // (the same values), near-first order, exact f64
   // primitive tests.  per_ray: n x 3 {wide nodes visited, primitive tests, closest hittable id or
   // 2^64-1}.  tests/test_bvh.py checks the closest hits against brute force.
   std::string err;
@@ -433,19 +434,21 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
     const double* q = rays + 8 * r;
     const double o[3] = {q[0], q[1], q[2]}, d[3] = {q[3], q[4], q[5]};
     const double tmin = q[6];
-    float inv[3], oinv[3];
-    double D = 0.0;
+    float inv[3], nb[3], fb[3];  // per axis: slope, near- and far-plane addends (rp_device.h setup_ray32)
     for (int k = 0; k < 3; k++) {
       const float o32 = (float)o[k];
       inv[k] = std::fmin(std::fmax(1.0f / (float)d[k], -0x1p64f), 0x1p64f);
-      oinv[k] = o32 * inv[k];
+      const float oinv = o32 * inv[k];
       const double e = std::fabs(o[k] - (double)o32);
-      D = std::fmax(D, (e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv[k]) * 0x1p-23 +
-                           ((!q8 || (std::fabs(inv[k]) == 0x1p64f && o32 == 0.0f))
-                                ? 0.0
-                                : std::fabs((double)inv[k]) * (2.0 * ps.qbound + std::fabs((double)o32)) * 0x1p-23 * (1.0 + 0x1p-20)));
+      const double Dk = ((e == 0.0 ? 0.0 : e * std::fabs((double)inv[k]) * (1.0 + 0x1p-20)) + std::fabs((double)oinv) * 0x1p-23 +
+                         ((!q8 || (std::fabs(inv[k]) == 0x1p64f && o32 == 0.0f))
+                              ? 0.0
+                              : std::fabs((double)inv[k]) * (2.0 * ps.qbound + std::fabs((double)o32)) * 0x1p-23 * (1.0 + 0x1p-20))) *
+                        (1.0 + 0x1p-20);
+      nb[k] = down(-(double)oinv - Dk);
+      fb[k] = up(-(double)oinv + Dk);
     }
-    const float slack = up(3.0 * D * (1.0 + 0x1p-20) + 0x1p-100), tmin32 = down(tmin);
+    const float tmin32 = down(tmin);
     double best = q[7];
     float best32 = up(best);
     int64_t bestp = -1;
@@ -496,22 +499,25 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
     for (;;) {
       while (!(cur & rpl::ENTRY_LEAF)) {
         visits++;
-        float lo4[4][3], hi4[4][3];
         const uint32_t* child;
+        float near4[4][3], far4[4][3];  // per child and axis: both planes with the near / far addend
         if (q8) {
           const rpl::Node4Q& nd = ps.qnodes[cur];
-          float A[3], B[3];
+          float A[3], Bn[3], Bf[3];
           for (int k = 0; k < 3; k++) {
             A[k] = nd.s[k] * inv[k];
-            B[k] = std::fma(nd.o[k], inv[k], -oinv[k]);
+            Bn[k] = std::fma(nd.o[k], inv[k], nb[k]);
+            Bf[k] = std::fma(nd.o[k], inv[k], fb[k]);
           }
           const uint8_t* L[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
           const uint8_t* H[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
           // plane t values directly: t = fma(q, A, B) (the device's dequantized form)
           for (int c = 0; c < 4; c++)
             for (int k = 0; k < 3; k++) {
-              lo4[c][k] = std::fma((float)L[k][c], A[k], B[k]);
-              hi4[c][k] = std::fma((float)H[k][c], A[k], B[k]);
+              const float a = std::fma((float)L[k][c], A[k], Bn[k]), b = std::fma((float)H[k][c], A[k], Bn[k]);
+              const float a2 = std::fma((float)L[k][c], A[k], Bf[k]), b2 = std::fma((float)H[k][c], A[k], Bf[k]);
+              near4[c][k] = std::fmin(a, b);
+              far4[c][k] = std::fmax(a2, b2);
             }
           child = nd.child;
         } else {
@@ -520,8 +526,10 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
           const float* hi[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
           for (int c = 0; c < 4; c++)
             for (int k = 0; k < 3; k++) {
-              lo4[c][k] = std::fma(lo[k][c], inv[k], -oinv[k]);
-              hi4[c][k] = std::fma(hi[k][c], inv[k], -oinv[k]);
+              const float a = std::fma(lo[k][c], inv[k], nb[k]), b = std::fma(hi[k][c], inv[k], nb[k]);
+              const float a2 = std::fma(lo[k][c], inv[k], fb[k]), b2 = std::fma(hi[k][c], inv[k], fb[k]);
+              near4[c][k] = std::fmin(a, b);
+              far4[c][k] = std::fmax(a2, b2);
             }
           child = nd.child;
         }
@@ -530,11 +538,10 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
         for (int c = 0; c < 4; c++) {
           float tnear = tmin32, tfar = best32;
           for (int k = 0; k < 3; k++) {
-            const float a = lo4[c][k], b = hi4[c][k];
-            tnear = std::fmax(tnear, std::fmin(a, b));
-            tfar = std::fmin(tfar, std::fmax(a, b));
+            tnear = std::fmax(tnear, near4[c][k]);
+            tfar = std::fmin(tfar, far4[c][k]);
           }
-          const bool hit = std::fma(tnear, 1.0f - 0x1p-19f, -slack) <= tfar && child[c] != rpl::ENTRY_EMPTY;
+          const bool hit = std::fma(tnear, 1.0f - 0x1p-19f, -0x1p-100f) <= tfar && child[c] != rpl::ENTRY_EMPTY;
           tn[c] = hit ? tnear : INFINITY;
           cc[c] = child[c];
         }

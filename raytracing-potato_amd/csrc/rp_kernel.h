@@ -40,7 +40,10 @@ enum { DIAG_N = 320 };
 // Timeline histograms (RPK_DIAG builds), 64 bins of DIAG_BIN_TICKS (100 MHz real-time clock) from the
 // block's start: [64 + b] lanes retiring in bin b, [128 + b] rays of the pixels fetched in bin b,
 // [192 + b] pixels fetched in bin b, [256 + b] the most rays of one unit fetched in bin b.
-enum { DIAG_HIST = 64, DIAG_BIN_TICKS = 1000000 };
+#ifndef RPK_DIAG_BIN_TICKS
+#define RPK_DIAG_BIN_TICKS 1000000
+#endif
+enum { DIAG_HIST = 64, DIAG_BIN_TICKS = RPK_DIAG_BIN_TICKS };
 // Region counters (RPK_DIAG builds), from DIAG_N index 16: per code region r, [16 + 2r] = wave
 // executions and [17 + 2r] = active lanes summed over them (lane utilisation = lanes / (64 x execs)).
 enum {

@@ -249,6 +249,11 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             atomicAdd(&A->diag[128 + b], (unsigned long long)(lane_rays - rays_pix));
             atomicAdd(&A->diag[192 + b], 1ull);
             atomicMax(&A->diag[256 + b], (unsigned long long)(lane_rays - rays_pix));
+            {  // the slowest unit of the frame: duration (100 MHz ticks), its pixel and batch, and its rays
+              const uint64_t now = __builtin_amdgcn_s_memrealtime();
+              atomicMax(&A->diag[13], ((now - t_pix) << 32) | ((uint64_t)batch << 28) | (uint64_t)(pipj & 0x0FFFFFFFu));
+              atomicMax(&A->diag[14], ((now - t_pix) << 32) | (uint64_t)(lane_rays - rays_pix));
+            }
             t_pix = __builtin_amdgcn_s_memrealtime();
             rays_pix = lane_rays;
           })
@@ -466,6 +471,9 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
 // tile index.  Padding keys sort last.
 static constexpr int SORT_BLOCK = 1024;
 static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
+#ifndef RPK_SORT_Q
+#define RPK_SORT_Q 4.0f  // buckets per octave of cost
+#endif
 __device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every other bit of 16
   v = (v | (v << 4)) & 0x0F0Fu;
   v = (v | (v << 2)) & 0x3333u;
@@ -495,8 +503,8 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
         // quarter-octave buckets of the costliest probed sample's cost and of the mean cost (C3: 2^(1/4)
         // steps 248.1 ms, 2^(1/32) steps 250.1 ms, the round-1 ray-count cost 254.7 ms per frame)
         const float mean = (float)cost[i] / (float)probe_px;
-        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * 4.0f), 63u);
-        qm = min((uint32_t)(log2f(mean + 1.0f) * 4.0f), 63u);
+        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * RPK_SORT_Q), 63u);
+        qm = min((uint32_t)(log2f(mean + 1.0f) * RPK_SORT_Q), 63u);
       }
       kk = ((63u - ql) << 22) | ((63u - qm) << 16) | (spread8(ty) << 1) | spread8(tx);
     }

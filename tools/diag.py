@@ -44,8 +44,11 @@ def main():
         "wave_cycles_per_iteration": round(tot / max(1, iters), 1),
         "traverse_cycles_per_trip": round(ph[2] / max(1, trips), 1),
     }
+    slow = {"ticks": d[13] >> 32, "ms": round((d[13] >> 32) / 1e5, 3), "pixel": [d[13] & 0xFFFF, (d[13] >> 16) & 0xFFF],
+            "batch": (d[13] >> 28) & 0xF, "rays": d[14] & 0xFFFFFFFF}
     t0, tq, t1 = (~d[10]) & (2**64 - 1), (~d[11]) & (2**64 - 1), d[12]
     if t1 > t0:  # 100 MHz real-time clock
+        out["slowest_unit"] = slow
         out["timeline_ms"] = {"queue_drained": round((tq - t0) / 1e5, 3), "last_exit": round((t1 - t0) / 1e5, 3),
                               "tail_frac": round((t1 - tq) / (t1 - t0), 4)}
     regions = ["node", "prim", "step", "shade", "surface", "sph_uv", "texture", "lambert", "metal", "dielectric",
