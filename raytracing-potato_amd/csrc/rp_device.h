@@ -345,8 +345,8 @@ RPK_INLINE double noise_real(int64_t x, int64_t y, int64_t z, int64_t seed) {
 // ------------------------------------------------------------------ traversal --------------------
 
 struct HitRec {
-  double t;
-  int32_t prim;  // -1 = miss
+  double t, u, v;  // u, v: barycentrics of hittable.rs:89-95 (triangles)
+  int32_t prim;    // -1 = miss
 };
 
 struct TravDiag {
@@ -456,10 +456,8 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
 // The traversal state is explicit (TravState) so a lane can stop between steps and resume later: the
 // render kernel steps traversal until few lanes are still traversing, shades the finished ones and
 // gives them new rays, then resumes (see render_kernel).
-// The closest triangle's barycentrics are not carried through the traversal: surface() recomputes them
-// with the identical expressions (tri_solve), which frees 4 VGPRs across the traversal loop.
 struct TravState {
-  double best;
+  double best, bu, bv;
   int32_t bestp;
   uint32_t cur, sp;
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
@@ -469,34 +467,16 @@ RPK_INLINE bool trav_done(const TravState& t) { return t.cur == rpl::ENTRY_EMPTY
 
 RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
   t.best = tmax;
+  t.bu = 0.0;
+  t.bv = 0.0;
   t.bestp = -1;
   t.cur = S.root;
   t.sp = 0;
   t.leaf = 0;
 }
 
-// hittable.rs:65-101 for one triangle {a, a-b, a-c}: det, t, u, v in the reference's expression order (ba, ca
-// pre-subtracted: the same IEEE op).  prim_test and surface share it, so the recomputed barycentrics of the
-// closest hit are the accepted test's bit for bit.
-RPK_INLINE double tri_solve(V3 a, V3 ba, V3 ca, V3 o, V3 d, double& t, double& u, double& v) {
-  const V3 pa = sub(a, o);
-  const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
-                   - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
-  const double inv_det = 1.0 / det;
-  t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
-     + pa.y * (ba.z * ca.x - ba.x * ca.z)
-     + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
-  u = (pa.x * (ca.y * d.z - ca.z * d.y)
-     + pa.y * (ca.z * d.x - ca.x * d.z)
-     + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
-  v = (pa.x * (ba.z * d.y - ba.y * d.z)
-     + pa.y * (ba.x * d.z - ba.z * d.x)
-     + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
-  return det;
-}
-
 // One exact f64 primitive test (the reference's Hittable::hit for a leaf, hittable.rs:39-101): on
-// acceptance `best` shrinks to t and the primitive is recorded.
+// acceptance `best` shrinks to t and the hit record is taken.
 RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, double& best, TravState& ts) {
   // 32-bit byte offset from the wave-uniform base (scalar-base + vector-offset loads)
   const double2* q = reinterpret_cast<const double2*>(reinterpret_cast<const char*>(S.prims) +
@@ -509,12 +489,23 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
     const V3 a = v3(g01.x, g01.y, g23.x);
     const V3 ba = v3(g23.y, g45.x, g45.y);
     const V3 ca = v3(g67.x, g67.y, g8k.x);
-    double t, u, v;
-    const double det = tri_solve(a, ba, ca, o, d, t, u, v);
+    const V3 pa = sub(a, o);
+    const double det = ba.x * ca.y * d.z + ba.y * ca.z * d.x + ba.z * ca.x * d.y
+                     - ba.x * ca.z * d.y - ba.y * ca.x * d.z - ba.z * ca.y * d.x;
     if (fabs(det) < SMOL) return;
+    const double inv_det = 1.0 / det;
+    const double t = (pa.x * (ba.y * ca.z - ba.z * ca.y)
+                    + pa.y * (ba.z * ca.x - ba.x * ca.z)
+                    + pa.z * (ba.x * ca.y - ba.y * ca.x)) * inv_det;
+    const double u = (pa.x * (ca.y * d.z - ca.z * d.y)
+                    + pa.y * (ca.z * d.x - ca.x * d.z)
+                    + pa.z * (ca.x * d.y - ca.y * d.x)) * inv_det;
+    const double v = (pa.x * (ba.z * d.y - ba.y * d.z)
+                    + pa.y * (ba.x * d.z - ba.z * d.x)
+                    + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
     const double w = 1.0 - u - v;
     if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) return;
-    best = t; ts.bestp = (int32_t)k;
+    best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
   } else {
     // hittable.rs:39-57
     const V3 c = v3(g01.x, g01.y, g23.x);
@@ -756,6 +747,8 @@ RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V
   trav_begin(S, o, d, tmin, tmax, t);
   while (!trav_done(t)) trav_step<false, NF>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
+  hr.u = t.bu;
+  hr.v = t.bv;
   hr.prim = t.bestp;
 }
 
@@ -776,10 +769,7 @@ RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, 
   s.v = 0.0;
   const bool need_uv = force_uv || S.mats[s.material].needs_uv != 0;
   if (p->kind == rpl::PRIM_TRIANGLE) {
-    double tt, u, v;
-    (void)tri_solve(v3(p->g[0], p->g[1], p->g[2]), v3(p->g[3], p->g[4], p->g[5]), v3(p->g[6], p->g[7], p->g[8]), o, d,
-                    tt, u, v);
-    const double w = 1.0 - u - v;
+    const double u = hr.u, v = hr.v, w = 1.0 - u - v;
     const rpl::PrimRef& pr = S.prim_refs[hr.prim];
     const uint32_t i0 = pr.v[0], i1 = pr.v[1], i2 = pr.v[2];
     const V3 n0 = v3(S.vnrm[3 * i0], S.vnrm[3 * i0 + 1], S.vnrm[3 * i0 + 2]);

@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   ts.sp = 0u;
   ts.best = 0.0;
   ts.bestp = -1;
+  ts.bu = ts.bv = 0.0;
   uint32_t pi = 0, pj = 0;
   bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
   pipj = pi | (pj << 16);
@@ -193,6 +194,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       DIAG(lane_rays++;)
       HitRec hr;
       hr.t = ts.best;
+      hr.u = ts.bu;
+      hr.v = ts.bv;
       hr.prim = ts.bestp;
 
       // ---- shade.  Hits and misses share one spherical-uv site and one texture-sampling site, so a wave

@@ -155,6 +155,8 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
     sz = w.in.sum[2 * P + i];
     HitRec hr;
     hr.t = w.hit[i];
+    hr.u = w.hit[P + i];
+    hr.v = w.hit[2 * P + i];
     hr.prim = w.prim[i];
     const bool first = (s & FIRST_BIT) != 0u;
     s &= ~FIRST_BIT;
@@ -273,6 +275,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
   ts.sp = 0u;
   ts.best = 0.0;
   ts.bestp = -1;
+  ts.bu = ts.bv = 0.0;
   for (;;) {
     const uint64_t idle = __ballot(!have);
     if (!drained && idle != 0 && ((uint32_t)__popcll(idle) >= RPK_WF_REFILL || __ballot(have) == 0)) {
@@ -301,6 +304,8 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
       trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
       if (trav_done(ts)) {
         w.hit[q] = ts.best;
+        w.hit[P + q] = ts.bu;
+        w.hit[2 * P + q] = ts.bv;
         w.prim[q] = ts.bestp;
         have = false;
       }
