@@ -195,7 +195,7 @@ enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
 /* Wide-node formats: 128 B f32 child boxes, or 64 B child boxes quantized to 8 bits per plane in a per-node
  * f32 frame (half the node bytes, more ALU per visit).  AUTO = Q8 for host-built trees of >= 2^21 hittables,
  * F32 otherwise. */
-enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2 };
+enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2, RP_NODES_W8 = 3 };
 /* Tile orders: PLAIN = shard order (row-major); COST = a probe launch traces sample 0 of a lattice of pixels
  * per tile and the costliest tiles go first (short frame tail); MORTON = Z-order of the tiles (neighbouring
  * tiles run together: a small cache working set).  AUTO = COST while the scene fits the 256 MB Infinity

@@ -287,7 +287,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
   if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
   if (o.wf_slots > 64) return fail(RP_EINVAL, "options.wf_slots must be 1..64");
-  if (o.node_format > RP_NODES_Q8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
+  if (o.node_format > RP_NODES_W8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
   if (o.leaf_break > 64) return fail(RP_EINVAL, "options.leaf_break must be 0..64");
   return RP_OK;
 }
@@ -331,7 +331,7 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
 }
 
 size_t rp_node_bytes(uint32_t node_format) {
-  return node_format == rpl::NODES_Q8 ? sizeof(rpl::Node4Q) : sizeof(rpl::Node4);
+  return node_format == rpl::NODES_W8 ? sizeof(rpl::Node8Q) : node_format == rpl::NODES_Q8 ? sizeof(rpl::Node4Q) : sizeof(rpl::Node4);
 }
 
 int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* opt_in, rp_scene** out) {
@@ -357,6 +357,8 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // (the device LBVH: 1.1 s) and renders 24 % faster; the LBVH stays an option.
   const bool gpu_build = opt.builder == RP_BUILDER_DEVICE;
   const bool use_gpu = gpu_build && desc->n_hittables >= 2;  // the LBVH needs two primitives
+  if (gpu_build && opt.node_format == RP_NODES_W8)
+    return fail(RP_EINVAL, "the device builder makes 4-wide trees (options.node_format RP_NODES_F32 or RP_NODES_Q8)");
   bo.tables_only = use_gpu;
   bo.max_leaf = opt.max_leaf;
   bo.cost_traverse = opt.cost_traverse;
@@ -412,8 +414,9 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
       chk.qbound = gt.qbound;
       if ((rc = rpb::check(chk, err))) return bail(fail(rc, "device BVH self-check: " + err));
     }
-  } else if ((rc = node_format == rpl::NODES_Q8 ? upload(ps.qnodes, (rpl::Node4Q**)&s->d_nodes)
-                                                    : upload(ps.nodes, (rpl::Node4**)&s->d_nodes)) ||
+  } else if ((rc = node_format == rpl::NODES_W8   ? upload(ps.wnodes, (rpl::Node8Q**)&s->d_nodes)
+                   : node_format == rpl::NODES_Q8 ? upload(ps.qnodes, (rpl::Node4Q**)&s->d_nodes)
+                                                  : upload(ps.nodes, (rpl::Node4**)&s->d_nodes)) ||
              (rc = upload(ps.prims, &s->d_prims)) ||
              (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
     return bail(rc);
@@ -442,6 +445,8 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
   // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
   s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
+  // Node8Q: groups of two words, per level at most the rest of a node group and one primitive group
+  if (node_format == rpl::NODES_W8) s->ks.stack_depth = 4 * (ps.max_depth + 1) + 3;
   // floor of 17 entries: the spill split below never keeps fewer in LDS (options.lds_depth tests force 17)
   if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
   s->n_nodes = n_tree_nodes;

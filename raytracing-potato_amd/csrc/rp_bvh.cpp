@@ -385,7 +385,8 @@ struct ParallelBuild {
 
 // The quantization frame of a wide node from its exact box (rp_layout.h qframe); an axis without a finite
 // extent (NaN geometry only) gets the frame at 0.
-void node_frame(const Box& b, rpl::Node4Q& n) {
+template <class N>
+void node_frame(const Box& b, N& n) {
   for (int a = 0; a < 3; a++) {
     const bool ok = std::isfinite(b.lo[a]) && std::isfinite(b.hi[a]) && b.lo[a] <= b.hi[a];
     rpl::qframe(ok ? b.lo[a] : 0.0, ok ? b.hi[a] : 0.0, n.o[a], n.s[a]);
@@ -505,6 +506,135 @@ struct Collapser {
     } else {
       for (int c = 0, j = 0; c < nk; c++)
         if (!bin[kids[c]].leaf()) fill(fam + (uint32_t)j++, kids[c], depth + 1);
+    }
+  }
+};
+
+// Collapse the binary tree into 8-wide quantized nodes (rp_layout.h Node8Q): the same opening rule as Collapser
+// up to 8 children; each child goes to the slot of the octant its box centre lies in relative to the node's
+// centre (greedy assignment by the largest alignment of centre offset and slot direction, Ylitie et al. 2017), so
+// that a ray's rank order slot ^ octant approximates near-first.  Records are numbered in families as in
+// Collapser (inner children consecutive, in slot order); the leaf children's primitives are re-laid out as one
+// run per node in slot order (`prims`: positions in the binary tree's leaf order), depth-first.  With par > 1 the
+// inner children's subtrees are collapsed on threads and spliced: the serial numbering, records and run order.
+struct Collapser8 {
+  const std::vector<BinNode>& bin;
+  const std::vector<uint32_t>& leaf_order;  // binary leaf order: BinNode first/count index it
+  unsigned par = 1;
+  std::vector<rpl::Node8Q> nodes;
+  std::vector<uint32_t> prims;  // hittable ids in the new leaf order
+  uint32_t max_depth = 0;
+
+  uint32_t emit_root(int32_t bi) {
+    nodes.emplace_back();
+    fill(0, bi, 0);
+    return 0;
+  }
+  // record i of another collapse into slot `dst`, its family index shifted by `ns` and its run by `ps`
+  void put(uint32_t dst, const Collapser8& o, uint32_t i, uint32_t ns, uint32_t ps) {
+    rpl::Node8Q n = o.nodes[i];
+    if (n.inner >> 24) n.inner = (n.inner & ~rpl::W8_INDEX) | (((n.inner & rpl::W8_INDEX) + ns) & rpl::W8_INDEX);
+    n.prim += ps;
+    nodes[dst] = n;
+  }
+
+  void fill(uint32_t self, int32_t bi, uint32_t depth) {
+    if (depth > max_depth) max_depth = depth;
+    int32_t kids[8];
+    int nk = 0;
+    if (bin[bi].leaf()) {
+      kids[nk++] = bi;
+    } else {
+      kids[nk++] = bin[bi].left;
+      kids[nk++] = bin[bi].right;
+      while (nk < 8) {
+        int best = -1;
+        double area = -1.0;
+        for (int k = 0; k < nk; k++)
+          if (!bin[kids[k]].leaf() && bin[kids[k]].box.area() > area) { area = bin[kids[k]].box.area(); best = k; }
+        if (best < 0) break;
+        const int32_t open = kids[best];
+        kids[best] = bin[open].left;
+        kids[nk++] = bin[open].right;
+      }
+    }
+    Box nb;
+    nb.reset();
+    for (int k = 0; k < nk; k++) nb.grow(bin[kids[k]].box);
+    // slot assignment: greedy on score(k, s) = sum over axes of +-(centre_k - centre_node)
+    int32_t at[8];
+    for (int s = 0; s < 8; s++) at[s] = -1;
+    {
+      double sc[8][8];
+      for (int k = 0; k < nk; k++) {
+        double v[3];
+        for (int a = 0; a < 3; a++) v[a] = 0.5 * (bin[kids[k]].box.lo[a] + bin[kids[k]].box.hi[a]) - 0.5 * (nb.lo[a] + nb.hi[a]);
+        for (int s = 0; s < 8; s++) {
+          double t = 0.0;
+          for (int a = 0; a < 3; a++) t += (s >> a & 1) ? v[a] : -v[a];
+          sc[k][s] = t == t ? t : 0.0;  // NaN geometry: no preference
+        }
+      }
+      bool used_k[8] = {false, false, false, false, false, false, false, false};
+      for (int round = 0; round < nk; round++) {
+        int bk = -1, bs = -1;
+        double bv = -HUGE_VAL;
+        for (int k = 0; k < nk; k++) {
+          if (used_k[k]) continue;
+          for (int s = 0; s < 8; s++)
+            if (at[s] < 0 && (bk < 0 || sc[k][s] > bv)) { bv = sc[k][s]; bk = k; bs = s; }
+        }
+        used_k[bk] = true;
+        at[bs] = bk;
+      }
+    }
+    rpl::Node8Q& n = nodes[self];
+    node_frame(nb, n);
+    n.prim = (uint32_t)prims.size();
+    uint32_t imask = 0, off = 0;
+    for (int s = 0; s < 8; s++) {
+      n.pmask[s] = 0;
+      if (at[s] < 0) { rpl::empty_child(n, s); continue; }
+      const BinNode& k = bin[kids[at[s]]];
+      rpl::quantize_child(n, s, k.box.lo, k.box.hi);
+      if (k.leaf()) {
+        n.pmask[s] = (uint32_t)(((1ull << k.count) - 1ull) << off);
+        for (uint32_t q = 0; q < k.count; q++) prims.push_back(leaf_order[k.first + q]);
+        off += k.count;
+      } else {
+        imask |= 1u << s;
+      }
+    }
+    for (int q = 0; q < 4; q++) n.pad[q] = 0;
+    const uint32_t inner = (uint32_t)__builtin_popcount(imask);
+    const uint32_t fam = inner ? (uint32_t)nodes.size() : 0u;
+    if (inner) nodes.resize(nodes.size() + inner);
+    nodes[self].inner = (fam & rpl::W8_INDEX) | imask << 24;  // (nodes may have moved)
+    if (par > 1 && inner >= 2) {
+      std::vector<std::unique_ptr<Collapser8>> sub;
+      std::vector<std::thread> th;
+      for (int s = 0; s < 8; s++) {
+        if (!(imask >> s & 1u)) continue;
+        sub.emplace_back(new Collapser8{bin, leaf_order, std::max(1u, par / inner), {}, {}, 0});
+        Collapser8* sc = sub.back().get();
+        const int32_t kb = kids[at[s]];
+        th.emplace_back([sc, kb] { sc->emit_root(kb); });
+      }
+      for (auto& t : th) t.join();
+      for (uint32_t j = 0; j < inner; j++) {
+        Collapser8& sc = *sub[j];
+        const uint32_t base = (uint32_t)nodes.size();
+        const uint32_t pbase = (uint32_t)prims.size();
+        const uint32_t m = (uint32_t)sc.nodes.size();
+        nodes.resize(nodes.size() + m - 1u);
+        put(fam + j, sc, 0, base - 1u, pbase);
+        for (uint32_t i = 1; i < m; i++) put(base + i - 1u, sc, i, base - 1u, pbase);
+        prims.insert(prims.end(), sc.prims.begin(), sc.prims.end());
+        max_depth = std::max(max_depth, depth + 1 + sc.max_depth);
+      }
+    } else {
+      for (int s = 0, j = 0; s < 8; s++)
+        if (imask >> s & 1u) fill(fam + (uint32_t)j++, kids[at[s]], depth + 1);
     }
   }
 };
@@ -690,7 +820,7 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   for (int k = 0; k < 3; k++) out.background.color[k] = d->background.color[k];
 
   if (opt.tables_only) return RP_OK;
-  if (opt.node_format > rpl::NODES_Q8) { err = "unknown node format"; return RP_EINVAL; }
+  if (opt.node_format > rpl::NODES_W8) { err = "unknown node format"; return RP_EINVAL; }
 
   // ---- BVH over all hittables (a List root is served by the same tree: closest hit is
   //      independent of visit order except exact-t ties)
@@ -739,7 +869,11 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   for (const Ref& r : refs)
     for (int k = 0; k < 3; k++) amax = max_(max_(amax, std::fabs(r.box.lo[k])), std::fabs(r.box.hi[k]));
   out.node_format = opt.node_format ? opt.node_format : auto_node_format(d->n_hittables, amax);
-  if (out.node_format == rpl::NODES_Q8 && !(amax <= rpl::COORD_MAX)) {
+  if (out.node_format == rpl::NODES_W8 && opt.max_leaf > rpl::W8_MAX_LEAF) {
+    err = "the 8-wide nodes hold leaves of at most 4 primitives (max_leaf <= 4)";
+    return RP_EINVAL;
+  }
+  if (out.node_format != rpl::NODES_F32 && !(amax <= rpl::COORD_MAX)) {
     err = "primitive coordinates beyond +-2^54 (or infinite) are not supported by the quantized nodes";
     return RP_EINVAL;
   }
@@ -750,7 +884,12 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   bin.reserve(n_tree ? 2 * (size_t)n_tree : 1);
   Builder B{opt, refs, bin, order};
   if (n_tree == 0) {
-    if (out.node_format == rpl::NODES_Q8) {
+    if (out.node_format == rpl::NODES_W8) {
+      rpl::Node8Q root{};
+      for (int a = 0; a < 3; a++) rpl::qframe(0.0, 0.0, root.o[a], root.s[a]);
+      for (int c = 0; c < 8; c++) rpl::empty_child(root, c);
+      out.wnodes.push_back(root);
+    } else if (out.node_format == rpl::NODES_Q8) {
       rpl::Node4Q root{};
       for (int a = 0; a < 3; a++) rpl::qframe(0.0, 0.0, root.o[a], root.s[a]);
       for (int c = 0; c < 4; c++) {
@@ -778,13 +917,24 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
     } else {
       B.build(0, n_tree, all);
     }
-    Collapser C{bin, out.node_format, threads, {}, {}, 0};
-    if (out.node_format == rpl::NODES_Q8) C.qnodes.reserve(bin.size() / 2 + 1);
-    else C.nodes.reserve(bin.size() / 2 + 1);
-    C.emit_root(0);
-    out.nodes.swap(C.nodes);
-    out.qnodes.swap(C.qnodes);
-    out.max_depth = C.max_depth;
+    if (out.node_format == rpl::NODES_W8) {
+      Collapser8 C{bin, order, threads, {}, {}, 0};
+      C.nodes.reserve(bin.size() / 6 + 1);
+      C.prims.reserve(order.size());
+      C.emit_root(0);
+      if (C.nodes.size() > rpl::W8_MAX_NODES) { err = "too many 8-wide nodes (> 2^24)"; return RP_EINVAL; }
+      out.wnodes.swap(C.nodes);
+      order.swap(C.prims);  // the tree's primitives in the 8-wide leaf order
+      out.max_depth = C.max_depth;
+    } else {
+      Collapser C{bin, out.node_format, threads, {}, {}, 0};
+      if (out.node_format == rpl::NODES_Q8) C.qnodes.reserve(bin.size() / 2 + 1);
+      else C.nodes.reserve(bin.size() / 2 + 1);
+      C.emit_root(0);
+      out.nodes.swap(C.nodes);
+      out.qnodes.swap(C.qnodes);
+      out.max_depth = C.max_depth;
+    }
   }
   out.root = 0;
   out.n_leaves = B.n_leaves;
@@ -880,7 +1030,61 @@ int check(const PackedScene& s, std::string& err) {
       }
     }
   };
-  if (s.node_format == rpl::NODES_Q8 && !(s.qbound > 0.0)) { err = "qbound not set"; return RP_EINTERNAL; }
+  if (s.node_format != rpl::NODES_F32 && !(s.qbound > 0.0)) { err = "qbound not set"; return RP_EINTERNAL; }
+  auto frame_ok = [&](const float* o, const float* sc) {
+    for (int a = 0; a < 3; a++)
+      if (!(sc[a] >= 0x1p-60f) || !std::isfinite(o[a]) || !(std::fabs((double)o[a]) <= s.qbound) ||
+          !(255.0 * (double)sc[a] <= s.qbound))
+        return false;
+    return true;
+  };
+  // 8-wide tree: inner children at inner + rank in imask, leaf children's primitives as pmask bits of the run
+  std::function<bool(uint32_t, uint32_t, Box&)> walk8 = [&](uint32_t node, uint32_t depth, Box& out) -> bool {
+    out.reset();
+    if (node >= s.wnodes.size()) { err = "node index out of range"; return false; }
+    if (visited[node]) { err = "node visited twice"; return false; }
+    visited[node] = 1;
+    if (depth > s.max_depth) { err = "depth exceeds max_depth"; return false; }
+    const rpl::Node8Q& n = s.wnodes[node];
+    if (!frame_ok(n.o, n.s)) { err = "node frame outside qbound"; return false; }
+    const uint32_t imask = n.inner >> 24;
+    const uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
+    const uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
+    uint32_t seen = 0;
+    for (int c = 0; c < 8; c++) {
+      const bool inner = imask >> c & 1u;
+      if (inner && n.pmask[c]) { err = "slot both inner and leaf"; return false; }
+      if (n.pmask[c] & seen) { err = "overlapping leaf runs"; return false; }
+      seen |= n.pmask[c];
+      if (!inner && !n.pmask[c]) continue;
+      Box sub;
+      if (inner) {
+        const uint32_t ch = (n.inner & rpl::W8_INDEX) + (uint32_t)__builtin_popcount(imask & ((1u << c) - 1u));
+        if (!walk8(ch, depth + 1, sub)) return false;
+      } else {
+        sub.reset();
+        if (__builtin_popcount(n.pmask[c]) > (int)rpl::W8_MAX_LEAF) { err = "leaf too large"; return false; }
+        for (uint32_t m = n.pmask[c]; m; m &= m - 1u) {
+          const uint64_t k = (uint64_t)n.prim + (uint32_t)__builtin_ctz(m);
+          if (k >= s.prims.size() || used[k]) { err = "primitive referenced twice or out of range"; return false; }
+          used[k] = 1;
+          np++;
+          Box b;
+          prim_box(s.prims[k], b);
+          sub.grow(b);
+        }
+      }
+      for (int a = 0; a < 3; a++) {
+        if (!(sub.lo[a] <= sub.hi[a])) continue;
+        if (!(rpl::plane_q(n.o[a], n.s[a], L[a][c]) <= sub.lo[a]) || !(rpl::plane_q(n.o[a], n.s[a], H[a][c]) >= sub.hi[a])) {
+          err = "child box does not contain its subtree";
+          return false;
+        }
+      }
+      out.grow(sub);
+    }
+    return true;
+  };
   // subtree box of `entry` into `out`; false (err set) on the first violation
   std::function<bool(uint32_t, uint32_t, Box&)> walk = [&](uint32_t entry, uint32_t depth, Box& out) -> bool {
     out.reset();
@@ -904,13 +1108,7 @@ int check(const PackedScene& s, std::string& err) {
     double plo[4][3], phi[4][3];  // the stored child box planes, exact in f64
     if (s.node_format == rpl::NODES_Q8) {
       const rpl::Node4Q& n = s.qnodes[entry];
-      for (int a = 0; a < 3; a++) {
-        if (!(n.s[a] >= 0x1p-60f) || !std::isfinite(n.o[a]) || !(std::fabs((double)n.o[a]) <= s.qbound) ||
-            !(255.0 * (double)n.s[a] <= s.qbound)) {
-          err = "node frame outside qbound";
-          return false;
-        }
-      }
+      if (!frame_ok(n.o, n.s)) { err = "node frame outside qbound"; return false; }
       const uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
       const uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
       for (int c = 0; c < 4; c++)
@@ -943,7 +1141,7 @@ int check(const PackedScene& s, std::string& err) {
     return true;
   };
   Box all;
-  if (!walk(s.root, 0, all)) return RP_EINTERNAL;
+  if (!(s.node_format == rpl::NODES_W8 ? walk8(s.root, 0, all) : walk(s.root, 0, all))) return RP_EINTERNAL;
   size_t expect = s.prims.size() - s.n_always;  // the always-tested tail is outside the tree
   if (np != expect && !(np == 0 && s.prims.size() == 1)) {
     err = "primitive count mismatch";

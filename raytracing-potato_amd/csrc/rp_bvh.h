@@ -27,7 +27,7 @@ struct BuildOptions {
   // ground sphere, r = 1000 under a bunny of size ~0.2).  always_max = 0 disables.
   uint32_t always_max = 4;
   double always_ratio = 4.0;
-  uint32_t node_format = rpl::NODES_F32;  // rpl::NODES_F32 (Node4), rpl::NODES_Q8 (Node4Q) or 0 (auto_node_format)
+  uint32_t node_format = rpl::NODES_F32;  // rpl::NODES_F32 (Node4), _Q8 (Node4Q), _W8 (Node8Q) or 0 (auto_node_format)
   uint32_t threads = 0;                   // host build threads (0 = the machine's, at most 16); same tree for any
 };
 
@@ -35,6 +35,7 @@ struct PackedScene {
   uint32_t node_format = rpl::NODES_F32;  // resolved (never 0 after a tree build)
   std::vector<rpl::Node4> nodes;      // NODES_F32: nodes[root] is the root (always an inner record)
   std::vector<rpl::Node4Q> qnodes;    // NODES_Q8: the same tree in the quantized format
+  std::vector<rpl::Node8Q> wnodes;    // NODES_W8: the 8-wide quantized tree (its own leaf order)
   std::vector<rpl::Prim> prims;       // leaf order
   std::vector<rpl::PrimRef> prim_refs;  // leaf order: vertex ids, source hittable
   std::vector<double> vnrm;           // 3 per global vertex (mesh vertices concatenated)
@@ -47,8 +48,10 @@ struct PackedScene {
   uint32_t max_depth = 0;             // deepest wide node (root = 0)
   uint32_t always_first = 0, n_always = 0;  // prims[always_first, +n_always): outside the tree, tested first
   uint64_t n_leaves = 0;
-  double qbound = 0.0;  // rp_layout.h qbound: >= |o| and 255 s of every node frame (NODES_Q8)
-  size_t n_nodes() const { return node_format == rpl::NODES_Q8 ? qnodes.size() : nodes.size(); }
+  double qbound = 0.0;  // rp_layout.h qbound: >= |o| and 255 s of every node frame (NODES_Q8, NODES_W8)
+  size_t n_nodes() const {
+    return node_format == rpl::NODES_W8 ? wnodes.size() : node_format == rpl::NODES_Q8 ? qnodes.size() : nodes.size();
+  }
 };
 
 // The node format of RP_NODES_AUTO for the host SAH tree: the 64 B quantized node once the 128 B tree

@@ -384,9 +384,17 @@ struct Ray32 {
   float fbx, fby, fbz;  // far-plane addends fl_up(-oinv + D) per axis
   float tmin;           // t_min rounded down
   uint32_t sx, sy, sz;  // per axis, by the sign of the slope: Node4 = byte offset of the near plane row
-                        // (lo_* or hi_*; the far row is the other); Node4Q = v_perm_b32 selector picking the
-                        // near plane codes out of the {hi, lo} word pair (the far codes out of {lo, hi})
+                        // (lo_* or hi_*; the far row is the other); Node4Q/Node8Q = v_perm_b32 selector picking
+                        // the near plane codes out of the {hi, lo} word pair (the far codes out of {lo, hi})
+  uint32_t oct;         // Node8Q: dir_octant(d), the children's rank order slot ^ oct
 };
+
+// Octant of a direction: bit a set when d_a has its sign bit set (the sign of rcp(fl(d_a)) below).  Node8Q
+// visits a node's children in rank order slot ^ octant (rp_layout.h); only the order depends on it.
+RPK_INLINE uint32_t dir_octant(V3 d) {
+  return (uint32_t)(__double_as_longlong(d.x) < 0) | (uint32_t)(__double_as_longlong(d.y) < 0) << 1 |
+         (uint32_t)(__double_as_longlong(d.z) < 0) << 2;
+}
 
 // next representable float towards +inf / -inf (finite inputs; the callers only step values that
 // rounded the wrong way, which are finite)
@@ -419,7 +427,7 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
   const double ex = fabs(o.x - (double)ox), ey = fabs(o.y - (double)oy), ez = fabs(o.z - (double)oz);
   const double k = 1.0 + 0x1p-20, u = 0x1p-23, q2 = 2.0 * qbound;
   const auto fr = [&](float inv, float o32) {  // the Node4Q frame term e (see above)
-    return (NF != rpl::NODES_Q8 || (fabsf(inv) == 0x1p64f && o32 == 0.0f))
+    return (NF == rpl::NODES_F32 || (fabsf(inv) == 0x1p64f && o32 == 0.0f))
                ? 0.0
                : fabs((double)inv) * (q2 + fabs((double)o32)) * u * k;
   };
@@ -433,7 +441,8 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
   r.fby = f32_up(-(double)oiy + Dy);
   r.fbz = f32_up(-(double)oiz + Dz);
   r.tmin = f32_down(tmin);
-  if (NF == rpl::NODES_Q8) {
+  r.oct = dir_octant(d);
+  if (NF != rpl::NODES_F32) {
     r.sx = r.ix < 0.0f ? 0x07060504u : 0x03020100u;
     r.sy = r.iy < 0.0f ? 0x07060504u : 0x03020100u;
     r.sz = r.iz < 0.0f ? 0x07060504u : 0x03020100u;
@@ -456,16 +465,24 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
 // The traversal state is explicit (TravState) so a lane can stop between steps and resume later: the
 // render kernel steps traversal until few lanes are still traversing, shades the finished ones and
 // gives them new rays, then resumes (see render_kernel).
+//
+// Node8Q trees (trav_step_w8) keep groups instead of entries: cur/gy = a node group {W8_GROUP | family index,
+// rank bits 0-7 | imask << 8} (the children still to visit, in rank order) or a primitive group {first primitive,
+// primitive bits}; leaf/py = the parked primitive group (py = 0: none, and then leaf = 0).
 struct TravState {
   double best, bu, bv;
   int32_t bestp;
   uint32_t cur, sp;
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
+  uint32_t gy, py;  // Node8Q only (0 otherwise)
 };
+static constexpr uint32_t W8_GROUP = 0x80000000u;  // cur: a node group (prim groups: first primitive < 2^31)
 
-RPK_INLINE bool trav_done(const TravState& t) { return t.cur == rpl::ENTRY_EMPTY && t.leaf == 0u; }
+RPK_INLINE bool trav_done(const TravState& t) { return t.cur == rpl::ENTRY_EMPTY && (t.leaf | t.py) == 0u; }
 
-RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
+// A new ray from the root; `d` orders a Node8Q root's children.
+template <uint32_t NF>
+RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t, V3 d) {
   t.best = tmax;
   t.bu = 0.0;
   t.bv = 0.0;
@@ -473,6 +490,12 @@ RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t) {
   t.cur = S.root;
   t.sp = 0;
   t.leaf = 0;
+  t.gy = 0;
+  t.py = 0;
+  if constexpr (NF == rpl::NODES_W8) {
+    t.cur = W8_GROUP | S.root;              // the root as a group of one: slot 0, rank 0 ^ oct
+    t.gy = (1u << dir_octant(d)) | 0x100u;  // imask = slot 0
+  }
 }
 
 // One exact f64 primitive test (the reference's Hittable::hit for a leaf, hittable.rs:39-101): on
@@ -531,8 +554,9 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
 // primitive for every starting lane, instead of a divergent leaf test deep in the prim loop; their hit
 // also bounds the traversal from the root.  The closest hit is the tree's (any test order, up to exact-t
 // ties).
+template <uint32_t NF>
 RPK_INLINE void trav_begin(const KScene& S, V3 o, V3 d, double tmin, double tmax, TravState& t) {
-  trav_init(S, tmax, t);
+  trav_init<NF>(S, tmax, t, d);
   double best = t.best;
   for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++) prim_test(S, k, o, d, tmin, best, t);
   t.best = best;
@@ -562,10 +586,150 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).  `work` (COUNT instantiations: the
 // cost probe) accumulates the lane's traversal work in WORK_* units.
 enum : uint32_t { WORK_VISIT = 2, WORK_TEST = 3, WORK_RAY = 16 };  // node visit : primitive test : shaded ray
+
+// Node8Q step.  The lane descends while it holds a node group with children left: it takes the lowest rank
+// (the nearest octant), pushes the rest of the group, and visits that child, whose hit inner children become
+// the new node group and whose hit leaf children's primitives one primitive group -- parked if the lane has
+// none parked (speculative traversal, as in the 4-wide step), else pushed.  Groups go on the stack as two
+// words.  `w8_settle` pops until the lane holds a node group with work, a primitive group it cannot park yet
+// (it waits for the leaf loop), or nothing.  The leaf loop tests one primitive per lane per iteration from the
+// parked group (lowest bit first), then takes a waiting primitive group.  Same exits as trav_step.
+template <bool SPILL>
+RPK_INLINE void w8_settle(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t& gx, uint32_t& gy,
+                          uint32_t& px, uint32_t& py, uint32_t& sp) {
+#pragma unroll
+  for (int it = 0; it < 2; it++) {  // at most a primitive group and then anything: two pops
+    if (gx & W8_GROUP) {
+      if (gy & 0xFFu) return;
+    } else {
+      if (py) return;
+      px = gx; py = gy;
+    }
+    if (sp == 0u) { gx = rpl::ENTRY_EMPTY; gy = 0u; return; }
+    sp -= 2u;
+    gx = stk_get<SPILL>(S, stk, stride, spl, sp);
+    gy = stk_get<SPILL>(S, stk, stride, spl, sp + 1u);
+  }
+}
+
+template <bool SPILL, bool COUNT>
+RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o,
+                             V3 d, double tmin, TravState& ts, bool& overflow, TravDiag* td, uint32_t* work) {
+  uint32_t gx = ts.cur, gy = ts.gy, px = ts.leaf, py = ts.py, sp = ts.sp;
+  double best = ts.best;
+  float best32 = f32_up(best);
+  const uint32_t cap = S.stack_depth - STACK_SLACK;  // words
+  auto push = [&](uint32_t x, uint32_t y) {
+    if (sp + 2u > cap) { overflow = true; return; }  // cannot happen for a stack sized from the tree depth
+    stk_put<SPILL>(S, stk, stride, spl, sp, x);
+    stk_put<SPILL>(S, stk, stride, spl, sp + 1u, y);
+    sp += 2u;
+  };
+  w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);
+  // ---- inner nodes
+  while ((gx & W8_GROUP) && (gy & 0xFFu)) {
+    DIAG(if (td) td->visits++;)
+    if constexpr (COUNT) *work += WORK_VISIT;
+    DREG(DREG_NODE)
+    const uint32_t slot = (uint32_t)__builtin_ctz(gy) ^ r.oct;
+    gy &= gy - 1u;
+    const uint32_t node = (gx & ~W8_GROUP) + (uint32_t)__builtin_popcount((gy >> 8) & ((1u << slot) - 1u));
+    if (gy & 0xFFu) push(gx, gy);
+    const char* nb = reinterpret_cast<const char*>(S.nodes);
+    const uint32_t no = node << 7;
+    const float4 c0 = *reinterpret_cast<const float4*>(nb + no);        // o.x o.y o.z s.x
+    const uint4 c1 = *reinterpret_cast<const uint4*>(nb + (no + 16u));  // s.y s.z inner prim
+    const uint4 cx = *reinterpret_cast<const uint4*>(nb + (no + 32u));  // lo_x[0-3] lo_x[4-7] hi_x[0-3] hi_x[4-7]
+    const uint4 cy = *reinterpret_cast<const uint4*>(nb + (no + 48u));
+    const uint4 cz = *reinterpret_cast<const uint4*>(nb + (no + 64u));
+    const uint4 pa = *reinterpret_cast<const uint4*>(nb + (no + 80u));  // pmask[0-3]
+    const uint4 pb = *reinterpret_cast<const uint4*>(nb + (no + 96u));  // pmask[4-7]
+    const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
+    const float Bnx = fmaf(c0.x, r.ix, r.nbx), Bny = fmaf(c0.y, r.iy, r.nby), Bnz = fmaf(c0.z, r.iz, r.nbz);
+    const float Bfx = fmaf(c0.x, r.ix, r.fbx), Bfy = fmaf(c0.y, r.iy, r.fby), Bfz = fmaf(c0.z, r.iz, r.fbz);
+    const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az};
+    const f2 bnx = {Bnx, Bnx}, bny = {Bny, Bny}, bnz = {Bnz, Bnz}, bfx = {Bfx, Bfx}, bfy = {Bfy, Bfy}, bfz = {Bfz, Bfz};
+    uint32_t hits = 0u, pm = 0u;
+#define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
+#pragma unroll
+    for (int half = 0; half < 2; half++) {  // children 4 half .. 4 half + 3
+      const uint32_t lx = half ? cx.y : cx.x, hx = half ? cx.w : cx.z;
+      const uint32_t ly = half ? cy.y : cy.x, hy = half ? cy.w : cy.z;
+      const uint32_t lz = half ? cz.y : cz.x, hz = half ? cz.w : cz.z;
+      const uint32_t qnx = __builtin_amdgcn_perm(hx, lx, r.sx), qfx = __builtin_amdgcn_perm(lx, hx, r.sx);
+      const uint32_t qny = __builtin_amdgcn_perm(hy, ly, r.sy), qfy = __builtin_amdgcn_perm(ly, hy, r.sy);
+      const uint32_t qnz = __builtin_amdgcn_perm(hz, lz, r.sz), qfz = __builtin_amdgcn_perm(lz, hz, r.sz);
+      const uint4 pq = half ? pb : pa;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const f2 NX = pk_fma(RPK_Q2(qnx, q), ax, bnx), FX = pk_fma(RPK_Q2(qfx, q), ax, bfx);
+        const f2 NY = pk_fma(RPK_Q2(qny, q), ay, bny), FY = pk_fma(RPK_Q2(qfy, q), ay, bfy);
+        const f2 NZ = pk_fma(RPK_Q2(qnz, q), az, bnz), FZ = pk_fma(RPK_Q2(qfz, q), az, bfz);
+        f2 TN, TF;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          TN[e] = fmaxf(fmaxf(NX[e], NY[e]), fmaxf(NZ[e], r.tmin));
+          TF[e] = fminf(fminf(FX[e], FY[e]), fminf(FZ[e], best32));
+        }
+        const f2 lhs = pk_fma(TN, f2{1.0f - 0x1p-19f, 1.0f - 0x1p-19f}, f2{-0x1p-100f, -0x1p-100f});
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int c = 4 * half + 2 * q + e;
+          const bool hit = lhs[e] <= TF[e];
+          hits |= hit ? 1u << c : 0u;
+          const uint32_t m = (2 * q + e) == 0 ? pq.x : (2 * q + e) == 1 ? pq.y : (2 * q + e) == 2 ? pq.z : pq.w;
+          pm |= hit ? m : 0u;
+        }
+      }
+    }
+#undef RPK_Q2
+    // hit inner children in rank order: bit (slot ^ oct)
+    const uint32_t imask = c1.z >> 24;
+    uint32_t ih = hits & imask;
+    if (r.oct & 1u) ih = ((ih & 0x55u) << 1) | ((ih >> 1) & 0x55u);
+    if (r.oct & 2u) ih = ((ih & 0x33u) << 2) | ((ih >> 2) & 0x33u);
+    if (r.oct & 4u) ih = ((ih & 0x0Fu) << 4) | ((ih >> 4) & 0x0Fu);
+    if (pm) {
+      if (py == 0u) { px = c1.w; py = pm; }
+      else push(c1.w, pm);
+    }
+    gx = W8_GROUP | (c1.z & rpl::W8_INDEX);
+    gy = ih | imask << 8;
+    w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);
+#ifndef RPK_NO_SPECULATIVE
+    if ((uint32_t)__popcll(__ballot(py == 0u)) <= S.leaf_break) break;
+#endif
+  }
+  // ---- leaves: one primitive per lane per iteration from the parked group, then a waiting one
+  while (py != 0u) {
+    DIAG(if (td) td->tests++;)
+    if constexpr (COUNT) *work += WORK_TEST;
+    DREG(DREG_PRIM)
+    const uint32_t k = px + (uint32_t)__builtin_ctz(py);
+    py &= py - 1u;
+    prim_test(S, k, o, d, tmin, best, ts);
+    if (py == 0u) {
+      px = 0u;
+      if (!(gx & W8_GROUP)) w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);  // park the waiting group
+    }
+    if (RPK_PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(py != 0u)) <= RPK_PRIM_BREAK) break;
+  }
+  ts.cur = gx;
+  ts.gy = gy;
+  ts.sp = sp;
+  ts.best = best;
+  ts.leaf = px;
+  ts.py = py;
+}
+
 template <bool SPILL, uint32_t NF, bool COUNT = false>
 RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr,
                           uint32_t* work = nullptr) {
+  if constexpr (NF == rpl::NODES_W8) {
+    trav_step_w8<SPILL, COUNT>(S, stk, stride, spl, r, o, d, tmin, ts, overflow, td, work);
+    return;
+  }
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
   double best = ts.best;
   float best32 = f32_up(best);
@@ -744,7 +908,7 @@ RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V
   Ray32 r;
   setup_ray32<NF>(o, d, tmin, S.qbound, r);
   TravState t;
-  trav_begin(S, o, d, tmin, tmax, t);
+  trav_begin<NF>(S, o, d, tmin, tmax, t);
   while (!trav_done(t)) trav_step<false, NF>(S, stk, stride, 0u, r, o, d, tmin, t, overflow, td);
   hr.t = t.best;
   hr.u = t.bu;

@@ -427,7 +427,8 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   bo.node_format = node_format;
   rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(err);
-  const bool q8 = ps.node_format == rpl::NODES_Q8;
+  const bool q8 = ps.node_format != rpl::NODES_F32;  // Node4Q or Node8Q: the frame term
+  const bool w8 = ps.node_format == rpl::NODES_W8;
   auto down = [](double x) { float f = (float)x; if ((double)f > x) f = std::nextafter(f, -INFINITY); return f; };
   auto up = [](double x) { float f = (float)x; if ((double)f < x) f = std::nextafter(f, INFINITY); return f; };
   for (uint64_t r = 0; r < n; r++) {
@@ -494,6 +495,56 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
     };
     // the always-tested primitives first (rp_bvh.h BuildOptions::always_max), as the kernel does
     for (uint32_t k = ps.always_first; k < ps.always_first + ps.n_always; k++) test(k);
+    if (w8) {
+      // 8-wide: children in rank order slot ^ octant; a stack of groups {family index | imask, rank bits}; the
+      // leaf children's primitives are tested when their node is visited (the kernel parks them, same hits)
+      const uint32_t oct = (d[0] < 0.0 ? 1u : 0u) | (d[1] < 0.0 ? 2u : 0u) | (d[2] < 0.0 ? 4u : 0u);
+      std::vector<std::pair<uint32_t, uint32_t>> groups;  // {inner word, remaining rank bits}
+      auto visit = [&](uint32_t node) {
+        visits++;
+        const rpl::Node8Q& nd = ps.wnodes[node];
+        float A[3], Bn[3], Bf[3];
+        for (int k = 0; k < 3; k++) {
+          A[k] = nd.s[k] * inv[k];
+          Bn[k] = std::fma(nd.o[k], inv[k], nb[k]);
+          Bf[k] = std::fma(nd.o[k], inv[k], fb[k]);
+        }
+        const uint8_t* L[3] = {nd.lo_x, nd.lo_y, nd.lo_z};
+        const uint8_t* H[3] = {nd.hi_x, nd.hi_y, nd.hi_z};
+        uint32_t hits = 0;
+        for (int c = 0; c < 8; c++) {
+          float tnear = tmin32, tfar = best32;
+          for (int k = 0; k < 3; k++) {
+            const float a = std::fma((float)L[k][c], A[k], Bn[k]), b = std::fma((float)H[k][c], A[k], Bn[k]);
+            const float a2 = std::fma((float)L[k][c], A[k], Bf[k]), b2 = std::fma((float)H[k][c], A[k], Bf[k]);
+            tnear = std::fmax(tnear, std::fmin(a, b));
+            tfar = std::fmin(tfar, std::fmax(a2, b2));
+          }
+          if (std::fma(tnear, 1.0f - 0x1p-19f, -0x1p-100f) <= tfar) hits |= 1u << c;
+        }
+        uint32_t pm = 0;
+        for (int c = 0; c < 8; c++)
+          if (hits >> c & 1u) pm |= nd.pmask[c];
+        for (; pm; pm &= pm - 1u) test(nd.prim + (uint32_t)__builtin_ctz(pm));
+        const uint32_t ih = hits & (nd.inner >> 24);
+        uint32_t ranks = 0;
+        for (int c = 0; c < 8; c++)
+          if (ih >> c & 1u) ranks |= 1u << (c ^ oct);
+        if (ranks) groups.push_back({nd.inner, ranks});
+      };
+      visit(ps.root);
+      while (!groups.empty()) {
+        auto& g = groups.back();
+        const uint32_t rk = (uint32_t)__builtin_ctz(g.second), slot = rk ^ oct, word = g.first;
+        g.second &= g.second - 1u;
+        if (!g.second) groups.pop_back();
+        visit((word & rpl::W8_INDEX) + (uint32_t)__builtin_popcount((word >> 24) & ((1u << slot) - 1u)));
+      }
+      per_ray[3 * r] = visits;
+      per_ray[3 * r + 1] = tests;
+      per_ray[3 * r + 2] = bestp < 0 ? ~0ull : (uint64_t)bestp;
+      continue;
+    }
     std::vector<uint32_t> stack;
     uint32_t cur = ps.root;
     for (;;) {
@@ -605,7 +656,8 @@ int rph_bvh_tree_hash(const rp_scene_desc* desc, uint32_t node_format, uint32_t 
     const uint8_t* b = static_cast<const uint8_t*>(p);
     for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 0x100000001b3ull;
   };
-  if (ps.node_format == rpl::NODES_Q8) mix(ps.qnodes.data(), ps.qnodes.size() * sizeof(rpl::Node4Q));
+  if (ps.node_format == rpl::NODES_W8) mix(ps.wnodes.data(), ps.wnodes.size() * sizeof(rpl::Node8Q));
+  else if (ps.node_format == rpl::NODES_Q8) mix(ps.qnodes.data(), ps.qnodes.size() * sizeof(rpl::Node4Q));
   else mix(ps.nodes.data(), ps.nodes.size() * sizeof(rpl::Node4));
   mix(ps.prim_refs.data(), ps.prim_refs.size() * sizeof(rpl::PrimRef));
   *hash = h;

@@ -113,6 +113,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   ts.best = 0.0;
   ts.bestp = -1;
   ts.bu = ts.bv = 0.0;
+  ts.gy = ts.py = 0u;
   uint32_t pi = 0, pj = 0;
   bool alive = fetch_pixel<PROBE>(slot, pi, pj, batch);
   pipj = pi | (pj << 16);
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       depth = A->P.max_bounce;
       T_x = T_y = T_z = 1.0;
       first = true;
-      trav_init(load_scene(A), INF, ts);
+      trav_init<NF>(load_scene(A), INF, ts, d);
       tdone = false;
       newray = true;
       start = fresh = false;
@@ -271,7 +272,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         }
         start = alive;  // next round, after the refill pass
       } else {
-        trav_init(load_scene(kargs()), INF, ts);
+        trav_init<NF>(load_scene(kargs()), INF, ts, d);
         tdone = false;
         newray = true;
       }
@@ -361,7 +362,9 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
   const hipStream_t st = (hipStream_t)stream;
 #define RPK_LAUNCH(P_, S_)                                                                                   \
   do {                                                                                                   \
-    if (s.node_format == rpl::NODES_Q8)                                                                  \
+    if (s.node_format == rpl::NODES_W8)                                                                  \
+      hipLaunchKernelGGL((render_kernel<P_, S_, rpl::NODES_W8>), dim3(grid), dim3(BLOCK), lds, st, a);   \
+    else if (s.node_format == rpl::NODES_Q8)                                                             \
       hipLaunchKernelGGL((render_kernel<P_, S_, rpl::NODES_Q8>), dim3(grid), dim3(BLOCK), lds, st, a);   \
     else                                                                                                 \
       hipLaunchKernelGGL((render_kernel<P_, S_, rpl::NODES_F32>), dim3(grid), dim3(BLOCK), lds, st, a);  \
@@ -544,6 +547,10 @@ uint64_t rng_slab_bytes_per_lane() { return (uint64_t)SLAB_N * sizeof(uint4); }
 
 int render_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t nf, int* blocks) {
   const size_t lds = (size_t)lds_depth * BLOCK * sizeof(uint32_t);
+  if (nf == rpl::NODES_W8) {
+    if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true, rpl::NODES_W8>, BLOCK, lds);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false, rpl::NODES_W8>, BLOCK, lds);
+  }
   if (nf == rpl::NODES_Q8) {
     if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, true, rpl::NODES_Q8>, BLOCK, lds);
     return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, render_kernel<false, false, rpl::NODES_Q8>, BLOCK, lds);
@@ -557,7 +564,10 @@ int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* ou
   if (n == 0) return 0;
   const size_t lds = (size_t)s.stack_depth * BLOCK * sizeof(uint32_t);
   const uint64_t grid = (n + BLOCK - 1) / BLOCK;
-  if (s.node_format == rpl::NODES_Q8)
+  if (s.node_format == rpl::NODES_W8)
+    hipLaunchKernelGGL(intersect_kernel<rpl::NODES_W8>, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s,
+                       rays, n, out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
+  else if (s.node_format == rpl::NODES_Q8)
     hipLaunchKernelGGL(intersect_kernel<rpl::NODES_Q8>, dim3((unsigned)grid), dim3(BLOCK), lds, (hipStream_t)stream, s,
                        rays, n, out_hit, out_mat, reinterpret_cast<unsigned long long*>(counters));
   else

@@ -48,7 +48,31 @@ struct alignas(16) Node4Q {
 };
 static_assert(sizeof(Node4Q) == 64, "Node4Q must be 64 B");
 
-enum : uint32_t { NODES_F32 = 1, NODES_Q8 = 2 };  // = RP_NODES_F32 / RP_NODES_Q8 (include/rp.h)
+// Node8Q (128 B, one cache line; host SAH trees): eight children quantized like Node4Q.  Slot s (0..7) holds a
+// child lying towards (s&1 ? +x : -x, s&2 ? +y : -y, s&4 ? +z : -z) of the node's centre, so a ray visits its
+// children in the order of rank = slot ^ octant (octant bit a set when the ray's slope on axis a is negative):
+// approximately near-first without sorting.  Inner children are consecutive records from `inner` in slot order
+// (child at slot s = (inner & W8_INDEX) + popcount(imask & ((1 << s) - 1)), imask = inner >> 24); the primitives
+// of the leaf children are one run from `prim`, pmask[s] the bits of slot s's leaf in that run (<= 32 bits: at
+// most 8 leaves of <= 4 primitives).  16 B chunks: {o.x, o.y, o.z, s.x} {s.y, s.z, inner, prim}
+// {lo_x, hi_x} {lo_y, hi_y} {lo_z, hi_z} {pmask[0..3]} {pmask[4..7]} {pad}: seven loads per visit.
+struct alignas(16) Node8Q {
+  float o[3];
+  float s[3];
+  uint32_t inner;
+  uint32_t prim;
+  uint8_t lo_x[8], hi_x[8];
+  uint8_t lo_y[8], hi_y[8];
+  uint8_t lo_z[8], hi_z[8];
+  uint32_t pmask[8];
+  uint32_t pad[4];
+};
+static_assert(sizeof(Node8Q) == 128, "Node8Q must be 128 B");
+constexpr uint32_t W8_INDEX = 0x00FFFFFFu;  // Node8Q.inner: family index bits (imask above)
+constexpr uint32_t W8_MAX_NODES = 1u << 24;
+constexpr uint32_t W8_MAX_LEAF = 4;
+
+enum : uint32_t { NODES_F32 = 1, NODES_Q8 = 2, NODES_W8 = 3 };  // = RP_NODES_F32 / _Q8 / _W8 (include/rp.h)
 
 #if defined(__HIPCC__)
 #define RPL_HD __host__ __device__
@@ -119,9 +143,10 @@ RPL_HD inline uint32_t q_up(double x, float o, float s) {  // smallest q with pl
 RPL_HD inline double qbound(double amax) { return 4.0 * amax + 0x1p-50; }
 constexpr double COORD_MAX = 0x1p54;
 
-// Quantize child c of node n from its exact f64 box (lo[3], hi[3]); a non-finite bound (NaN geometry: never
+// Quantize child c of node n (Node4Q or Node8Q) from its exact f64 box (lo[3], hi[3]); a non-finite bound (NaN geometry: never
 // hit) takes the whole frame.
-RPL_HD inline void quantize_child(Node4Q& n, int c, const double lo[3], const double hi[3]) {
+template <class N>
+RPL_HD inline void quantize_child(N& n, int c, const double lo[3], const double hi[3]) {
   uint8_t* L[3] = {n.lo_x, n.lo_y, n.lo_z};
   uint8_t* H[3] = {n.hi_x, n.hi_y, n.hi_z};
   for (int a = 0; a < 3; a++) {
@@ -130,7 +155,8 @@ RPL_HD inline void quantize_child(Node4Q& n, int c, const double lo[3], const do
     H[a][c] = ok ? (uint8_t)q_up(hi[a], n.o[a], n.s[a]) : (uint8_t)255;
   }
 }
-RPL_HD inline void empty_child(Node4Q& n, int c) {
+template <class N>
+RPL_HD inline void empty_child(N& n, int c) {
   n.lo_x[c] = n.lo_y[c] = n.lo_z[c] = 255;
   n.hi_x[c] = n.hi_y[c] = n.hi_z[c] = 0;
 }

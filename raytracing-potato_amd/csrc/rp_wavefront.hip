@@ -276,6 +276,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
   ts.best = 0.0;
   ts.bestp = -1;
   ts.bu = ts.bv = 0.0;
+  ts.gy = ts.py = 0u;
   for (;;) {
     const uint64_t idle = __ballot(!have);
     if (!drained && idle != 0 && ((uint32_t)__popcll(idle) >= RPK_WF_REFILL || __ballot(have) == 0)) {
@@ -286,7 +287,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
           d = v3(w.in.ray[3 * P + q], w.in.ray[4 * P + q], w.in.ray[5 * P + q]);
           const KScene S = load_scene(kargs());
           setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
-          trav_init(S, INF, ts);
+          trav_init<NF>(S, INF, ts, d);
           double best = ts.best;
           for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++)
             prim_test(S, k, o, d, RAY_EPSILON, best, ts);
@@ -358,7 +359,10 @@ int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* 
   for (uint32_t it = 1;; it++) {
     if (it > bound) return (int)hipErrorUnknown;
     set(cur);
-    if (s.node_format == rpl::NODES_Q8) {
+    if (s.node_format == rpl::NODES_W8) {
+      if (spill) hipLaunchKernelGGL((wf_trace_kernel<true, rpl::NODES_W8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+      else hipLaunchKernelGGL((wf_trace_kernel<false, rpl::NODES_W8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
+    } else if (s.node_format == rpl::NODES_Q8) {
       if (spill) hipLaunchKernelGGL((wf_trace_kernel<true, rpl::NODES_Q8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
       else hipLaunchKernelGGL((wf_trace_kernel<false, rpl::NODES_Q8>), dim3(trace_grid), dim3(BLOCK), lds, st, a, w);
     } else {
@@ -379,6 +383,10 @@ int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* 
 
 int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t nf, int* blocks) {
   const size_t lds = (size_t)lds_depth * BLOCK * sizeof(uint32_t);
+  if (nf == rpl::NODES_W8) {
+    if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<true, rpl::NODES_W8>, BLOCK, lds);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<false, rpl::NODES_W8>, BLOCK, lds);
+  }
   if (nf == rpl::NODES_Q8) {
     if (spill) return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<true, rpl::NODES_Q8>, BLOCK, lds);
     return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, wf_trace_kernel<false, rpl::NODES_Q8>, BLOCK, lds);

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 
-FORMATS = [1, 2]  # RP_NODES_F32, RP_NODES_Q8
+FORMATS = [1, 2, 3]  # RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8
 
 
 def _selfcheck(scene, node_format=0):

@@ -74,6 +74,8 @@ def test_c5_10m_triangles(gpu):
     for fmt in ("f32", "q8"):
         with gpu.DeviceScene(scene, options={"builder": "gpu", "node_format": fmt}) as ds:
             results.append(ds.intersect(rays))
+    with gpu.DeviceScene(scene, options={"node_format": "w8"}) as ds:  # the host 8-wide tree
+        results.append(ds.intersect(rays))
     assert st["pixels"] == 4096 * 4096 and np.isfinite(rgb).all()
     assert 1.0 < st["rays"] / st["samples"] < 8.0
     desc = scene.desc()
@@ -247,7 +249,8 @@ def test_frame_assemble_multi_rank_layout(gpu, world):
 @pytest.mark.parametrize("name,arg,spp,opts", [
     ("bunny_full", None, 40, {}), ("three_balls", None, 3, {}), ("variants", None, 6, {}),
     ("variants_sky", None, 5, {}), ("more_balls_optimized", None, 4, {}), ("glass_bunny", None, 4, {}),
-    ("random_mesh", 200_000, 4, {"lds_depth": 17}), ("bunny_full", None, 9, {"wf_slots": 1})])
+    ("random_mesh", 200_000, 4, {"lds_depth": 17}), ("bunny_full", None, 9, {"wf_slots": 1}),
+    ("random_mesh", 200_000, 4, {"node_format": "w8"})])
 def test_wavefront_engine_matches_megakernel(gpu, name, arg, spp, opts):
     """The stage-split engine (rp_scene_options.engine = wavefront: trace / shade passes over a path-slot pool)
     renders the megakernel's image bit for bit -- same paths, same RNG stream, same accumulation order --

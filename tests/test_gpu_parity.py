@@ -173,14 +173,19 @@ def test_render_device_torch(gpu):
     assert int(ctr[0]) == st["rays"] and int(ctr[3]) == 0
 
 
-@pytest.mark.parametrize("fmt", ["f32", "q8"])
+@pytest.mark.parametrize("fmt", ["f32", "q8", "w8"])
 @pytest.mark.parametrize("builder", ["host", "gpu"])
 def test_intersect_rays(gpu, builder, fmt):
     """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle --
     over the host SAH tree and the device-built LBVH (rp_scene_options.builder), with f32 or 8-bit quantized
-    child boxes (rp_scene_options.node_format)."""
+    child boxes, 4-wide or (host trees) 8-wide (rp_scene_options.node_format)."""
     from oracle import oracle_py as O
     from rtpotato import scenes
+    from rtpotato import _ffi as F
+    if builder == "gpu" and fmt == "w8":  # the device builder makes 4-wide trees only: refused, not substituted
+        with pytest.raises(F.RPError, match="4-wide"):
+            gpu.DeviceScene(scenes.bunny_full(), options={"builder": "gpu", "node_format": "w8"})
+        return
     rng = np.random.default_rng(5)
     scene = scenes.bunny_full()
     n = 20000
@@ -300,7 +305,7 @@ def test_device_bvh_builder(gpu, name, arg, fmt):
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
-@pytest.mark.parametrize("fmt", ["f32", "q8"])
+@pytest.mark.parametrize("fmt", ["f32", "q8", "w8"])
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
 def test_spilled_traversal_stack(gpu, name, arg, fmt):
     """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
@@ -325,14 +330,15 @@ def test_always_tested_primitives(gpu, always_max):
         _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"always_max": int(always_max)})
 
 
+@pytest.mark.parametrize("fmt", ["q8", "w8"])
 @pytest.mark.parametrize("name", ["bunny_full", "more_balls", "two_balls", "earth", "variants"])
-def test_quantized_nodes_scenes(gpu, name):
-    """The 64 B quantized node format (options.node_format = q8, the default above 2^17 hittables) on the
-    small catalogue scenes, whose default is the f32 format: same image and ray counts as the oracle."""
+def test_quantized_nodes_scenes(gpu, name, fmt):
+    """The quantized node formats (options.node_format: q8 = 64 B 4-wide, w8 = 128 B 8-wide) on the small
+    catalogue scenes, whose default is the f32 format: same image and ray counts as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
     sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
-    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"node_format": "q8"})
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"node_format": fmt})
 
 
 def test_tile_orders_bitwise(gpu):
