@@ -201,6 +201,11 @@ enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2, RP_NODES_W8 = 3 };
  * tiles run together: a small cache working set).  AUTO = COST while the scene fits the 256 MB Infinity
  * Cache, MORTON above. */
 enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON = 3 };
+/* Unit queues: SINGLE = one device-wide queue over the tile order; XCD_TILES = eight queues, one per group of
+ * render blocks sharing an XCD (and its L2), tile k of the order served by queue k mod 8 (a tile's pixels
+ * run on one XCD); XCD_REGIONS = queue g serves the g-th eighth of the tile order (a compact region per XCD
+ * under Z-order).  A drained queue's blocks take units from the others.  AUTO = XCD_TILES. */
+enum { RP_QUEUES_AUTO = 0, RP_QUEUES_SINGLE = 1, RP_QUEUES_XCD_TILES = 2, RP_QUEUES_XCD_REGIONS = 3 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles) */
@@ -219,6 +224,7 @@ typedef struct rp_scene_options {
   uint32_t leaf_break;      /* speculative traversal: a wave moves to the leaf tests once at most this many of its
                                lanes still look for a leaf (0 -> 8 for scenes within the 256 MB Infinity Cache,
                                12 above; 1..64) */
+  uint32_t unit_queues;     /* RP_QUEUES_*: how the render blocks share out the units */
 } rp_scene_options;
 
 typedef struct rp_stats {

@@ -82,6 +82,7 @@ void dfree(void* p) {
 
 // Defaults of rp_scene_options (the measured best).
 constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
+constexpr uint32_t DEF_UNIT_QUEUES = RP_QUEUES_XCD_TILES;
 constexpr double DEF_COST_TRAVERSE = 0.7;
 
 }  // namespace
@@ -92,7 +93,7 @@ struct rp_workspace {
   rp_scene* scene = nullptr;
   uint64_t* d_ctr = nullptr;         // counters when the caller passes none (CTR_N x u64)
   uint64_t* d_probe_ctr = nullptr;   // counters of the probe launch
-  uint32_t* d_queue = nullptr;       // unit queues: [0] the frame, [1] the probe
+  uint32_t* d_queue = nullptr;       // unit queues, one 128 B line each: the frame's groups, then the probe
   uint32_t* d_tile_cost = nullptr;   // cost probe output, 2 x rpk::TILE_SORT_MAX entries
   uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
   uint32_t* d_slab = nullptr;        // keystream cache, one slab per resident render lane
@@ -170,7 +171,7 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
   *w = rp_workspace{};
   w->scene = s;
   const uint64_t lanes = s->lanes();
-  if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, 2) ||
+  if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, rpk::QUEUE_WORDS) ||
       !dalloc(&w->d_tile_cost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_tile_order, rpk::TILE_SORT_MAX) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
@@ -289,6 +290,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.wf_slots > 64) return fail(RP_EINVAL, "options.wf_slots must be 1..64");
   if (o.node_format > RP_NODES_W8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
   if (o.leaf_break > 64) return fail(RP_EINVAL, "options.leaf_break must be 0..64");
+  if (o.unit_queues > RP_QUEUES_XCD_REGIONS) return fail(RP_EINVAL, "options.unit_queues must be RP_QUEUES_*");
   return RP_OK;
 }
 
@@ -532,8 +534,16 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.spp_batch = t.sps;  // the RNG contract's samples per stream (rp_render_params.samples_per_stream)
   kp.nbatch = t.nbatch;
   kp.n_queue = t.n_slots * kp.nbatch;
-  // the 32-bit queue word also takes one failed fetch per resident lane after the last unit
-  if (kp.n_queue + s->lanes() >= 0xffffffffull)
+  // Per-XCD queues (rp.h RP_QUEUES_*): groups of blocks blockIdx mod 8 share an XCD (MI355X_MICROARCH.md,
+  // observed round-robin dispatch; speed only -- any placement gives the same image).  The stage-split engine
+  // keeps the single queue.
+  uint32_t qmode = s->opt.unit_queues == RP_QUEUES_AUTO ? (uint32_t)DEF_UNIT_QUEUES : s->opt.unit_queues;
+  if (s->opt.engine == RP_ENGINE_WAVEFRONT) qmode = RP_QUEUES_SINGLE;
+  kp.queue_groups = qmode == RP_QUEUES_SINGLE ? 1u : (uint32_t)rpk::QUEUE_GROUPS;
+  kp.queue_regions = qmode == RP_QUEUES_XCD_REGIONS ? 1u : 0u;
+  // a 32-bit queue word takes its units, plus one failed fetch per resident lane after the last unit (single
+  // queue) or one per fetch that passes a drained queue on the way to another (per-XCD queues)
+  if ((kp.queue_groups > 1 ? 2 * kp.n_queue : kp.n_queue) + s->lanes() >= 0xffffffffull)
     return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units with the resident lanes)");
   if (kp.nbatch > 1) {
     if (kp.n_queue > w->partial_units)
@@ -549,7 +559,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
     return (int)std::max<uint64_t>(1, std::min(want, resident));
   };
-  RP_HIP(hipMemsetAsync(w->d_queue, 0, sizeof(uint32_t) * 2, st));
+  RP_HIP(hipMemsetAsync(w->d_queue, 0, sizeof(uint32_t) * rpk::QUEUE_WORDS, st));
   const rpk::TileGeom tg{t.tiles_x, kp.shard, kp.nshards};
   const uint32_t tiles_y = t.tiles_y;
   uint32_t order_mode = s->opt.tile_order;
@@ -575,10 +585,11 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     pk.nbatch = 1;
     pk.spp_batch = 1;
     pk.n_queue = pk.n_slots;
+    pk.queue_groups = 1;
     pk.tile_cost = w->d_tile_cost;
     RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
     RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
-    int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + 1, grid_for(pk.n_slots), stream);
+    int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + rpk::QUEUE_PROBE, grid_for(pk.n_slots), stream);
     if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
     e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, tg, w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));

@@ -69,6 +69,8 @@ struct KParams {
   uint32_t nbatch;          // sample batches (RNG streams) per pixel: ceil(spp / spp_batch); 1 in a probe
   uint32_t spp_batch;       // samples per batch: SPP_BATCH (the contract); other values for timing studies only
   uint64_t n_queue;         // queue entries: n_slots * nbatch units (render), probed pixels (probe)
+  uint32_t queue_groups;    // render: unit queues (1, or QUEUE_GROUPS: one per group blockIdx mod 8 = one XCD)
+  uint32_t queue_regions;   // render, groups > 1: queue g serves the g-th run of the tile order (else tile k mod G)
   double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
   uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
@@ -94,6 +96,10 @@ enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
 // 0.8% faster on one GPU but left an 8-GPU shard with a 30% latency-bound tail (projection, 70% vs 84%
 // efficiency).
 enum { SPP_BATCH = 32 };
+
+// Unit-queue words of a workspace: group g's counter at g * QUEUE_STRIDE (own 128 B line), the probe's at
+// QUEUE_PROBE.
+enum { QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_STRIDE, QUEUE_WORDS = QUEUE_PROBE + 1 };
 
 // Counter block layout (RP_COUNTERS_LEN x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_N = 4 };

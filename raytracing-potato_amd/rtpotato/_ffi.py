@@ -30,6 +30,7 @@ RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
 RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
 RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON = 0, 1, 2, 3
+RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 
 
 class rp_hittable(Structure):
@@ -87,7 +88,8 @@ class rp_scene_options(Structure):
     _fields_ = [("builder", c_uint32), ("max_leaf", c_uint32), ("cost_traverse", c_double),
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
-                ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32)]
+                ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
+                ("unit_queues", c_uint32)]
 
 
 class rp_stats(Structure):
