@@ -291,6 +291,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.node_format > RP_NODES_W8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
   if (o.leaf_break > 64) return fail(RP_EINVAL, "options.leaf_break must be 0..64");
   if (o.unit_queues > RP_QUEUES_XCD_REGIONS) return fail(RP_EINVAL, "options.unit_queues must be RP_QUEUES_*");
+  if (o.queue_chunk > 4096) return fail(RP_EINVAL, "options.queue_chunk must be 0..4096");
   return RP_OK;
 }
 
@@ -540,7 +541,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   uint32_t qmode = s->opt.unit_queues == RP_QUEUES_AUTO ? (uint32_t)DEF_UNIT_QUEUES : s->opt.unit_queues;
   if (s->opt.engine == RP_ENGINE_WAVEFRONT) qmode = RP_QUEUES_SINGLE;
   kp.queue_groups = qmode == RP_QUEUES_SINGLE ? 1u : (uint32_t)rpk::QUEUE_GROUPS;
-  kp.queue_regions = qmode == RP_QUEUES_XCD_REGIONS ? 1u : 0u;
+  kp.queue_chunk = qmode == RP_QUEUES_XCD_REGIONS ? (t.n_shard_tiles + kp.queue_groups - 1) / kp.queue_groups
+                  : kp.queue_groups > 1 && s->opt.queue_chunk ? s->opt.queue_chunk : 1u;
+  if (kp.queue_chunk == 0) kp.queue_chunk = 1;
   // a 32-bit queue word takes its units, plus one failed fetch per resident lane after the last unit (single
   // queue) or one per fetch that passes a drained queue on the way to another (per-XCD queues)
   if ((kp.queue_groups > 1 ? 2 * kp.n_queue : kp.n_queue) + s->lanes() >= 0xffffffffull)
@@ -586,6 +589,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     pk.spp_batch = 1;
     pk.n_queue = pk.n_slots;
     pk.queue_groups = 1;
+    pk.queue_chunk = 1;
     pk.tile_cost = w->d_tile_cost;
     RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
     RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));

@@ -1298,9 +1298,9 @@ RPK_INLINE KArgsPtr kargs() {
   return p;
 }
 
-// Pull the next unit (pixel, sample batch) of the shard from the device-wide queue.  Queue order: shard
-// tiles (in cost order when tile_order is set), inside a tile batch-major, then the tile's pixels
-// row-major; slots of edge tiles outside the frame are skipped.  Returns false when the queue is drained.
+// Pull the next unit (pixel, sample batch) of the shard from the unit queues.  Queue order: shard tiles
+// (in cost or Z-order when tile_order is set), inside a tile the pixels row-major, each pixel's batches
+// consecutive; slots of edge tiles outside the frame are skipped.  Returns false when every queue is drained.
 template <bool PROBE>
 RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t& batch) {
   KArgsPtr A = kargs();
@@ -1331,12 +1331,10 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     uint32_t g = home + tries;
     if (g >= G) g -= G;
     g = __builtin_amdgcn_readfirstlane(g);
-    uint32_t klo = g, kstep = G, nk = (K + G - 1 - g) / G;  // tiles k = g + G * i
-    if (A->P.queue_regions) {
-      klo = (uint32_t)((uint64_t)g * K / G);
-      kstep = 1;
-      nk = (uint32_t)((uint64_t)(g + 1) * K / G) - klo;
-    }
+    // queue g serves the chunks g, g + G, ... of C consecutive tiles of the order: tile k of its i-th unit
+    // run is (i / C) * G * C + g * C + i % C
+    const uint32_t C = A->P.queue_chunk, GC = G * C;
+    const uint32_t rest = K % GC, nk = (K / GC) * C + min(rest - min(rest, g * C), C);
     const uint32_t q = atomicAdd(queue + g * QUEUE_STRIDE, 1u);
     const bool drained = (uint64_t)q >= (uint64_t)nk * tile_units;
     if (__ballot(drained) != 0) {
@@ -1348,9 +1346,12 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     }
     const uint32_t i = q / tile_units;
     const uint32_t rem = q - i * tile_units;
-    uint32_t k = klo + i * kstep;
-    batch = rem / tile_px;
-    const uint32_t local = rem - batch * tile_px;
+    uint32_t k = (i / C) * GC + g * C + i % C;
+    // a tile's units pixel-major, a pixel's batches consecutive: a wave fetches 64 / nbatch pixels with all
+    // their batches, whose camera rays traverse nearly the same nodes (C3 -0.9 %, C5 -0.9 % against
+    // batch-major, ab32)
+    const uint32_t local = rem / A->P.nbatch;
+    batch = rem - local * A->P.nbatch;
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
     slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
     const uint32_t t = A->P.shard + k * A->P.nshards;

@@ -70,7 +70,7 @@ struct KParams {
   uint32_t spp_batch;       // samples per batch: SPP_BATCH (the contract); other values for timing studies only
   uint64_t n_queue;         // queue entries: n_slots * nbatch units (render), probed pixels (probe)
   uint32_t queue_groups;    // render: unit queues (1, or QUEUE_GROUPS: one per group blockIdx mod 8 = one XCD)
-  uint32_t queue_regions;   // render, groups > 1: queue g serves the g-th run of the tile order (else tile k mod G)
+  uint32_t queue_chunk;     // render: queue g serves the chunks g, g + G, ... of queue_chunk consecutive tiles (>= 1)
   double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
   uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)

@@ -89,7 +89,7 @@ class rp_scene_options(Structure):
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
                 ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
-                ("unit_queues", c_uint32)]
+                ("unit_queues", c_uint32), ("queue_chunk", c_uint32)]
 
 
 class rp_stats(Structure):

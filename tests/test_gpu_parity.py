@@ -357,10 +357,12 @@ def test_tile_orders_bitwise(gpu):
             assert np.array_equal(rgb, frames[0][0]) and rays == frames[0][1]
 
 
-@pytest.mark.parametrize("queues", ["single", "xcd_tiles", "xcd_regions"])
+@pytest.mark.parametrize("queues", [{"unit_queues": "single"}, {"unit_queues": "xcd_tiles"},
+                                    {"unit_queues": "xcd_regions"}, {"unit_queues": "xcd_tiles", "queue_chunk": 3}])
 def test_unit_queues_bitwise(gpu, queues):
-    """options.unit_queues (one device-wide unit queue, or one per XCD group of blocks serving every 8th tile
-    or an eighth of the tile order, stealing once drained) changes the schedule only: identical frames --
+    """options.unit_queues / queue_chunk (one device-wide unit queue, or one per XCD group of blocks serving
+    every 8th tile, every 8th chunk of tiles or an eighth of the tile order, stealing once drained) changes the
+    schedule only: identical frames --
     including frames with fewer tiles than queues, edge tiles outside the frame and multi-batch pixels."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
@@ -368,9 +370,9 @@ def test_unit_queues_bitwise(gpu, queues):
     for p in (RenderParams(96, 64, 40, 8, 5, 16, 16), RenderParams(96, 64, 8, 8, 5, 8, 8, shard=1, num_shards=3),
               RenderParams(70, 50, 3, 8, 5, 32, 32)):
         frames = []
-        for q in ("single", queues):
+        for q in ({"unit_queues": "single"}, queues):
             for order in ("cost", "morton"):
-                with gpu.DeviceScene(sc, options={"tile_order": order, "unit_queues": q}) as ds:
+                with gpu.DeviceScene(sc, options={"tile_order": order, **q}) as ds:
                     rgb, _, st = ds.render(p)
                 frames.append((rgb, st["rays"], st["pixels"]))
         for rgb, rays, px in frames[1:]:
