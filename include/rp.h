@@ -223,7 +223,7 @@ typedef struct rp_scene_options {
   uint32_t node_format;     /* RP_NODES_* */
   uint32_t leaf_break;      /* speculative traversal: a wave moves to the leaf tests once at most this many of its
                                lanes still look for a leaf (0 -> 8 for scenes within the 256 MB Infinity Cache,
-                               12 above; 1..64) */
+                               16 above; 1..64) */
   uint32_t unit_queues;     /* RP_QUEUES_*: how the render blocks share out the units */
   uint32_t queue_chunk;     /* XCD_TILES: consecutive tiles of the order dealt to one queue at a time (0 -> 1) */
 } rp_scene_options;

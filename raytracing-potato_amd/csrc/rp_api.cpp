@@ -463,8 +463,9 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // 256 MB Infinity Cache (C5: 2.5 GB) loses 5-7 % to any reordering that scatters the concurrently rendered
   // tiles over the frame, and the Z-order keeps them together.
   s->tiles_auto = s->device_bytes > (256ull << 20) ? RP_TILES_MORTON : RP_TILES_COST;
-  // the speculative-traversal exit: C3 246.3 ms at 8 (3: 248.2, 12: 248.5), C5 2,103 ms at 12 (8: 2,118, 3: 2,229)
-  s->ks.leaf_break = opt.leaf_break ? opt.leaf_break : (s->device_bytes > (256ull << 20) ? 12u : 8u);
+  // the speculative-traversal exit: C3 246.3 ms at 8 (3: 248.2, 12: 248.5); C5 at 16 (per-XCD queues, ab34: 12 +0.4 %,
+  // 20 +0.1 %, 24 +0.7 %)
+  s->ks.leaf_break = opt.leaf_break ? opt.leaf_break : (s->device_bytes > (256ull << 20) ? 16u : 8u);
   // lanes still traversing before the finished ones shade: C3 24 (16: +0.2 %, 32: +0.7 %), C5 32 (-1.6 %)
   if (s->opt.trav_threshold == 0) s->opt.trav_threshold = s->device_bytes > (256ull << 20) ? 32u : DEF_TRAV_THRESHOLD;
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a

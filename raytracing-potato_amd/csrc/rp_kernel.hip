@@ -3,9 +3,9 @@
 // One lane = one pixel's path state.  Each lane loops
 //     [fetch pixel] -> [new sample: jitter + Camera::shoot] -> traverse -> shade -> ...
 // as a single flat loop (path regeneration), so every live lane of a wave executes the SAME traversal
-// code each iteration whatever bounce or sample it is on; lanes that finish a pixel refetch from a
-// device-wide atomic queue (persistent threads; the compiler folds the per-lane atomicAdd into one
-// wave atomic via ballot + mbcnt).  Traversal stacks live in LDS, lane-major ([depth][lane]) so a
+// code each iteration whatever bounce or sample it is on; lanes that finish a pixel refetch from the
+// atomic unit queue of their XCD group (persistent threads; the compiler folds the per-lane atomicAdd into
+// one wave atomic via ballot + mbcnt).  Traversal stacks live in LDS, lane-major ([depth][lane]) so a
 // wave's push/pop is bank-conflict-free whatever depth each lane is at.
 //
 // Arithmetic is IEEE binary64 in the reference's exact operation order (no contraction: this file is
