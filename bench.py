@@ -10,8 +10,8 @@ persistent HIP kernel (librp.so) from scene data resident in HBM, followed by li
 (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
 xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
 output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the
-RCCL communicator and takes the barrier and max-time reduction.  With N > 1 two frames are in flight (frame
-k renders on stream k % 2 with its own rp_workspace), so the end of one frame overlaps the start of the
+RCCL communicator and takes the barrier and max-time reduction.  With N > 1 three frames are in flight (frame
+k renders on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the
 next (--inflight).  The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both
 sides; the max over ranks is used.
 
@@ -142,7 +142,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
-                         "(0 = 1 on one GPU, 2 on several)")
+                         "(0 = 1 on one GPU, 3 on several)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic, one GPU: render only shard 0 of this many (the per-rank work of an N-GPU "
+                         "run), no gather; not a bench line")
     ap.add_argument("--opt", action="append", default=[],
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
@@ -174,13 +177,15 @@ def main():
     ds = DeviceScene(scene, device=local, options=options)
     info = ds.info()
     log(f"[rank {rank}] scene ready in {time.time() - t:.2f}s: {info}")
-    sp = shard_params(params, rank, world)
+    sp = shard_params(params, rank, world) if not args.shard_of else shard_params(params, 0, args.shard_of)
     with stdout_to_stderr():
         comm = bootstrap_comm(rank, world, local)
     # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
     # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.
-    F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 2)
+    # Per-rank work of an 8-GPU C3 frame (shard 0 of 8 on one GPU, --shard-of 8): 35.8 ms with one frame in
+    # flight, 29.9 with two, 29.3 with three, against 26.8 ms of work (profiles/r2/c3_v40_shard_inflight.json)
+    F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
     wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
@@ -209,6 +214,9 @@ def main():
             done = torch.cuda.Event()
             done.record(st)
             main_stream.wait_event(done)
+        if args.shard_of:
+            freed[i] = done if st is not main_stream else None
+            return
         # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks), on the main stream
         ds.frame_gather(comm, sp, bufs[i], frame_bgra=frame, counters=ctrs[i], stream=main_stream,
                         workspace=wss[i])
@@ -283,7 +291,9 @@ def main():
                        "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
-                       "scene_options": options or "defaults"},
+                       "scene_options": options or "defaults",
+                       **({"simulated_shard": f"shard 0 of {args.shard_of}, no gather (diagnostic)"}
+                          if args.shard_of else {})},
             "roofline": roof,
             "cpu_baseline": None,
         }
