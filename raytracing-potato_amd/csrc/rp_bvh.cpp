@@ -672,6 +672,8 @@ int validate(const rp_scene_desc* d, std::string& err) {
   if (d->n_hittables && !d->hittables) return fail("hittables is NULL");
   if (d->n_meshes && !d->meshes) return fail("meshes is NULL");
   if (d->n_materials && !d->materials) return fail("materials is NULL");
+  // the kernel carries a hit's material in 31 bits beside its primitive kind (rp_device.h HitRec::km)
+  if (d->n_materials >= 0x7FFFFFFFu) return fail("too many materials (>= 2^31 - 1)");
   if (d->n_textures && !d->textures) return fail("textures is NULL");
   auto check_tex = [&](uint32_t t, const char* what) -> bool {
     if (t >= d->n_textures) { err = std::string(what) + ": TextureId out of range"; return false; }

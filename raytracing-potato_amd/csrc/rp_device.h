@@ -344,9 +344,15 @@ RPK_INLINE double noise_real(int64_t x, int64_t y, int64_t z, int64_t seed) {
 
 // ------------------------------------------------------------------ traversal --------------------
 
+// The closest hit's primitive kind and material travel with it from the accepting test (bit 31 = triangle,
+// bits 0-30 = material; scene_create caps materials below 2^31 - 1): the shading of a triangle hit then
+// starts at the material and vertex loads instead of re-reading the primitive record first (one dependent
+// L2 round trip less).  KM_UNKNOWN: read them from the record (the stage-split engine does not keep them).
+constexpr uint32_t KM_TRIANGLE = 0x80000000u, KM_UNKNOWN = 0xFFFFFFFFu;
 struct HitRec {
   double t, u, v;  // u, v: barycentrics of hittable.rs:89-95 (triangles)
   int32_t prim;    // -1 = miss
+  uint32_t km = KM_UNKNOWN;
 };
 
 struct TravDiag {
@@ -472,6 +478,7 @@ RPK_INLINE void setup_ray32(V3 o, V3 d, double tmin, double qbound, Ray32& r) {
 struct TravState {
   double best, bu, bv;
   int32_t bestp;
+  uint32_t bestm;  // the closest hit's kind and material (HitRec::km)
   uint32_t cur, sp;
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
   uint32_t gy, py;  // Node8Q only (0 otherwise)
@@ -487,6 +494,7 @@ RPK_INLINE void trav_init(const KScene& S, double tmax, TravState& t, V3 d) {
   t.bu = 0.0;
   t.bv = 0.0;
   t.bestp = -1;
+  t.bestm = KM_UNKNOWN;
   t.cur = S.root;
   t.sp = 0;
   t.leaf = 0;
@@ -506,7 +514,8 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
                                                       k * (uint32_t)sizeof(rpl::Prim));
   const double2 g01 = q[0], g23 = q[1], g45 = q[2], g67 = q[3];
   const double2 g8k = q[4];  // g[8], {kind, material}
-  const uint32_t kind = (uint32_t)__double_as_longlong(g8k.y);
+  const uint64_t km = (uint64_t)__double_as_longlong(g8k.y);
+  const uint32_t kind = (uint32_t)km, mat = (uint32_t)(km >> 32);
   if (kind == rpl::PRIM_TRIANGLE) {
     // hittable.rs:65-101, exact expression order; ba, ca were pre-subtracted (same IEEE op)
     const V3 a = v3(g01.x, g01.y, g23.x);
@@ -528,7 +537,7 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
                     + pa.z * (ba.y * d.x - ba.x * d.y)) * inv_det;
     const double w = 1.0 - u - v;
     if (t < tmin || t > best || u < 0.0 || v < 0.0 || w < 0.0) return;
-    best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v;
+    best = t; ts.bestp = (int32_t)k; ts.bu = u; ts.bv = v; ts.bestm = KM_TRIANGLE | mat;
   } else {
     // hittable.rs:39-57
     const V3 c = v3(g01.x, g01.y, g23.x);
@@ -545,7 +554,7 @@ RPK_INLINE void prim_test(const KScene& S, uint32_t k, V3 o, V3 d, double tmin, 
       t = (-half_b + sq) / a;
       if (t < tmin || t > best) return;
     }
-    best = t; ts.bestp = (int32_t)k;
+    best = t; ts.bestp = (int32_t)k; ts.bestm = mat;
   }
 }
 
@@ -914,6 +923,7 @@ RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V
   hr.u = t.bu;
   hr.v = t.bv;
   hr.prim = t.bestp;
+  hr.km = t.bestm;
 }
 
 // Hit record of the closest primitive (hittable.rs:59-62, 103-107).
@@ -928,11 +938,12 @@ struct Surf {
 RPK_INLINE bool surface(const KScene& S, const HitRec& hr, V3 o, V3 d, Surf& s, bool force_uv = false) {
   const rpl::Prim* p = S.prims + hr.prim;
   s.p = add(o, smul(hr.t, d));  // Ray::at (utility.rs:67)
-  s.material = p->material;
+  const bool known = hr.km != KM_UNKNOWN;
+  s.material = known ? hr.km & ~KM_TRIANGLE : p->material;
   s.u = 0.0;
   s.v = 0.0;
   const bool need_uv = force_uv || S.mats[s.material].needs_uv != 0;
-  if (p->kind == rpl::PRIM_TRIANGLE) {
+  if (known ? (hr.km & KM_TRIANGLE) != 0 : p->kind == rpl::PRIM_TRIANGLE) {
     const double u = hr.u, v = hr.v, w = 1.0 - u - v;
     const rpl::PrimRef& pr = S.prim_refs[hr.prim];
     const uint32_t i0 = pr.v[0], i1 = pr.v[1], i2 = pr.v[2];

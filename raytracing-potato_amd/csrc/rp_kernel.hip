@@ -112,6 +112,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   ts.sp = 0u;
   ts.best = 0.0;
   ts.bestp = -1;
+  ts.bestm = KM_UNKNOWN;
   ts.bu = ts.bv = 0.0;
   ts.gy = ts.py = 0u;
   uint32_t pi = 0, pj = 0;
@@ -198,6 +199,10 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       hr.u = ts.bu;
       hr.v = ts.bv;
       hr.prim = ts.bestp;
+      // the f32-node (cache-resident scene) kernel carries the hit's kind and material out of the traversal
+      // (C3 -0.5 %); the q8 kernel of large scenes re-reads them (carrying them cost C5 +0.9 %: its traversal,
+      // 2/3 of the wave-cycles, pays the register)
+      hr.km = NF == rpl::NODES_Q8 ? KM_UNKNOWN : ts.bestm;
 
       // ---- shade.  Hits and misses share one spherical-uv site and one texture-sampling site, so a wave
       // with both pays for each f64 atan2/asin and texture walk once.

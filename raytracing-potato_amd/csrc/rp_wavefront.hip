@@ -275,6 +275,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
   ts.sp = 0u;
   ts.best = 0.0;
   ts.bestp = -1;
+  ts.bestm = KM_UNKNOWN;
   ts.bu = ts.bv = 0.0;
   ts.gy = ts.py = 0u;
   for (;;) {
