@@ -127,7 +127,7 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 #ifndef RPK_RNG_BATCH
 #define RPK_RNG_BATCH 48
 #endif
-static constexpr uint32_t RING = RPK_RING;
+static constexpr uint32_t RING = RPK_RING;  // slab ring capacity; a kernel keeps RngT::ring <= RING blocks ahead
 // Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs) -- measured 3.7% faster on C3 than
 // 3 waves/SIMD with the whole traversal stack in LDS (-DRPK_W3).
 #ifndef RPK_W3
@@ -160,17 +160,27 @@ static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
 #endif
 static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // this many lanes with room force a refill pass
 
-struct Rng {
+// RN = ring blocks in use (a power of two <= RING): the render kernel of the quantized-node (large-scene)
+// format keeps 4, the others 8 (rp_kernel.hip RingFor).
+template <uint32_t RN>
+struct RngT {
+  static constexpr uint32_t ring = RN;
+  // a lane's slab for this ring: key, RN ring blocks, 2 jitter blocks (compact: 416 B for RN = 4)
+  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = jit + 8;
+  static_assert(RN > RNG_CRIT && RN <= RING && (RN & (RN - 1)) == 0,
+                "ring: a power of two above the critical refill level (a full ring is never refilled), <= RING");
   uint4* slab;     // global: this lane's slab
   uint32_t pos;    // next keystream word (even)
   uint32_t* end;   // LDS cursor: one past the newest ring block
   uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
+template <class Rng>
 RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
   const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
   k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
   k[4] = c.x; k[5] = c.y; k[6] = c.z; k[7] = c.w;
 }
+template <class Rng>
 RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
   r.slab[SLAB_KEY] = make_uint4(k[0], k[1], k[2], k[3]);
   r.slab[SLAB_KEY + 1] = make_uint4(k[4], k[5], k[6], k[7]);
@@ -186,24 +196,27 @@ RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
 }
-RPK_INLINE uint4* ring_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_RING + 4 * (b % RING); }
-RPK_INLINE uint4* jit_slot(const Rng& r, uint32_t b) { return r.slab + SLAB_JIT + 4 * (b & 1u); }
+template <uint32_t RN>
+RPK_INLINE uint4* ring_slot(const RngT<RN>& r, uint32_t b) { return r.slab + SLAB_RING + 4 * (b & (RN - 1u)); }
+template <uint32_t RN>
+RPK_INLINE uint4* jit_slot(const RngT<RN>& r, uint32_t b) { return r.slab + RngT<RN>::jit + 4 * (b & 1u); }
 
 // The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
 // samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
 // round, not started) gets its key from the unit's seed and keystream block 0 here, batched with the other
 // lanes' ChaCha work -- at the fetch site the whole wave paid a ChaCha block for each fetching lane.
-RPK_INLINE void rng_refill(Rng& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
+template <uint32_t RN>
+RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
   const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
   const uint32_t b1 = (s + 1) >> 2, b2 = b1 + 1;
   const bool j1 = alive && !fresh && 4 * b1 < spp && r.jtag[(b1 & 1u) * BLOCK] != b1;
   const bool j2 = alive && !fresh && 4 * b2 < spp && r.jtag[(b2 & 1u) * BLOCK] != b2;
   const bool crit = alive && (fresh || have <= RNG_CRIT);
-  const bool room = alive && (fresh || have < RING || j1 || j2);
+  const bool room = alive && (fresh || have < RN || j1 || j2);
   if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
   if (room) {
     DREG(DREG_REFILL)
-    const bool main = fresh || crit || !(j1 || j2);
+    const bool main = fresh || crit || !(j1 || j2);  // crit: have <= RNG_CRIT < RN, so the ring has room
     const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
     uint32_t k[8], w[16];
     if (fresh) {
@@ -241,7 +254,8 @@ static __device__ __attribute__((noinline)) void gen_block(const uint4* slab, ui
   store_block(dst, w);
 }
 
-RPK_INLINE uint4 rng_jitter(Rng& r, uint32_t s) {
+template <uint32_t RN>
+RPK_INLINE uint4 rng_jitter(RngT<RN>& r, uint32_t s) {
   const uint32_t b = s >> 2;
   if (r.jtag[(b & 1u) * BLOCK] != b) {
     DREG(DREG_JIT_FALLBACK)
@@ -276,19 +290,23 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 #ifndef RPK_TRIES
 #define RPK_TRIES 2
 #endif
-static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * RING words (a power of two)");
-RPK_INLINE uint2 ring_u64(const Rng& r, uint32_t a) {  // stream words a, a+1 (a even)
-  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RING - 1u)) >> 1];
+static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * ring words (a power of two)");
+template <uint32_t RN>
+RPK_INLINE uint2 ring_u64(const RngT<RN>& r, uint32_t a) {  // stream words a, a+1 (a even)
+  return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RN - 1u)) >> 1];
 }
-RPK_INLINE double ring_f64(const Rng& r, uint32_t a) {  // Standard f64
+template <uint32_t RN>
+RPK_INLINE double ring_f64(const RngT<RN>& r, uint32_t a) {  // Standard f64
   const uint2 v = ring_u64(r, a);
   return words_f64(v.x, v.y);
 }
-RPK_INLINE double ring_sym(const Rng& r, uint32_t a) {  // 2 * Standard f64 - 1
+template <uint32_t RN>
+RPK_INLINE double ring_sym(const RngT<RN>& r, uint32_t a) {  // 2 * Standard f64 - 1
   const uint2 v = ring_u64(r, a);
   return words_sym(v.x, v.y);
 }
-RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
+template <uint32_t RN>
+RPK_INLINE void ring_ensure(RngT<RN>& r, uint32_t last_blk) {
   while (last_blk >= *r.end) {
     DREG(DREG_RNG_FALLBACK)
     const uint32_t b = *r.end;
@@ -297,7 +315,8 @@ RPK_INLINE void ring_ensure(Rng& r, uint32_t last_blk) {
   }
 }
 // One Standard f64 draw (rand 0.8 gen::<f64>, two stream words)
-RPK_INLINE double gen_f64(Rng& r) {
+template <uint32_t RN>
+RPK_INLINE double gen_f64(RngT<RN>& r) {
   ring_ensure(r, r.pos >> 4);
   const double x = ring_f64(r, r.pos);
   r.pos += 2;

@@ -37,6 +37,12 @@ namespace rpk {
 #ifndef RPK_PRIO_REFILL
 #define RPK_PRIO_REFILL 0
 #endif
+// Keystream blocks a lane keeps ahead (rp_device.h RngT): 8, or 4 in the quantized-node kernel that large
+// scenes use -- C5 -1.7 % (its smaller slab footprint leaves L2 and the Infinity Cache to the 1.1 GB scene;
+// 2 blocks: -0.9 %), while C3 wants 8 (4: +0.6 %, 2: +16 %), ab38.  A run-time ring size cost C3 +0.3 % (ab39).
+template <uint32_t NF>
+constexpr uint32_t RingFor = NF == rpl::NODES_Q8 ? 4u : RING;
+
 // PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
 // and timings of the frame kernel never mix with it.
 template <bool PROBE, bool SPILL, uint32_t NF>
@@ -96,8 +102,12 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   uint32_t depth = 0;
   uint32_t work = 0;  // PROBE: the probed sample's traversal work (rp_device.h WORK_*)
   bool first = true;
-  Rng rng;
+  RngT<RingFor<NF>> rng;
+#ifdef RPK_COLD_SLAB  // the experiment's cold words sit behind the full-ring layout (SLAB_N per lane)
   rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N;
+#else
+  rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * RngT<RingFor<NF>>::lane_n;
+#endif
   rng.end = c_u + 5 * BLOCK + tid;
   rng.jtag = c_u + 6 * BLOCK + tid;
   rng.pos = 0;

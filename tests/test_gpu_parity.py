@@ -317,6 +317,18 @@ def test_spilled_traversal_stack(gpu, name, arg, fmt):
     _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 17, "node_format": fmt})
 
 
+@pytest.mark.parametrize("fmt", ["f32", "q8"])
+@pytest.mark.parametrize("name", ["bunny_full", "more_balls"])
+def test_keystream_ring_sizes(gpu, name, fmt):
+    """The keystream ring is a cache of the same stream: the f32-node kernel keeps 8 ChaCha12 blocks per lane
+    ahead, the q8 kernel 4 in a compact slab (rp_kernel.hip RingFor).  At 40 spp (10 jitter blocks, many ring
+    wraps) both give the oracle's image and ray counts."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.CATALOGUE[name](), 64, 40)
+    _check(gpu, sc, RenderParams(64, 40, 40, 8, scenes.DEFAULT_SEED), options={"node_format": fmt})
+
+
 @pytest.mark.parametrize("always_max", [0, 4])
 def test_always_tested_primitives(gpu, always_max):
     """Primitives whose box dwarfs the rest of the scene (the C3 ground sphere) are kept out of the tree and
