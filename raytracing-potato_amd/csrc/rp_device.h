@@ -290,6 +290,9 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 #ifndef RPK_TRIES
 #define RPK_TRIES 2
 #endif
+#ifndef RPK_TRIES_BALL  // UnitBall (Metal fuzz): its own count, for experiments
+#define RPK_TRIES_BALL RPK_TRIES
+#endif
 static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * ring words (a power of two)");
 template <uint32_t RN>
 RPK_INLINE uint2 ring_u64(const RngT<RN>& r, uint32_t a) {  // stream words a, a+1 (a even)
@@ -1126,20 +1129,20 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, R& rng
       DREG(DREG_METAL)
       if (dot(h.n, d) > 0.0) return false;
       double x = 0.0, y = 0.0, z = 0.0;
-      // UnitBall (randomness.rs:39-53): tries of 3 draws, RPK_TRIES per round (see ring_ensure)
-      for (uint32_t a = rng.pos;; a += 6u * RPK_TRIES) {
+      // UnitBall (randomness.rs:39-53): tries of 3 draws, RPK_TRIES_BALL per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 6u * RPK_TRIES_BALL) {
         DREG(DREG_LOOP_METAL)
-        ring_ensure(rng, (a + 6u * RPK_TRIES - 1u) >> 4);
-        double tx[RPK_TRIES], ty[RPK_TRIES], tz[RPK_TRIES];
+        ring_ensure(rng, (a + 6u * RPK_TRIES_BALL - 1u) >> 4);
+        double tx[RPK_TRIES_BALL], ty[RPK_TRIES_BALL], tz[RPK_TRIES_BALL];
 #pragma unroll
-        for (int j = 0; j < RPK_TRIES; j++) {
+        for (int j = 0; j < RPK_TRIES_BALL; j++) {
           tx[j] = ring_sym(rng, a + 6u * j);
           ty[j] = ring_sym(rng, a + 6u * j + 2u);
           tz[j] = ring_sym(rng, a + 6u * j + 4u);
         }
         bool done = false;
 #pragma unroll
-        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+        for (int j = RPK_TRIES_BALL - 1; j >= 0; j--) {  // the first accepted try wins
           const double qx = tx[j], qy = ty[j], qz = tz[j];
           if ((qx * qx + qy * qy) + qz * qz < 1.0) { x = qx; y = qy; z = qz; rng.pos = a + 6u * (j + 1); done = true; }
         }
