@@ -187,7 +187,16 @@ RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
 }
 RPK_INLINE void store_block(uint4* dst, const uint32_t w[16]) {
 #pragma unroll
-  for (int q = 0; q < 4; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  for (int q = 0; q < 4; q++) {
+#if defined(RPK_NT_STORE) || defined(RPK_NT_ALL)  // experiment: keystream blocks stored non-temporal
+    __builtin_nontemporal_store(w[4 * q], &dst[q].x);
+    __builtin_nontemporal_store(w[4 * q + 1], &dst[q].y);
+    __builtin_nontemporal_store(w[4 * q + 2], &dst[q].z);
+    __builtin_nontemporal_store(w[4 * q + 3], &dst[q].w);
+#else
+    dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+#endif
+  }
 }
 RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
 #pragma unroll
@@ -246,7 +255,7 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
 // Keystream block b of the lane's key into dst, for the rare draw that finds its block not made yet.  Out
 // of line: the kernel is ~50 KB of code against a 64 KB instruction cache shared by two CUs, and each
 // inlined ChaCha12 is ~2.5 KB that only the fallback paths execute.
-static __device__ __attribute__((noinline)) void gen_block(const uint4* slab, uint32_t b, uint4* dst) {
+static __device__ __attribute__((noinline, unused)) void gen_block(const uint4* slab, uint32_t b, uint4* dst) {
   const uint4 a = slab[SLAB_KEY], c = slab[SLAB_KEY + 1];
   const uint32_t k[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
   uint32_t w[16];
@@ -262,7 +271,13 @@ RPK_INLINE uint4 rng_jitter(RngT<RN>& r, uint32_t s) {
     gen_block(r.slab, b, jit_slot(r, b));
     r.jtag[(b & 1u) * BLOCK] = b;
   }
+#ifdef RPK_NT_ALL
+  const uint4* j = jit_slot(r, b) + (s & 3u);
+  return make_uint4(__builtin_nontemporal_load(&j->x), __builtin_nontemporal_load(&j->y),
+                    __builtin_nontemporal_load(&j->z), __builtin_nontemporal_load(&j->w));
+#else
   return jit_slot(r, b)[s & 3u];
+#endif
 }
 
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
@@ -296,7 +311,12 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * ring words (a power of two)");
 template <uint32_t RN>
 RPK_INLINE uint2 ring_u64(const RngT<RN>& r, uint32_t a) {  // stream words a, a+1 (a even)
+#ifdef RPK_NT_ALL
+  const uint2* q = reinterpret_cast<const uint2*>(r.slab + SLAB_RING) + ((a & (16u * RN - 1u)) >> 1);
+  return make_uint2(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y));
+#else
   return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RN - 1u)) >> 1];
+#endif
 }
 template <uint32_t RN>
 RPK_INLINE double ring_f64(const RngT<RN>& r, uint32_t a) {  // Standard f64
