@@ -1026,6 +1026,15 @@ RPK_INLINE uint32_t tex_resolve(const KScene& S, uint32_t tid, const Surf& h) {
   return tid;
 }
 
+// One RGBA8 texel (RPK_NT_TEX experiment: a non-temporal load, the sky's random bounce lookups kept out of L2)
+RPK_INLINE uint32_t texel(const KScene& S, uint64_t i) {
+#ifdef RPK_NT_TEX
+  return __builtin_nontemporal_load(S.texels + i);
+#else
+  return S.texels[i];
+#endif
+}
+
 // texture.rs:40-49 Image: clamp, then saturating `as u32` -> texel index
 RPK_INLINE uint64_t image_texel(const rpl::Texture& t, const Surf& h) {
   const double w = (double)t.width, hh = (double)t.height;
@@ -1087,7 +1096,7 @@ RPK_INLINE V3 tex_value(const KScene& S, uint32_t tid, const Surf& h, uint32_t p
 RPK_INLINE V3 tex_sample(const KScene& S, uint32_t tid, const Surf& h) {
   tid = tex_resolve(S, tid, h);
   const rpl::Texture& t = S.texs[tid];
-  const uint32_t px = t.kind == 3 ? S.texels[image_texel(t, h)] : 0u;
+  const uint32_t px = t.kind == 3 ? texel(S, image_texel(t, h)) : 0u;
   return tex_value(S, tid, h, px);
 }
 
@@ -1251,11 +1260,11 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
       t.height = S.background.img_h;
       t.texel_offset = S.background.img_off;
       tid1 = S.background.tex;
-      px1 = S.texels[image_texel(t, h)];
+      px1 = texel(S, image_texel(t, h));
     } else {
       tid1 = tex_resolve(S, ta ? m->absorb_tex : emit_tex, h);
       const rpl::Texture& t = S.texs[tid1];
-      if (t.kind == 3) px1 = S.texels[image_texel(t, h)];
+      if (t.kind == 3) px1 = texel(S, image_texel(t, h));
     }
   }
   // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)

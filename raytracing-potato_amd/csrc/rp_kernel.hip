@@ -254,10 +254,17 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           } else {  // one batch of several: its sum, reduced in batch order by reduce_batches
             const uint64_t u = (uint64_t)slot * A->P.nbatch + batch;
             double* part = A->P.partial;
+#ifdef RPK_NT_OUT  // experiment: the batch sums (written once, read by reduce_batches) stored non-temporal
+            __builtin_nontemporal_store(sum_x, &part[3 * u + 0]);
+            __builtin_nontemporal_store(sum_y, &part[3 * u + 1]);
+            __builtin_nontemporal_store(sum_z, &part[3 * u + 2]);
+            __builtin_nontemporal_store((uint32_t)hits, &A->P.partial_hits[u]);
+#else
             part[3 * u + 0] = sum_x;
             part[3 * u + 1] = sum_y;
             part[3 * u + 2] = sum_z;
             A->P.partial_hits[u] = hits;
+#endif
           }
           ended_pixel = batch == 0;
           DIAG(if (!PROBE) {
