@@ -133,7 +133,13 @@ static constexpr uint32_t RING = RPK_RING;  // slab ring capacity; a kernel keep
 #ifndef RPK_W3
 #define RPK_W4
 #endif
+#ifdef RPK_SLAB_ALIGN  // experiment: ring and jitter blocks 64 B aligned, each lane's slab on its own 128 B lines
+static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 4, SLAB_JIT = 4 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
+#define RPK_SLAB_ROUND(n) (((n) + 7u) & ~7u)
+#else
 static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
+#define RPK_SLAB_ROUND(n) (n)
+#endif
 // The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS; the
 // host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to the lane's global run
 // (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).  -DRPK_COLD_IN_SLAB keeps them
@@ -142,10 +148,13 @@ static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, 
 #if defined(RPK_W4) && defined(RPK_COLD_IN_SLAB)
 #define RPK_COLD_SLAB
 #endif
+#ifndef RPK_SLAB_PAD  // experiment: uint4 units of padding after each lane's slab (128 B line alignment)
+#define RPK_SLAB_PAD 0
+#endif
 #ifdef RPK_COLD_SLAB
 static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
 #else
-static constexpr uint32_t SLAB_N = SLAB_COLD;
+static constexpr uint32_t SLAB_N = RPK_SLAB_ROUND(SLAB_COLD + RPK_SLAB_PAD);
 #endif
 #ifndef RPK_RNG_CRIT
 #define RPK_RNG_CRIT 2
@@ -166,7 +175,7 @@ template <uint32_t RN>
 struct RngT {
   static constexpr uint32_t ring = RN;
   // a lane's slab for this ring: key, RN ring blocks, 2 jitter blocks (compact: 416 B for RN = 4)
-  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = jit + 8;
+  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = RPK_SLAB_ROUND(jit + 8 + RPK_SLAB_PAD);
   static_assert(RN > RNG_CRIT && RN <= RING && (RN & (RN - 1)) == 0,
                 "ring: a power of two above the critical refill level (a full ring is never refilled), <= RING");
   uint4* slab;     // global: this lane's slab
