@@ -184,12 +184,6 @@ struct RngT {
   uint32_t* jtag;  // LDS cursors: jtag[0], jtag[BLOCK]
 };
 template <class Rng>
-RPK_INLINE void load_key(const Rng& r, uint32_t k[8]) {
-  const uint4 a = r.slab[SLAB_KEY], c = r.slab[SLAB_KEY + 1];
-  k[0] = a.x; k[1] = a.y; k[2] = a.z; k[3] = a.w;
-  k[4] = c.x; k[5] = c.y; k[6] = c.z; k[7] = c.w;
-}
-template <class Rng>
 RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
   r.slab[SLAB_KEY] = make_uint4(k[0], k[1], k[2], k[3]);
   r.slab[SLAB_KEY + 1] = make_uint4(k[4], k[5], k[6], k[7]);
@@ -219,7 +213,8 @@ RPK_INLINE uint4* ring_slot(const RngT<RN>& r, uint32_t b) { return r.slab + SLA
 template <uint32_t RN>
 RPK_INLINE uint4* jit_slot(const RngT<RN>& r, uint32_t b) { return r.slab + RngT<RN>::jit + 4 * (b & 1u); }
 
-// The refill pass (wave-uniform call site).  `s` is the lane's last sample whose jitter is consumed;
+// The refill pass (wave-uniform call site).  `seed` is the lane's unit seed (the RNG contract's
+// seed_from_u64 argument).  `s` is the lane's last sample whose jitter is consumed;
 // samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
 // round, not started) gets its key from the unit's seed and keystream block 0 here, batched with the other
 // lanes' ChaCha work -- at the fetch site the whole wave paid a ChaCha block for each fetching lane.
@@ -237,12 +232,13 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
     const bool main = fresh || crit || !(j1 || j2);  // crit: have <= RNG_CRIT < RN, so the ring has room
     const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
     uint32_t k[8], w[16];
+    // The key is recomputed from the unit's seed (PCG32 seed_from_u64, ~100 VALU) rather than loaded from the
+    // slab: a slab load that misses L2 stalls the whole pass before its ChaCha work (C3 -0.7 %, C5 -0.1 %,
+    // ab48).  A fresh unit still stores it for the in-place fallback (gen_block).
+    seed_key(seed, k);
     if (fresh) {
       DREG(DREG_BEGIN_PIXEL)
-      seed_key(seed, k);
       store_key(r, k);
-    } else {
-      load_key(r, k);
     }
     chacha12(k, b, w);
     store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);

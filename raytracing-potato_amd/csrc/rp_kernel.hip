@@ -146,7 +146,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     if (RPK_PRIO_REFILL != RPK_PRIO_SHADE) __builtin_amdgcn_s_setprio(RPK_PRIO_REFILL);
     {
       KArgsPtr A = kargs();
-      const uint64_t seed = fresh ? unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch) : 0ull;  // RNG contract
+      const uint64_t seed = unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch);  // RNG contract
       rng_refill(rng, alive, fresh, seed, start ? s - 1 : s, unit_spp(A, batch));
     }
     if (start) {
