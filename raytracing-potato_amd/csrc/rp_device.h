@@ -20,6 +20,18 @@
     defined(RPK_BATCH_LEAF)
 #error "result-changing experiment macros are not part of the product kernel"
 #endif
+// Timing experiments are not compile-time switches of the product sources either: the kernel below is the
+// product path only (plus the RPK_DIAG instrumentation).  tools/build_variant.sh builds an experiment from a
+// patched copy of these sources; the switches of earlier rounds are refused so a stale command line cannot
+// silently build something else.
+#if defined(RPK_NT_STORE) || defined(RPK_NT_ALL) || defined(RPK_NT_TEX) || defined(RPK_NT_OUT) ||           \
+    defined(RPK_SLAB_ALIGN) || defined(RPK_SLAB_PAD) || defined(RPK_COLD_SLAB) || defined(RPK_COLD_IN_SLAB) || \
+    defined(RPK_W3) || defined(RPK_W4) || defined(RPK_WAVES) || defined(RPK_TRIES_BALL) ||             \
+    defined(RPK_NO_SPECULATIVE) || defined(RPK_NODE_BREAK) || defined(RPK_TRIES) || defined(RPK_RING) ||       \
+    defined(RPK_RNG_BATCH) || defined(RPK_RNG_CRIT) || defined(RPK_PRIM_BREAK) || defined(RPK_PRIO_TRAV) ||    \
+    defined(RPK_PRIO_SHADE) || defined(RPK_PRIO_REFILL) || defined(RPK_SORT_Q) || defined(RPK_WF_REFILL)
+#error "experiment macros are not part of the product kernel (tools/build_variant.sh patches a copy instead)"
+#endif
 
 namespace rpk {
 
@@ -121,53 +133,19 @@ RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 // Slab layout per lane (uint4 units): [0,2) key words, [2, 2+4*RING) ring (block b in slot b % RING),
 // [2+4*RING, +8) jitter blocks (block b in slot b & 1).  Per-lane cursors (LDS): end = one past the
 // newest ring block; jtag[2] = block held by each jitter slot.
-#ifndef RPK_RING
-#define RPK_RING 8
-#endif
-#ifndef RPK_RNG_BATCH
-#define RPK_RNG_BATCH 48
-#endif
-static constexpr uint32_t RING = RPK_RING;  // slab ring capacity; a kernel keeps RngT::ring <= RING blocks ahead
-// Occupancy: the default build asks for 4 waves/SIMD (128 VGPRs) -- measured 3.7% faster on C3 than
-// 3 waves/SIMD with the whole traversal stack in LDS (-DRPK_W3).
-#ifndef RPK_W3
-#define RPK_W4
-#endif
-#ifdef RPK_SLAB_ALIGN  // experiment: ring and jitter blocks 64 B aligned, each lane's slab on its own 128 B lines
-static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 4, SLAB_JIT = 4 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
-#define RPK_SLAB_ROUND(n) (((n) + 7u) & ~7u)
-#else
-static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING, SLAB_COLD = SLAB_JIT + 8;
-#define RPK_SLAB_ROUND(n) (n)
-#endif
-// The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS; the
-// host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to the lane's global run
-// (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).  -DRPK_COLD_IN_SLAB keeps them
-// in the keystream slab instead (v31 and before): C3 +2.6 %, C5 +4.6 % frame time -- the slab shrinks
-// from 720 to 672 B per lane and the shading site loses 6 global loads and 6 stores.
-#if defined(RPK_W4) && defined(RPK_COLD_IN_SLAB)
-#define RPK_COLD_SLAB
-#endif
-#ifndef RPK_SLAB_PAD  // experiment: uint4 units of padding after each lane's slab (128 B line alignment)
-#define RPK_SLAB_PAD 0
-#endif
-#ifdef RPK_COLD_SLAB
-static constexpr uint32_t SLAB_N = SLAB_COLD + 3;  // + pixel sum and throughput (6 f64) when not in LDS
-#else
-static constexpr uint32_t SLAB_N = RPK_SLAB_ROUND(SLAB_COLD + RPK_SLAB_PAD);
-#endif
-#ifndef RPK_RNG_CRIT
-#define RPK_RNG_CRIT 2
-#endif
-static constexpr uint32_t RNG_CRIT = RPK_RNG_CRIT;
+static constexpr uint32_t RING = 8;  // slab ring capacity; a kernel keeps RngT::ring <= RING blocks ahead
+static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING;
+// The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS (in the
+// slab: C3 +2.6 %, C5 +4.6 %); the host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to
+// the lane's global run (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).
+static constexpr uint32_t SLAB_N = SLAB_JIT + 8;
+// A refill pass runs when some lane is at or below RNG_CRIT blocks ahead, or RNG_BATCH lanes have room.
+static constexpr uint32_t RNG_CRIT = 2, RNG_BATCH = 48;
 // Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
 // the wave still look for a leaf (rp_scene_options.leaf_break; C3: 0 -> 3 was -2.7 % frame time, 8 is -0.8 %
-// more; C5 wants 12), and the leaf loop once at most RPK_PRIM_BREAK lanes still test primitives (their
+// more; C5 wants 12-16), and the leaf loop once at most PRIM_BREAK lanes still test primitives (their
 // remaining run is parked as a leaf entry; C3 0 -> 12: -3.7 %, C5 -0.8 %; 6-16 within 0.5 %).
-#ifndef RPK_PRIM_BREAK
-#define RPK_PRIM_BREAK 12
-#endif
-static constexpr uint32_t RNG_BATCH = RPK_RNG_BATCH;  // this many lanes with room force a refill pass
+static constexpr uint32_t PRIM_BREAK = 12;
 
 // RN = ring blocks in use (a power of two <= RING): the render kernel of the quantized-node (large-scene)
 // format keeps 4, the others 8 (rp_kernel.hip RingFor).
@@ -175,7 +153,7 @@ template <uint32_t RN>
 struct RngT {
   static constexpr uint32_t ring = RN;
   // a lane's slab for this ring: key, RN ring blocks, 2 jitter blocks (compact: 416 B for RN = 4)
-  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = RPK_SLAB_ROUND(jit + 8 + RPK_SLAB_PAD);
+  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = jit + 8;
   static_assert(RN > RNG_CRIT && RN <= RING && (RN & (RN - 1)) == 0,
                 "ring: a power of two above the critical refill level (a full ring is never refilled), <= RING");
   uint4* slab;     // global: this lane's slab
@@ -191,14 +169,7 @@ RPK_INLINE void store_key(Rng& r, const uint32_t k[8]) {
 RPK_INLINE void store_block(uint4* dst, const uint32_t w[16]) {
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-#if defined(RPK_NT_STORE) || defined(RPK_NT_ALL)  // experiment: keystream blocks stored non-temporal
-    __builtin_nontemporal_store(w[4 * q], &dst[q].x);
-    __builtin_nontemporal_store(w[4 * q + 1], &dst[q].y);
-    __builtin_nontemporal_store(w[4 * q + 2], &dst[q].z);
-    __builtin_nontemporal_store(w[4 * q + 3], &dst[q].w);
-#else
     dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
-#endif
   }
 }
 RPK_INLINE void load_block(const uint4* src, uint32_t w[16]) {
@@ -276,13 +247,7 @@ RPK_INLINE uint4 rng_jitter(RngT<RN>& r, uint32_t s) {
     gen_block(r.slab, b, jit_slot(r, b));
     r.jtag[(b & 1u) * BLOCK] = b;
   }
-#ifdef RPK_NT_ALL
-  const uint4* j = jit_slot(r, b) + (s & 3u);
-  return make_uint4(__builtin_nontemporal_load(&j->x), __builtin_nontemporal_load(&j->y),
-                    __builtin_nontemporal_load(&j->z), __builtin_nontemporal_load(&j->w));
-#else
   return jit_slot(r, b)[s & 3u];
-#endif
 }
 
 // rand 0.8 Standard f64: (u64 >> 11) * 2^-53 (exact conversions)
@@ -301,27 +266,17 @@ RPK_INLINE double words_sym(uint32_t lo, uint32_t hi) {
 // its slab (L2-resident), so stream word a sits at ring word a % (16*RING) while its block is held
 // (blocks [end - RING, end)).  A draw site makes sure every block it touches is there (ring_ensure:
 // generated in place when the refill pass has not made it yet, rare) and loads its u64 words with one
-// dwordx2 each.  Rejection loops (UnitBall / UnitSphere / UnitDisk) load and evaluate RPK_TRIES tries at
+// dwordx2 each.  Rejection loops (UnitBall / UnitSphere / UnitDisk) load and evaluate TRIES tries at
 // once and keep the first accepted one -- the draws consumed, and so the stream, are exactly the
 // sequential loop's.  A wave iterates until its slowest lane accepts: with
 // acceptance p a lane needs a geometric number of tries, and the wave's maximum over its ~20 shading lanes
 // is ~5 single tries for the ball (p = pi/6); each round pays one ring-load latency.  (Before, a draw
 // checked its block and the wave copied a 16-word block into LDS whenever any lane crossed one.)
-#ifndef RPK_TRIES
-#define RPK_TRIES 2
-#endif
-#ifndef RPK_TRIES_BALL  // UnitBall (Metal fuzz): its own count, for experiments
-#define RPK_TRIES_BALL RPK_TRIES
-#endif
+static constexpr uint32_t TRIES = 2;  // (1 or 3 tries: +0.6 / +0.9 %; 3 or 4 for Metal alone: +0.6 / +1.3 %)
 static_assert((RING & (RING - 1)) == 0, "ring_u64 indexes the ring as 16 * ring words (a power of two)");
 template <uint32_t RN>
 RPK_INLINE uint2 ring_u64(const RngT<RN>& r, uint32_t a) {  // stream words a, a+1 (a even)
-#ifdef RPK_NT_ALL
-  const uint2* q = reinterpret_cast<const uint2*>(r.slab + SLAB_RING) + ((a & (16u * RN - 1u)) >> 1);
-  return make_uint2(__builtin_nontemporal_load(&q->x), __builtin_nontemporal_load(&q->y));
-#else
   return reinterpret_cast<const uint2*>(r.slab + SLAB_RING)[(a & (16u * RN - 1u)) >> 1];
-#endif
 }
 template <uint32_t RN>
 RPK_INLINE double ring_f64(const RngT<RN>& r, uint32_t a) {  // Standard f64
@@ -752,9 +707,7 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
     gx = W8_GROUP | (c1.z & rpl::W8_INDEX);
     gy = ih | imask << 8;
     w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);
-#ifndef RPK_NO_SPECULATIVE
     if ((uint32_t)__popcll(__ballot(py == 0u)) <= S.leaf_break) break;
-#endif
   }
   // ---- leaves: one primitive per lane per iteration from the parked group, then a waiting one
   while (py != 0u) {
@@ -768,7 +721,7 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
       px = 0u;
       if (!(gx & W8_GROUP)) w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);  // park the waiting group
     }
-    if (RPK_PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(py != 0u)) <= RPK_PRIM_BREAK) break;
+    if (PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(py != 0u)) <= PRIM_BREAK) break;
   }
   ts.cur = gx;
   ts.gy = gy;
@@ -907,7 +860,6 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     }
     if (n_hit) cur = cc[0];
     else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
-#ifndef RPK_NO_SPECULATIVE
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
     // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.
     if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
@@ -917,10 +869,6 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
     // last few descents ran with most of the wave idle (those lanes resume their descent next step)
     if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
-#ifdef RPK_NODE_BREAK  // experiment: leave once at most this many lanes are still descending at all
-    if ((uint32_t)__popcll(__ballot(true)) <= RPK_NODE_BREAK) break;
-#endif
-#endif
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
@@ -946,7 +894,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
         leaf = 0u;
       }
     }
-    if (RPK_PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= RPK_PRIM_BREAK) {
+    if (PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= PRIM_BREAK) {
       // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
       if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
       break;
@@ -1031,14 +979,8 @@ RPK_INLINE uint32_t tex_resolve(const KScene& S, uint32_t tid, const Surf& h) {
   return tid;
 }
 
-// One RGBA8 texel (RPK_NT_TEX experiment: a non-temporal load, the sky's random bounce lookups kept out of L2)
-RPK_INLINE uint32_t texel(const KScene& S, uint64_t i) {
-#ifdef RPK_NT_TEX
-  return __builtin_nontemporal_load(S.texels + i);
-#else
-  return S.texels[i];
-#endif
-}
+// One RGBA8 texel (a non-temporal load, keeping the sky's random bounce lookups out of L2, cost +5 %)
+RPK_INLINE uint32_t texel(const KScene& S, uint64_t i) { return S.texels[i]; }
 
 // texture.rs:40-49 Image: clamp, then saturating `as u32` -> texel index
 RPK_INLINE uint64_t image_texel(const rpl::Texture& t, const Surf& h) {
@@ -1137,19 +1079,19 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, R& rng
       DREG(DREG_LAMBERT)
       if (dot(h.n, d) > 0.0) return false;
       double x = 0.0, y = 0.0, s = 0.0;
-      // UnitSphere (randomness.rs:58-73): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
-      for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
+      // UnitSphere (randomness.rs:58-73): tries of 2 draws, TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 4u * TRIES) {
         DREG(DREG_LOOP_LAMBERT)
-        ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
-        double tx[RPK_TRIES], ty[RPK_TRIES];
+        ring_ensure(rng, (a + 4u * TRIES - 1u) >> 4);
+        double tx[TRIES], ty[TRIES];
 #pragma unroll
-        for (int j = 0; j < RPK_TRIES; j++) {
+        for (int j = 0; j < TRIES; j++) {
           tx[j] = ring_sym(rng, a + 4u * j);
           ty[j] = ring_sym(rng, a + 4u * j + 2u);
         }
         bool done = false;
 #pragma unroll
-        for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+        for (int j = TRIES - 1; j >= 0; j--) {  // the first accepted try wins
           const double qx = tx[j], qy = ty[j], qs = qx * qx + qy * qy;
           if (qs < 1.0) { x = qx; y = qy; s = qs; rng.pos = a + 4u * (j + 1); done = true; }
         }
@@ -1163,20 +1105,20 @@ RPK_INLINE bool scatter_eval(const rpl::Material& m, V3 d, const Surf& h, R& rng
       DREG(DREG_METAL)
       if (dot(h.n, d) > 0.0) return false;
       double x = 0.0, y = 0.0, z = 0.0;
-      // UnitBall (randomness.rs:39-53): tries of 3 draws, RPK_TRIES_BALL per round (see ring_ensure)
-      for (uint32_t a = rng.pos;; a += 6u * RPK_TRIES_BALL) {
+      // UnitBall (randomness.rs:39-53): tries of 3 draws, TRIES per round (see ring_ensure)
+      for (uint32_t a = rng.pos;; a += 6u * TRIES) {
         DREG(DREG_LOOP_METAL)
-        ring_ensure(rng, (a + 6u * RPK_TRIES_BALL - 1u) >> 4);
-        double tx[RPK_TRIES_BALL], ty[RPK_TRIES_BALL], tz[RPK_TRIES_BALL];
+        ring_ensure(rng, (a + 6u * TRIES - 1u) >> 4);
+        double tx[TRIES], ty[TRIES], tz[TRIES];
 #pragma unroll
-        for (int j = 0; j < RPK_TRIES_BALL; j++) {
+        for (int j = 0; j < TRIES; j++) {
           tx[j] = ring_sym(rng, a + 6u * j);
           ty[j] = ring_sym(rng, a + 6u * j + 2u);
           tz[j] = ring_sym(rng, a + 6u * j + 4u);
         }
         bool done = false;
 #pragma unroll
-        for (int j = RPK_TRIES_BALL - 1; j >= 0; j--) {  // the first accepted try wins
+        for (int j = TRIES - 1; j >= 0; j--) {  // the first accepted try wins
           const double qx = tx[j], qy = ty[j], qz = tz[j];
           if ((qx * qx + qy * qy) + qz * qz < 1.0) { x = qx; y = qy; z = qz; rng.pos = a + 6u * (j + 1); done = true; }
         }
@@ -1451,18 +1393,18 @@ RPK_INLINE void start_sample(R& rng, uint32_t s, uint32_t pi, uint32_t pj, V3& o
   const double ju = ((double)pi + words_f64(w0, w1)) / (double)A->P.W;
   const double jv = ((double)pj + words_f64(w2, w3)) / (double)A->P.H;
   double dx = 0.0, dy = 0.0;
-  // UnitDisk (randomness.rs:21-34): tries of 2 draws, RPK_TRIES per round (see ring_ensure)
-  for (uint32_t a = rng.pos;; a += 4u * RPK_TRIES) {
-    ring_ensure(rng, (a + 4u * RPK_TRIES - 1u) >> 4);
-    double tx[RPK_TRIES], ty[RPK_TRIES];
+  // UnitDisk (randomness.rs:21-34): tries of 2 draws, TRIES per round (see ring_ensure)
+  for (uint32_t a = rng.pos;; a += 4u * TRIES) {
+    ring_ensure(rng, (a + 4u * TRIES - 1u) >> 4);
+    double tx[TRIES], ty[TRIES];
 #pragma unroll
-    for (int j = 0; j < RPK_TRIES; j++) {
+    for (int j = 0; j < TRIES; j++) {
       tx[j] = ring_sym(rng, a + 4u * j);
       ty[j] = ring_sym(rng, a + 4u * j + 2u);
     }
     bool done = false;
 #pragma unroll
-    for (int j = RPK_TRIES - 1; j >= 0; j--) {  // the first accepted try wins
+    for (int j = TRIES - 1; j >= 0; j--) {  // the first accepted try wins
       const double qx = tx[j], qy = ty[j];
       if (qx * qx + qy * qy < 1.0) { dx = qx; dy = qy; rng.pos = a + 4u * (j + 1); done = true; }
     }

@@ -18,25 +18,13 @@
 
 namespace rpk {
 
-#if defined(RPK_WAVES)  // occupancy experiments (tools/build_variant.sh -DRPK_WAVES=5 with RP_LDS_DEPTH)
-#define RPK_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(RPK_WAVES)))
-#elif defined(RPK_W4)
+// 4 waves per SIMD (128 VGPRs): measured 3.7 % faster on C3 than 3 waves/SIMD with the whole traversal stack in
+// LDS; 5 waves (96 VGPRs) spills and loses 4-13 %.
 #define RPK_RENDER_ATTR __attribute__((amdgpu_waves_per_eu(4)))
-#else
-#define RPK_RENDER_ATTR
-#endif
 // Wave issue priority by phase (s_setprio): traversal 2 > shading 1 > keystream refill 0 -- a traversing
 // wave's next node fetch goes out sooner while VALU-heavy work fills the gaps (C3 234.7 -> 230.1 ms, C5
-// 2,039 -> 2,015 ms; traversal-only priority 231.5, priority to shading 237.6)
-#ifndef RPK_PRIO_TRAV
-#define RPK_PRIO_TRAV 2
-#endif
-#ifndef RPK_PRIO_SHADE
-#define RPK_PRIO_SHADE 1
-#endif
-#ifndef RPK_PRIO_REFILL
-#define RPK_PRIO_REFILL 0
-#endif
+// 2,039 -> 2,015 ms; traversal-only priority 231.5, priority to shading 237.6, refill at 1: +1.7 %)
+static constexpr int PRIO_TRAV = 2, PRIO_SHADE = 1, PRIO_REFILL = 0;
 // Keystream blocks a lane keeps ahead (rp_device.h RngT): 8, or 4 in the quantized-node kernel that large
 // scenes use -- C5 -1.7 % (its smaller slab footprint leaves L2 and the Infinity Cache to the 1.1 GB scene;
 // 2 blocks: -0.9 %), while C3 wants 8 (4: +0.6 %, 2: +16 %), ab38.  A run-time ring size cost C3 +0.3 % (ab39).
@@ -70,10 +58,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   // ---- lane state: one pixel's path at a time.  Hot state (ray, throughput, radiance, traversal)
   // in registers; cold per-pixel state (pixel sum, slot/pixel/sample counters, keystream cursors) in
   // LDS, structure-of-arrays so every access is bank-conflict-free; keystream blocks in the slab.
-#ifndef RPK_COLD_SLAB
   __shared__ double c_sum[3 * BLOCK];
   __shared__ double c_T[3 * BLOCK];
-#endif
   // (8 words per lane: one more would push the block past 40 KB of LDS and cost a block per CU)
   __shared__ uint32_t c_u[8 * BLOCK];
   const uint32_t tid = threadIdx.x;
@@ -82,32 +68,17 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   uint32_t& s = c_u[3 * BLOCK + tid];
   uint32_t& hits = c_u[4 * BLOCK + tid];
   uint32_t& batch = c_u[2 * BLOCK + tid];
-#ifdef RPK_COLD_SLAB
-  double* cold = reinterpret_cast<double*>(reinterpret_cast<uint4*>(kargs()->S.rng_slab) +
-                                           ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N + SLAB_COLD);
-  double& sum_x = cold[0];
-  double& sum_y = cold[1];
-  double& sum_z = cold[2];
-  double& T_x = cold[3];
-  double& T_y = cold[4];
-  double& T_z = cold[5];
-#else
   double& sum_x = c_sum[tid];
   double& sum_y = c_sum[BLOCK + tid];
   double& sum_z = c_sum[2 * BLOCK + tid];
   double& T_x = c_T[tid];  // path throughput (read and written once per shade)
   double& T_y = c_T[BLOCK + tid];
   double& T_z = c_T[2 * BLOCK + tid];
-#endif
   uint32_t depth = 0;
   uint32_t work = 0;  // PROBE: the probed sample's traversal work (rp_device.h WORK_*)
   bool first = true;
   RngT<RingFor<NF>> rng;
-#ifdef RPK_COLD_SLAB  // the experiment's cold words sit behind the full-ring layout (SLAB_N per lane)
-  rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * SLAB_N;
-#else
   rng.slab = reinterpret_cast<uint4*>(kargs()->S.rng_slab) + ((uint64_t)blockIdx.x * BLOCK + tid) * RngT<RingFor<NF>>::lane_n;
-#endif
   rng.end = c_u + 5 * BLOCK + tid;
   rng.jtag = c_u + 6 * BLOCK + tid;
   rng.pos = 0;
@@ -143,7 +114,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   for (;;) {
     DIAG(iters++;)
     DREG(DREG_ROUND)
-    if (RPK_PRIO_REFILL != RPK_PRIO_SHADE) __builtin_amdgcn_s_setprio(RPK_PRIO_REFILL);
+    __builtin_amdgcn_s_setprio(PRIO_REFILL);
     {
       KArgsPtr A = kargs();
       const uint64_t seed = unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch);  // RNG contract
@@ -178,7 +149,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       }
       Ray32 r;
       setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
-      __builtin_amdgcn_s_setprio(RPK_PRIO_TRAV);  // (RPK_PRIO_* above)
+      __builtin_amdgcn_s_setprio(PRIO_TRAV);  // (PRIO_* above)
       for (;;) {
         if (alive && !tdone) {
           DREG(DREG_STEP)
@@ -194,7 +165,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
         if (act == 0 || (waiting != 0 && (uint32_t)__popcll(act) < thr)) break;
       }
     }
-    __builtin_amdgcn_s_setprio(RPK_PRIO_SHADE);
+    __builtin_amdgcn_s_setprio(PRIO_SHADE);
     DIAG({ uint64_t t = stamp(); ph[2] += t - t_prev; t_prev = t; })
     if (__ballot(alive) == 0) break;
 
@@ -254,17 +225,10 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           } else {  // one batch of several: its sum, reduced in batch order by reduce_batches
             const uint64_t u = (uint64_t)slot * A->P.nbatch + batch;
             double* part = A->P.partial;
-#ifdef RPK_NT_OUT  // experiment: the batch sums (written once, read by reduce_batches) stored non-temporal
-            __builtin_nontemporal_store(sum_x, &part[3 * u + 0]);
-            __builtin_nontemporal_store(sum_y, &part[3 * u + 1]);
-            __builtin_nontemporal_store(sum_z, &part[3 * u + 2]);
-            __builtin_nontemporal_store((uint32_t)hits, &A->P.partial_hits[u]);
-#else
             part[3 * u + 0] = sum_x;
             part[3 * u + 1] = sum_y;
             part[3 * u + 2] = sum_z;
             A->P.partial_hits[u] = hits;
-#endif
           }
           ended_pixel = batch == 0;
           DIAG(if (!PROBE) {
@@ -496,9 +460,7 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
 // tile index.  Padding keys sort last.
 static constexpr int SORT_BLOCK = 1024;
 static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
-#ifndef RPK_SORT_Q
-#define RPK_SORT_Q 4.0f  // buckets per octave of cost
-#endif
+static constexpr float SORT_Q = 4.0f;  // buckets per octave of cost
 __device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every other bit of 16
   v = (v | (v << 4)) & 0x0F0Fu;
   v = (v | (v << 2)) & 0x3333u;
@@ -528,8 +490,8 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
         // quarter-octave buckets of the costliest probed sample's cost and of the mean cost (C3: 2^(1/4)
         // steps 248.1 ms, 2^(1/32) steps 250.1 ms, the round-1 ray-count cost 254.7 ms per frame)
         const float mean = (float)cost[i] / (float)probe_px;
-        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * RPK_SORT_Q), 63u);
-        qm = min((uint32_t)(log2f(mean + 1.0f) * RPK_SORT_Q), 63u);
+        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * SORT_Q), 63u);
+        qm = min((uint32_t)(log2f(mean + 1.0f) * SORT_Q), 63u);
       }
       kk = ((63u - ql) << 22) | ((63u - qm) << 16) | (spread8(ty) << 1) | spread8(tx);
     }

@@ -252,11 +252,9 @@ __global__ void __launch_bounds__(BLOCK) wf_shade_kernel(const KArgs args, const
 
 // ---- trace pass ---------------------------------------------------------------------------------------
 // Persistent: every lane takes the next queued ray as soon as its ray is done.  A wave refills its idle
-// lanes when at least RPK_WF_REFILL of them wait (the ray setup runs with many lanes) or when none
+// lanes when at least WF_REFILL of them wait (the ray setup runs with many lanes) or when none
 // traverse; the refilling lanes get consecutive entries (wave-aggregated atomic), so the ray loads coalesce.
-#ifndef RPK_WF_REFILL
-#define RPK_WF_REFILL 16
-#endif
+static constexpr uint32_t WF_REFILL = 16;
 template <bool SPILL, uint32_t NF>
 __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const WfArgs w) {
   extern __shared__ uint32_t lds_stack[];
@@ -280,7 +278,7 @@ __global__ void __launch_bounds__(BLOCK) wf_trace_kernel(const KArgs args, const
   ts.gy = ts.py = 0u;
   for (;;) {
     const uint64_t idle = __ballot(!have);
-    if (!drained && idle != 0 && ((uint32_t)__popcll(idle) >= RPK_WF_REFILL || __ballot(have) == 0)) {
+    if (!drained && idle != 0 && ((uint32_t)__popcll(idle) >= WF_REFILL || __ballot(have) == 0)) {
       if (!have) {
         q = atomicAdd(&w.wc[WC_FETCH], 1u);
         if (q < n) {

@@ -113,3 +113,26 @@ def test_product_kernel_refuses_result_changing_macros():
         r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-E", f"-D{macro}", src, "-o", os.devnull],
                            capture_output=True, text=True)
         assert r.returncode != 0 and "result-changing" in r.stderr, macro
+
+
+def test_product_kernel_has_no_experiment_switches():
+    """The product kernel sources are the product path plus the RPK_DIAG instrumentation only:
+    no #if on an experiment macro, and the switches of earlier rounds are refused by #error."""
+    import subprocess
+    allowed = {"RPK_DIAG", "RPK_DIAG_NOSTAMP", "RPK_DIAG_BIN_TICKS"}
+    for f in ("rp_device.h", "rp_kernel.hip", "rp_kernel.h", "rp_wavefront.hip", "rp_layout.h"):
+        src = open(os.path.join(PKG, "csrc", f)).read()
+        conds = re.findall(r"^\s*#\s*(?:if|ifdef|ifndef|elif)\b(.*)$", src, flags=re.M)
+        used = set()
+        for c in conds:
+            if "#error" in c:
+                continue
+            used |= set(re.findall(r"\bRPK_[A-Z0-9_]+", c))
+        # the refusal list itself is a single #if feeding an #error
+        refusal = set(re.findall(r"defined\((RPK_[A-Z0-9_]+)\)", src))
+        assert used - allowed <= refusal, (f, used - allowed - refusal)
+    src = os.path.join(PKG, "csrc", "rp_kernel.hip")
+    for macro in ("RPK_NT_STORE", "RPK_COLD_IN_SLAB", "RPK_NO_SPECULATIVE", "RPK_TRIES=3"):
+        r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-E", f"-D{macro}", src, "-o", os.devnull],
+                           capture_output=True, text=True)
+        assert r.returncode != 0 and "experiment macros" in r.stderr, macro
