@@ -5,7 +5,8 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one frame of the config (1920x1080x256 spp bunny scene with full materials by default),
-tile-sharded across the N ranks (tile t -> rank t % N, strong scaling: the frame is fixed), rendered by the
+tile-sharded across the N ranks (the balanced tile plan, RP_SHARD_BALANCED: tiles dealt by a probed cost; strong
+scaling: the frame is fixed), rendered by the
 persistent HIP kernel (librp.so) from scene data resident in HBM, followed by librp's frame gather
 (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
 xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
@@ -16,14 +17,18 @@ next (--inflight).  The timed region is K steps bracketed by a barrier + torch.c
 sides; the max over ranks is used.
 
 Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays / time.
-roofline: the render kernel's measured memory-side traffic per ray (rocprofv3 PMC record
-committed under profiles/, tools/roofline.py) x this launch's rays / the launch's duration measured with HIP
-events on its stream, against the 8 TB/s HBM peak; beside it the VALU-issue fraction from the same record's
-SQ counters (the bound of the cache-resident bunny configs) and, for reference, the rate the reference's
-own traversal would need (its event counts x SURVEY.md 8d bytes per event).  cpu_baseline: the CPU
-oracle's -O3 restatement of the reference driver (main.rs:36-106: LIFO tile queue, worker threads with
-their own StdRng) on a bounded sample of the same scene, at the reference's 4 workers and at 16, rank 0,
-N = 1 only.
+roofline: per ray of the render kernel, from the committed profile record of THIS build
+(profiles/current.json -> tools/roofline.py output, refused when its build id differs from rp_build_id()):
+  achieved = the kernel's algorithmic bytes (its own node visits x node bytes + primitive tests x 80 B + the
+             closest hit's records + texels + keystream, from the diagnostic build's counts) x this launch's rays /
+             the launch's duration (HIP events on its stream), against the 8 TB/s HBM peak;
+  traffic  = memory-side bytes of the launch from the PMC counters (2 x FETCH_SIZE + WRITE_SIZE, gfx950);
+  binding  = the larger of the VALU-issue fraction and the traffic fraction (what limits the kernel);
+and, for reference, the rate the reference's own traversal would need (its event counts x SURVEY.md 8d bytes
+per event).  cpu_baseline: the CPU oracle's -O3 restatement of the reference driver (main.rs:36-106: LIFO tile
+queue, worker threads with their own StdRng) on a bounded sample of the same scene, at the reference's 4 workers
+and at 16 (the box's CPU share per GPU), rank 0, N = 1 only; the full host is extrapolated from the 16-worker
+run, not run (the pool's rule: a GPU job sizes its worker pools to its 16-core share).
 """
 from __future__ import annotations
 
@@ -45,7 +50,8 @@ CLOCK_HZ = 2.4e9             # MI355X_MICROARCH.md max clock
 VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
 # SURVEY.md 8d algorithmic bytes per event of the REFERENCE traversal (reference tree, f64 layout)
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
-CPU_WORKERS = (4, 16)        # main.rs:27 num_workers = 4; 16 = the GPU box's CPU share per GPU
+# (workers, spp) of the CPU baseline runs, ~13 s each: main.rs:27 num_workers = 4; 16 = the GPU box's CPU share
+CPU_RUNS = ((4, 8), (16, 32))
 
 
 def log(*a):
@@ -106,8 +112,8 @@ def host_cpu():
             "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
-def cpu_baseline(config: str, spp: int, workers_list):
-    """The reference driver restated (oracle, -O3, no per-event counters): 1920x1080 at `spp`."""
+def cpu_baseline(config: str, runs_plan, spp_override: int = 0):
+    """The reference driver restated (oracle, -O3, no per-event counters): 1920x1080 at each run's spp."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     scene, params = scenes.config_scene(config)
@@ -115,20 +121,32 @@ def cpu_baseline(config: str, spp: int, workers_list):
     os_ = O.OracleScene(d.addr(), d, fast=True)
     cam = scene.camera.to_c()
     runs = []
-    for workers in workers_list:
+    for workers, spp in runs_plan:
+        spp = spp_override or spp
         secs, ctr, _ = os_.baseline(ctypes.addressof(cam), params.width, params.height, spp, params.max_bounce, 32,
                                     workers, params.seed)
-        runs.append({"workers": workers, "value": ctr["rays"] / secs / 1e6, "seconds": round(secs, 3),
+        runs.append({"workers": workers, "spp": spp, "value": ctr["rays"] / secs / 1e6, "seconds": round(secs, 3),
                      "rays": ctr["rays"]})
-        log(f"[rank 0] cpu baseline {workers} workers: {runs[-1]['value']:.2f} Mrays/s in {secs:.1f}s")
+        log(f"[rank 0] cpu baseline {workers} workers, {spp} spp: {runs[-1]['value']:.2f} Mrays/s in {secs:.1f}s")
     os_.close()
-    best = max(runs, key=lambda r: r["value"])
-    return {"value": best["value"], "unit": "Mrays/s", "cores": best["workers"], "kind": "port",
-            "sample": f"{config} scene {params.width}x{params.height}x{spp}spp (GPU runs {params.spp}spp); C "
-                      f"restatement (-O3, oracle/liboracle_fast.so) of main.rs:36-106: LIFO tile queue of 32x32 "
-                      f"tiles, one StdRng per worker; runs at {', '.join(str(w) for w in workers_list)} workers "
-                      f"(main.rs:27 default 4); value = the faster run; Rust reference unbuildable here",
-            "runs": runs, "host": host_cpu()}
+    host = host_cpu()
+    main = max(runs, key=lambda r: r["workers"])
+    out = {"value": main["value"], "unit": "Mrays/s", "cores": main["workers"], "kind": "port",
+           "sample": f"{config} scene {params.width}x{params.height} at {', '.join(str(r['spp']) for r in runs)} spp for "
+                     f"{', '.join(str(r['workers']) for r in runs)} workers (GPU runs {params.spp}spp); C restatement "
+                     f"(-O3, oracle/liboracle_fast.so) of main.rs:36-106: LIFO tile queue of 32x32 tiles, one StdRng "
+                     f"per worker (main.rs:27 default 4 workers); value = the {main['workers']}-worker run (the GPU "
+                     f"box's CPU share); Rust reference unbuildable here",
+           "runs": runs, "host": host}
+    phys = host.get("physical_cores")
+    if phys:
+        per = main["value"] / main["workers"]
+        out["full_host_extrapolated"] = {
+            "value": round(per * phys, 2), "cores": phys,
+            "basis": f"{main['workers']}-worker rate x {phys} physical cores / {main['workers']} (linear: 4 -> 16 "
+                     f"workers scaled {runs[-1]['value'] / runs[0]['value']:.2f}x for 4x); not run -- a GPU job on this "
+                     f"pool sizes its worker pools to its {main['workers']}-core share"}
+    return out
 
 
 def main():
@@ -138,14 +156,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
-    ap.add_argument("--cpu-spp", type=int, default=16)
+    ap.add_argument("--cpu-spp", type=int, default=0, help="override the CPU baseline runs' spp (0 = per run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 3 on several)")
     ap.add_argument("--shard-of", type=int, default=0,
-                    help="diagnostic, one GPU: render only shard 0 of this many (the per-rank work of an N-GPU "
+                    help="diagnostic, one GPU: render only shard --shard of this many (the per-rank work of an N-GPU "
                          "run), no gather; not a bench line")
+    ap.add_argument("--shard", type=int, default=0, help="with --shard-of: which shard")
+    ap.add_argument("--shard-map", default="auto", choices=("auto", "interleave", "balanced"),
+                    help="tile deal across ranks (rp_render_params.shard_map); auto = balanced for N > 1 or --shard-of")
     ap.add_argument("--opt", action="append", default=[],
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
@@ -177,7 +198,10 @@ def main():
     ds = DeviceScene(scene, device=local, options=options)
     info = ds.info()
     log(f"[rank {rank}] scene ready in {time.time() - t:.2f}s: {info}")
-    sp = shard_params(params, rank, world) if not args.shard_of else shard_params(params, 0, args.shard_of)
+    nsh = args.shard_of or world
+    smap = args.shard_map if args.shard_map != "auto" else ("balanced" if nsh > 1 else "interleave")
+    params = replace(params, shard_map=F.RP_SHARD_BALANCED if smap == "balanced" else F.RP_SHARD_INTERLEAVE)
+    sp = shard_params(params, rank, world) if not args.shard_of else shard_params(params, args.shard, args.shard_of)
     with stdout_to_stderr():
         comm = bootstrap_comm(rank, world, local)
     # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
@@ -246,8 +270,8 @@ def main():
         kernel_s = elapsed / args.steps
     cs = [c.cpu().tolist() for c in ctrs]
     bad = [c[3] for c in cs if c[3] != 0]
-    if bad:
-        raise RuntimeError(f"render kernel reported status {bad}")
+    if bad:  # RP_STATUS_* bits (OR-ed over the ranks by the gather): stack overflow, plan mismatch
+        raise RuntimeError(f"render kernel reported status {bad}: frame refused")
     rays_step, samples_step = cs[0][0], cs[0][1]  # summed over the ranks by rp_frame_gather
     tmax = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -256,24 +280,39 @@ def main():
     value = rays_step * args.steps / elapsed_max / 1e6
 
     if rank == 0:
-        local_rays = rays_step / world  # this rank's launch (shards are balanced by the tile interleave)
+        local_rays = rays_step / world  # this rank's launch (shards carry near-equal work under the balanced plan)
         rec = kernel_record(args.config) if args.spp == 0 else None
-        roof = {"bound": "valu" if args.config != "C5" else "hbm", "achieved": None, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": None, "traffic": None,
-                "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3)}
+        build = F.rp().rp_build_id().decode()
+        roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
+                "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3), "build_id": build}
+        if rec and rec.get("build_id") != build:
+            roof["stale_record"] = f"{rec['source']} was measured on build {rec.get('build_id')}; not used"
+            rec = None
         if rec:
             traffic = rec["traffic_bytes_per_ray"] * local_rays
-            achieved = traffic / kernel_s / 1e9
+            tr_gbs = traffic / kernel_s / 1e9
             issue = rec["valu_per_ray"] * local_rays / kernel_s
+            valu_frac = issue / VALU_ISSUE_PEAK
             roof.update({
-                "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": round(traffic),
-                "traffic_bytes_per_ray": round(rec["traffic_bytes_per_ray"], 1),
+                "traffic": round(traffic), "traffic_bytes_per_ray": round(rec["traffic_bytes_per_ray"], 1),
+                "traffic_GBps": round(tr_gbs, 1), "traffic_frac": round(tr_gbs / HBM_PEAK_GBS, 4),
                 "valu_issue": {"achieved": round(issue / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
-                               "unit": "Gwave-inst/s", "frac": round(issue / VALU_ISSUE_PEAK, 4),
+                               "unit": "Gwave-inst/s", "frac": round(valu_frac, 4),
                                "valu_per_ray": round(rec["valu_per_ray"], 2)},
                 "cycle_budget": rec.get("cycle_budget"),
-                "source": f"{rec['source']} (rocprofv3 PMC, build {rec.get('git')}; per-ray figures x this "
-                          f"launch's rays / its HIP-event duration)"})
+                "source": f"{rec['source']} (rocprofv3 PMC + diagnostic counts, build {rec.get('build_id')}; per-ray "
+                          f"figures x this launch's rays / its HIP-event duration)"})
+            alg = rec.get("algorithmic_bytes_per_ray")
+            if alg:
+                achieved = alg * local_rays / kernel_s / 1e9
+                roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                             "algorithmic_bytes_per_ray": round(alg, 1),
+                             "algorithmic_breakdown": rec.get("algorithmic_breakdown"),
+                             "traffic_over_algorithmic": round(rec["traffic_bytes_per_ray"] / alg, 4)})
+            bind = ("valu_issue", valu_frac) if valu_frac >= tr_gbs / HBM_PEAK_GBS else ("hbm_traffic", tr_gbs / HBM_PEAK_GBS)
+            roof["binding"] = {"resource": bind[0], "frac": round(bind[1], 4),
+                               "note": "the kernel is latency-bound (cycle_budget: waves wait on memory ~45 % of their "
+                                       "cycles); its algorithmic bytes are mostly served by L2 / Infinity Cache"}
         ref_bpr = reference_equivalent(args.config)
         roof["reference_equivalent"] = {
             "bytes_per_ray": round(ref_bpr, 1), "GBps": round(ref_bpr * local_rays / kernel_s / 1e9, 1),
@@ -291,16 +330,20 @@ def main():
                        "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
-                       "scene_options": options or "defaults",
-                       **({"simulated_shard": f"shard 0 of {args.shard_of}, no gather (diagnostic)"}
+                       "scene_options": options or "defaults", "shard_map": smap,
+                       **({"simulated_shard": f"shard {args.shard} of {args.shard_of}, no gather (diagnostic)"}
                           if args.shard_of else {})},
             "roofline": roof,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.shard_of:
             log("[rank 0] cpu baseline ...")
-            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_spp, CPU_WORKERS)
-            out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+            cb = cpu_baseline(args.config, CPU_RUNS, args.cpu_spp)
+            out["cpu_baseline"] = cb
+            ratios = {f"vs_{r['workers']}_workers": round(value / r["value"], 1) for r in cb["runs"]}
+            if "full_host_extrapolated" in cb:
+                ratios["vs_full_host_extrapolated"] = round(value / cb["full_host_extrapolated"]["value"], 1)
+            out["gpu_over_cpu"] = ratios
         print(json.dumps(out), flush=True)
     comm.close()
     ds.close()

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 4
+#define RP_ABI_VERSION 5
 
 /* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -57,8 +57,9 @@ extern "C" {
  * status}.  Nothing else is written through the pointer (the unit queue lives in the workspace). */
 #define RP_COUNTERS_LEN 4
 enum { RP_CTR_RAYS = 0, RP_CTR_SAMPLES = 1, RP_CTR_PIXELS = 2, RP_CTR_STATUS = 3 };
-/* status bits */
-#define RP_STATUS_STACK_OVERFLOW 1u
+/* status bits (OR-ed over the ranks of a frame gather, never summed) */
+#define RP_STATUS_STACK_OVERFLOW 1u  /* a lane's traversal stack overflowed (entries dropped: the frame is wrong) */
+#define RP_STATUS_PLAN_MISMATCH 2u   /* ranks of a balanced frame made different tile plans (frame invalid) */
 
 /* Bytes of an RCCL unique id (rp_comm_unique_id). */
 #define RP_COMM_ID_BYTES 128
@@ -170,8 +171,17 @@ typedef struct rp_camera {
 } rp_camera;
 
 /* One frame (or one shard of it).  The frame is cut into tile_w x tile_h tiles in row-major tile
- * order (image.rs:151-167); shard s of S renders tiles t with t % S == s (interleaved, balances sky
- * against bunny cost across GPUs). */
+ * order (image.rs:151-167), and the tiles are dealt to the S shards (GPUs) by shard_map:
+ *   RP_SHARD_INTERLEAVE: shard s renders tiles t with t % S == s, its k-th tile is t = s + k*S.
+ *   RP_SHARD_BALANCED: a tile plan deals them by cost.  The render of a shard first traces a cost probe of the
+ *     WHOLE frame (sample 0 of a lattice of pixels per tile, traversal work counted without any dependence on
+ *     the scheduling, so every rank measures the same costs) and deals the tiles, costliest first, in rounds of
+ *     S alternating direction; shard s's k-th tile is the deal order's entry s + k*S.  Every shard holds exactly
+ *     the interleave's number of tiles (same buffer sizes and gather strides), and every rank computes the same
+ *     plan (the frame gather compares their hashes: RP_STATUS_PLAN_MISMATCH).  The plan lives in the workspace of
+ *     the render; rp_workspace_tile_map returns it.  Frames of more than 16384 tiles are dealt as the interleave.
+ * Neither choice changes a pixel (per-pixel seeding): only which GPU renders it. */
+enum { RP_SHARD_INTERLEAVE = 0, RP_SHARD_BALANCED = 1 };
 typedef struct rp_render_params {
   uint32_t width, height;   /* Multisampler {width, height} */
   uint32_t spp;             /* Multisampler {num_samples} */
@@ -181,7 +191,7 @@ typedef struct rp_render_params {
   uint32_t shard, num_shards;/* num_shards 0 -> 1 */
   uint32_t samples_per_stream; /* RNG contract batch size N, 0 -> RP_SAMPLES_PER_STREAM; N >= spp: one
                                   stream per pixel */
-  uint32_t reserved;        /* 0 */
+  uint32_t shard_map;       /* RP_SHARD_INTERLEAVE (0) or RP_SHARD_BALANCED */
 } rp_render_params;
 
 /* Scene build and kernel tuning options (rp_scene_create_ex).  None of them changes an image beyond
@@ -226,6 +236,9 @@ typedef struct rp_scene_options {
                                16 above; 1..64) */
   uint32_t unit_queues;     /* RP_QUEUES_*: how the render blocks share out the units */
   uint32_t queue_chunk;     /* XCD_TILES: consecutive tiles of the order dealt to one queue at a time (0 -> 1) */
+  uint32_t debug_stack_depth; /* TESTS ONLY (0 = off): traversal-stack entries per lane, 8..4096, instead of the
+                               depth the tree needs.  Too small a stack drops entries -- wrong frames -- and the
+                               render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */
 } rp_scene_options;
 
 typedef struct rp_stats {
@@ -238,8 +251,10 @@ typedef struct rp_stats {
 typedef struct rp_scene rp_scene;   /* opaque: device-resident scene + acceleration structure */
 typedef struct rp_workspace rp_workspace;  /* opaque: per-frame device state of a render (see below) */
 
-/* Library / device queries. */
+/* Library / device queries.  rp_build_id: a hash of the render kernel's sources this library was built from
+ * (profile records of the kernel carry it; a record of another build is stale). */
 int rp_abi_version(void);
+const char* rp_build_id(void);
 const char* rp_last_error(void);
 int rp_device_count(int* count);
 
@@ -256,10 +271,14 @@ int rp_scene_info(const rp_scene* scene, uint64_t* n_nodes, uint64_t* n_leaves, 
 
 /* Number of pixels in shard params->shard (the length of the compact shard buffer). */
 int rp_shard_pixel_count(const rp_render_params* params, uint64_t* count);
-/* Scatter a compact shard buffer (shard order: its tiles in increasing tile index, row-major inside a
- * tile) into a full frame; `channels` values per pixel. */
+/* Scatter a compact shard buffer (shard order: its tiles in deal order k = 0, 1, ..., row-major inside a
+ * tile) into a full frame; `channels` values per pixel.  RP_SHARD_INTERLEAVE frames only (a balanced frame is
+ * refused with RP_EINVAL): rp_shard_unpack_map takes the deal order of a balanced frame (rp_workspace_tile_map;
+ * NULL = the interleave). */
 int rp_shard_unpack(const rp_render_params* params, const double* shard_buf, uint32_t channels,
                     double* frame);
+int rp_shard_unpack_map(const rp_render_params* params, const uint32_t* tile_map, const double* shard_buf,
+                        uint32_t channels, double* frame);
 
 /* Render synchronously into host memory.  out_rgb: width*height*3 doubles (only the shard's pixels are
  * written).  out_foreground (nullable): width*height floats, fraction of samples whose first ray hit
@@ -295,6 +314,11 @@ int rp_render_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camer
  * uses for this frame size.  Synchronous (allocates; may free a smaller reservation); idempotent for a
  * shape it already covers.  rp_render reserves for itself. */
 int rp_workspace_reserve(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params);
+/* The deal order of params' frame (one entry per frame tile; shard s's k-th tile is tile_map[s + k*num_shards]):
+ * for RP_SHARD_BALANCED the plan the last render of this frame in `workspace` (NULL = the scene's) made, for the
+ * interleave 0, 1, 2, ...  n >= the frame's tile count.  Synchronises the device. */
+int rp_workspace_tile_map(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                          uint32_t* tile_map, uint32_t n);
 
 /* Output stage on the device: the reference's to_srgb_u8 (utility.rs:212-220, alpha 255) of every slot of
  * a compact shard buffer, bytes in tga::save's pixel order B, G, R, A (image.rs:116-137), so a gathered
@@ -321,9 +345,9 @@ int rp_intersect(rp_scene* scene, const double* rays, uint64_t n, double* out_hi
 int rp_diagnostics(rp_scene* scene, uint64_t* out, uint32_t n, int reset);
 
 /* ---------------------------------------------------------------- multi-GPU -- */
-/* Image tiles are interleaved across the GPUs (tile t -> rank t % nranks, params.shard = rank), every
- * GPU holds its own copy of the scene, and one RCCL all-gather over xGMI per frame moves the shards;
- * each rank then de-interleaves them into frame order on its device.  This replaces the reference's
+/* Image tiles are dealt across the GPUs (params.shard = rank, params.shard_map: the interleave tile t -> rank
+ * t % nranks, or the balanced plan), every GPU holds its own copy of the scene, and one RCCL all-gather over xGMI
+ * per frame moves the shards; each rank then de-interleaves them into frame order on its device.  This replaces the reference's
  * thread tile queue (main.rs:36-106, num_workers main.rs:27).  The per-pixel RNG contract makes the
  * gathered frame bitwise identical for any number of GPUs. */
 typedef struct rp_comm rp_comm;     /* opaque: one rank's RCCL communicator (one device) */
@@ -338,11 +362,16 @@ int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
 
 /* Collective over all ranks of `comm`, asynchronous on `stream` (every rank must call it, in the same
  * order relative to its other collectives on comm).  params: this rank's shard (shard = rank, num_shards
- * = nranks), the workspace reserved for it (rp_workspace_reserve).  d_shard_rgb: the rank's finished
- * shard (rp_render_device_ws output).  Outputs (either nullable, on the rank's device, frame order, row 0
- * = bottom): d_frame_bgra width*height*4 bytes = to_srgb_u8 in tga::save byte order (rp_shard_to_bgra8)
- * -- the body of output.tga; d_frame_rgb width*height*3 linear f64.  d_counters (nullable): the rank's
- * RP_COUNTERS_LEN counters, summed over the ranks in place. */
+ * = nranks), the workspace reserved for it (rp_workspace_reserve) -- for RP_SHARD_BALANCED the workspace that
+ * rendered the shard (it holds the plan).  d_shard_rgb: the rank's finished shard (rp_render_device_ws output).
+ * Outputs (either nullable, on the rank's device, frame order, row 0 = bottom): d_frame_bgra width*height*4
+ * bytes = to_srgb_u8 in tga::save byte order (rp_shard_to_bgra8) -- the body of output.tga; d_frame_rgb
+ * width*height*3 linear f64.  Every rank must pass the same NULL / non-NULL combination of d_frame_bgra and
+ * d_frame_rgb: the collectives issued are, in this order, an all-gather of every rank's counter block (always),
+ * of the BGRA8 shards (d_frame_bgra) and of the f64 shards (d_frame_rgb).  d_counters (nullable): the rank's
+ * RP_COUNTERS_LEN counters in, the frame's out -- rays, samples and pixels summed over the ranks, status bits
+ * OR-ed over them, plus RP_STATUS_PLAN_MISMATCH when the ranks' balanced plans differ.  A caller that does not
+ * pass counters does not learn the status. */
 int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                     const double* d_shard_rgb, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, void* stream);
@@ -352,8 +381,12 @@ int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, con
  * per slot (1 for the BGRA8 bytes of rp_shard_to_bgra8, 6 for f64 RGB); d_frame receives width*height
  * slots in frame order.  Asynchronous on `stream`, on the current device. */
 int rp_gather_stride(const rp_render_params* params, uint64_t* stride);
+/* RP_SHARD_INTERLEAVE frames; a balanced frame is refused (RP_EINVAL): rp_frame_assemble_ws assembles with the
+ * plan held by the workspace that rendered this rank's shard of the frame. */
 int rp_frame_assemble(const rp_render_params* params, const void* d_gathered, uint32_t words_per_slot,
                       void* d_frame, void* stream);
+int rp_frame_assemble_ws(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                         const void* d_gathered, uint32_t words_per_slot, void* d_frame, void* stream);
 
 /* rp_render_device_ws into the workspace's shard buffer, then rp_frame_gather, on one stream. */
 int rp_render_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
@@ -366,9 +399,10 @@ int rp_multi_create(const rp_scene_desc* desc, const int* devices, int n_devices
                     rp_multi** out);
 void rp_multi_destroy(rp_multi* multi);
 /* Synchronous frame on every device of `multi` (params.shard / num_shards are ignored: device k renders
- * shard k of n_devices).  out_rgb (nullable): width*height*3 doubles on the host, frame order; out_bgra
- * (nullable): width*height*4 bytes (to_srgb_u8, tga::save order).  stats (nullable): summed counters,
- * seconds = wall time of the frame. */
+ * shard k of n_devices; params.shard_map applies -- RP_SHARD_BALANCED is the better split).  out_rgb
+ * (nullable): width*height*3 doubles on the host, frame order; out_bgra (nullable): width*height*4 bytes
+ * (to_srgb_u8, tga::save order).  stats (nullable): summed counters, seconds = wall time of the frame.  Returns
+ * RP_EINTERNAL when any device reported a status bit (stack overflow, plan mismatch). */
 int rp_render_multi(rp_multi* multi, const rp_camera* camera, const rp_render_params* params,
                     double* out_rgb, uint8_t* out_bgra, rp_stats* stats);
 

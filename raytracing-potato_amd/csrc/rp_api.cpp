@@ -23,7 +23,8 @@
 
 static_assert(rpk::CTR_N == RP_COUNTERS_LEN, "kernel counter block = the ABI's");
 static_assert(rpk::CTR_RAYS == RP_CTR_RAYS && rpk::CTR_STATUS == RP_CTR_STATUS, "counter order");
-static_assert(rpk::STATUS_STACK_OVERFLOW == RP_STATUS_STACK_OVERFLOW, "status bits");
+static_assert(rpk::STATUS_STACK_OVERFLOW == RP_STATUS_STACK_OVERFLOW && rpk::STATUS_PLAN_MISMATCH == RP_STATUS_PLAN_MISMATCH,
+              "status bits");
 static_assert(sizeof(ncclUniqueId) == RP_COMM_ID_BYTES, "RCCL unique id size");
 static_assert(sizeof(rp_render_params) == 48, "rp_render_params layout (bindings mirror it)");
 
@@ -108,6 +109,14 @@ struct rp_workspace {
   uint32_t* d_gather_bgra = nullptr; //   all ranks' bytes (nranks x stride words)
   uint64_t gs_slots = 0;             // capacity of d_gs_* in slots
   uint64_t gather_slots = 0;         // capacity of d_gather_* in slots (over all ranks)
+  uint64_t* d_ctr_send = nullptr;    // this rank's counter block of a frame gather (rpk::GATHER_CTR words)
+  uint64_t* d_ctr_gather = nullptr;  // every rank's block (ctr_ranks x rpk::GATHER_CTR)
+  uint32_t ctr_ranks = 0;
+  // the balanced tile plan (RP_SHARD_BALANCED) of the last frame rendered with this workspace: the deal order,
+  // its inverse and its hash (rpk::launch_tile_plan), and the frame geometry it was made for
+  uint32_t* d_plan = nullptr;
+  bool plan_on = false;
+  uint32_t plan_geom[5] = {0, 0, 0, 0, 0};  // width, height, tile_w, tile_h, num_shards
   rpk::WfBuffers wf{};               // the stage-split engine's path-slot pool (engine = wavefront only)
 };
 
@@ -160,7 +169,7 @@ void ws_release(rp_workspace* w) {
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
-                  (void*)w->d_gather_bgra})
+                  (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan})
     dfree(p);
   *w = rp_workspace{};
 }
@@ -173,6 +182,7 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
   const uint64_t lanes = s->lanes();
   if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, rpk::QUEUE_WORDS) ||
       !dalloc(&w->d_tile_cost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_tile_order, rpk::TILE_SORT_MAX) ||
+      !dalloc(&w->d_plan, 2 * rpk::TILE_SORT_MAX + 2) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
     ws_release(w);
@@ -201,6 +211,7 @@ struct Tiling {
   uint32_t tw, th, shards, shard, tiles_x, tiles_y, n_tiles, n_shard_tiles;
   uint64_t n_slots;
   uint32_t sps, nbatch;  // RNG contract: samples per stream, batches per pixel
+  bool balanced;         // RP_SHARD_BALANCED in effect: the tiles are dealt by a plan (frames of <= TILE_SORT_MAX tiles)
 };
 
 int make_tiling(const rp_render_params* p, Tiling& t) {
@@ -221,7 +232,32 @@ int make_tiling(const rp_render_params* p, Tiling& t) {
   if (t.n_slots >= 0xffffffffull) return fail(RP_EINVAL, "shard too large (>= 2^32 pixel slots)");
   t.sps = p->samples_per_stream ? p->samples_per_stream : RP_SAMPLES_PER_STREAM;
   t.nbatch = p->spp ? (uint32_t)(((uint64_t)p->spp + t.sps - 1) / t.sps) : 0;
+  if (p->shard_map > RP_SHARD_BALANCED) return fail(RP_EINVAL, "shard_map must be RP_SHARD_INTERLEAVE or RP_SHARD_BALANCED");
+  t.balanced = p->shard_map == RP_SHARD_BALANCED && t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX;
   return RP_OK;
+}
+
+// Scatter a compact shard buffer into a frame on the host (rp_shard_unpack), tiles dealt by `map` (the deal order
+// of a balanced plan) or the interleave (map NULL).
+void unpack_host(const rp_render_params* p, const Tiling& t, const uint32_t* map, const void* shard_buf, size_t elem,
+                 uint32_t channels, void* frame) {
+  const uint64_t tile_px = (uint64_t)t.tw * t.th;
+  const char* src = static_cast<const char*>(shard_buf);
+  char* dst = static_cast<char*>(frame);
+  for (uint32_t k = 0; k < t.n_shard_tiles; k++) {
+    const uint32_t dk = t.shard + k * t.shards, tile = map ? map[dk] : dk;
+    const uint32_t ox = (tile % t.tiles_x) * t.tw, oy = (tile / t.tiles_x) * t.th;
+    for (uint32_t lj = 0; lj < t.th && oy + lj < p->height; lj++)
+      for (uint32_t li = 0; li < t.tw && ox + li < p->width; li++)
+        std::memcpy(dst + ((uint64_t)(oy + lj) * p->width + ox + li) * channels * elem,
+                    src + (k * tile_px + (uint64_t)lj * t.tw + li) * channels * elem, channels * elem);
+  }
+}
+
+// The workspace's plan applies to frames of params' geometry (the render of this frame's shard made it).
+bool plan_matches(const rp_workspace* w, const rp_render_params* p, const Tiling& t) {
+  return w->plan_on && w->plan_geom[0] == p->width && w->plan_geom[1] == p->height && w->plan_geom[2] == t.tw &&
+         w->plan_geom[3] == t.th && w->plan_geom[4] == t.shards;
 }
 
 // to_srgb_u8's byte for one channel (utility.rs:212-216), in the host libm: the reference's arithmetic
@@ -268,6 +304,7 @@ rp_scene_options default_options() {
   o.probe_n = rpk::PROBE_LATTICE_N;
   o.engine = RP_ENGINE_MEGAKERNEL;
   o.wf_slots = 2;
+  o.debug_stack_depth = 0;
   return o;
 }
 
@@ -292,6 +329,8 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.leaf_break > 64) return fail(RP_EINVAL, "options.leaf_break must be 0..64");
   if (o.unit_queues > RP_QUEUES_XCD_REGIONS) return fail(RP_EINVAL, "options.unit_queues must be RP_QUEUES_*");
   if (o.queue_chunk > 4096) return fail(RP_EINVAL, "options.queue_chunk must be 0..4096");
+  if (o.debug_stack_depth != 0 && (o.debug_stack_depth < 8 || o.debug_stack_depth > 4096))
+    return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
   return RP_OK;
 }
 
@@ -329,6 +368,15 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
     if ((rc = grow(w->d_gs_rgb, w->d_gs_bgra, w->gs_slots, stride, 3, 1, "gather staging"))) return rc;
     if ((rc = grow(w->d_gather_rgb, w->d_gather_bgra, w->gather_slots, stride * t.shards, 3, 1, "gather buffers")))
       return rc;
+    if (t.shards > w->ctr_ranks) {
+      dfree(w->d_ctr_send);
+      dfree(w->d_ctr_gather);
+      w->d_ctr_send = w->d_ctr_gather = nullptr;
+      w->ctr_ranks = 0;
+      if (!dalloc(&w->d_ctr_send, rpk::GATHER_CTR) || !dalloc(&w->d_ctr_gather, (uint64_t)rpk::GATHER_CTR * t.shards))
+        return fail(RP_ENOMEM, "hipMalloc gather counters");
+      w->ctr_ranks = t.shards;
+    }
   }
   return RP_OK;
 }
@@ -452,6 +500,9 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   if (node_format == rpl::NODES_W8) s->ks.stack_depth = 4 * (ps.max_depth + 1) + 3;
   // floor of 17 entries: the spill split below never keeps fewer in LDS (options.lds_depth tests force 17)
   if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
+  // test-only: a stack too small for the tree (the kernels flag RP_STATUS_STACK_OVERFLOW, never write past it)
+  const bool debug_stack = opt.debug_stack_depth != 0;
+  if (debug_stack) s->ks.stack_depth = opt.debug_stack_depth;
   s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
@@ -476,14 +527,14 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   int bpc = 0;
   if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   int bpc_spill = 0;
-  if (rpk::render_blocks_per_cu(17, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
+  if (!debug_stack && rpk::render_blocks_per_cu(17, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
     uint32_t L = s->ks.stack_depth - 1;
     int b = 0;
     while (L > 17 && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
     s->ks.lds_depth = L;
     bpc = bpc_spill;
   }
-  if (opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
+  if (!debug_stack && opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
     s->ks.lds_depth = opt.lds_depth;
     if (rpk::render_blocks_per_cu(opt.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   }
@@ -564,39 +615,71 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     return (int)std::max<uint64_t>(1, std::min(want, resident));
   };
   RP_HIP(hipMemsetAsync(w->d_queue, 0, sizeof(uint32_t) * rpk::QUEUE_WORDS, st));
-  const rpk::TileGeom tg{t.tiles_x, kp.shard, kp.nshards};
   const uint32_t tiles_y = t.tiles_y;
   uint32_t order_mode = s->opt.tile_order;
   if (order_mode == RP_TILES_AUTO) order_mode = s->tiles_auto;
-  // both sorts key the tiles by their Z-order code (frame grids up to 256 x 256 tiles; larger ones keep shard
-  // order)
-  const bool sortable = t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX && t.tiles_x <= 256 &&
-                        tiles_y <= 256;
-  if (order_mode == RP_TILES_MORTON && sortable) {
-    int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
-    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
-    kp.tile_order = w->d_tile_order;
-  }
-  if (order_mode == RP_TILES_COST && sortable) {
-    // probe sample 0 of an n x n lattice of pixels per tile, then sort the tiles by cost (same stream,
-    // no host sync)
+  // The cost probe: sample 0 of an n x n lattice of pixels per tile traced by the probe instantiation of the
+  // render kernel, which adds up per tile the traversal work and shaded rays (summed and costliest sample) --
+  // over the shard's tiles, or over the whole frame for a balanced plan (same stream, no host sync).
+  auto probe = [&](uint32_t shard, uint32_t nshards, uint32_t n_tiles, uint32_t lattice, uint32_t& probe_px) -> int {
     rpk::KParams pk = kp;
     pk.probe = 1;
     pk.spp = 1;
-    pk.probe_n = std::min(s->opt.probe_n, std::min(t.tw, t.th));
+    pk.shard = shard;
+    pk.nshards = nshards;
+    pk.n_shard_tiles = n_tiles;
+    pk.probe_n = std::min(lattice, std::min(t.tw, t.th));
     pk.probe_px = pk.probe_n * pk.probe_n;
-    pk.n_slots = (uint64_t)t.n_shard_tiles * pk.probe_px;
+    pk.n_slots = (uint64_t)n_tiles * pk.probe_px;
     pk.nbatch = 1;
     pk.spp_batch = 1;
     pk.n_queue = pk.n_slots;
     pk.queue_groups = 1;
     pk.queue_chunk = 1;
     pk.tile_cost = w->d_tile_cost;
+    pk.tile_order = nullptr;
+    pk.tile_map = nullptr;
+    probe_px = pk.probe_px;
     RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
     RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
     int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + rpk::QUEUE_PROBE, grid_for(pk.n_slots), stream);
     if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
-    e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, pk.probe_px, tg, w->d_tile_order, stream);
+    return RP_OK;
+  };
+  // both sorts key the tiles by their Z-order code (frame grids up to 256 x 256 tiles; larger ones keep shard
+  // order)
+  const bool sortable = t.n_shard_tiles > 1 && t.n_shard_tiles <= rpk::TILE_SORT_MAX && t.tiles_x <= 256 &&
+                        tiles_y <= 256;
+  rpk::TileGeom tg{t.tiles_x, kp.shard, kp.nshards, nullptr, 0, 0};
+  uint32_t probe_px = 0;
+  bool frame_costs = false;
+  w->plan_on = false;
+  if (t.balanced) {
+    // RP_SHARD_BALANCED: probe the whole frame (deterministic costs, rp_device.h trav_step COUNT), and deal its tiles
+    // to the ranks by cost (rpk::launch_tile_plan) -- every rank computes the same plan from the same probe.  Scenes
+    // past the Infinity Cache (Z-order tiles, no cost order inside the shard) probe a sparser 4 x 4 lattice.
+    const uint32_t lattice = order_mode == RP_TILES_COST ? s->opt.probe_n : std::min(s->opt.probe_n, 4u);
+    if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
+    int e = rpk::launch_tile_plan(w->d_tile_cost, t.n_tiles, t.shards, w->d_plan, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("tile plan launch: ") + hipGetErrorString((hipError_t)e));
+    kp.tile_map = w->d_plan;
+    tg.map = w->d_plan;
+    tg.map_tiles = t.n_tiles;
+    frame_costs = true;
+    w->plan_on = true;
+    const uint32_t geom[5] = {p->width, p->height, t.tw, t.th, t.shards};
+    std::memcpy(w->plan_geom, geom, sizeof geom);
+  }
+  if (order_mode == RP_TILES_MORTON && sortable) {
+    int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
+    if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
+    kp.tile_order = w->d_tile_order;
+  }
+  if (order_mode == RP_TILES_COST && sortable) {
+    // the shard's tiles by cost: from the frame probe of a balanced plan, else a probe of the shard
+    if (!frame_costs && (rc = probe(kp.shard, kp.nshards, t.n_shard_tiles, s->opt.probe_n, probe_px))) return rc;
+    tg.cost_by_tile = frame_costs ? 1u : 0u;
+    int e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, probe_px, tg, w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
@@ -619,6 +702,7 @@ struct GatherPlan {
   Tiling t;
   uint64_t stride;  // slots per rank buffer
   rpk::FrameGeom geom;
+  const uint32_t* plan_hash;  // the workspace's plan hash (balanced frames), NULL = interleave
 };
 
 int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_render_params* p, GatherPlan& gp) {
@@ -628,7 +712,7 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   if ((int)gp.t.shards != nranks || (int)gp.t.shard != rank)
     return fail(RP_EINVAL, "params.shard / num_shards must be the communicator's rank / size");
   gp.stride = stage_slots(gp.t);
-  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots)
+  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || (uint32_t)nranks > w->ctr_ranks)
     return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
   gp.geom.W = p->width;
   gp.geom.H = p->height;
@@ -637,14 +721,25 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   gp.geom.tiles_x = gp.t.tiles_x;
   gp.geom.nranks = (uint32_t)nranks;
   gp.geom.stride = gp.stride;
+  gp.geom.tile_pos = nullptr;
+  gp.plan_hash = nullptr;
+  if (gp.t.balanced) {
+    if (!plan_matches(w, p, gp.t))
+      return fail(RP_EINVAL, "balanced frame: render this rank's shard with the same workspace before gathering it");
+    gp.geom.tile_pos = w->d_plan + gp.t.n_tiles;
+    gp.plan_hash = w->d_plan + 2 * gp.t.n_tiles;
+  }
   return RP_OK;
 }
 
+// (1) this rank's part: its counter block for the counter all-gather, its to_srgb_u8 bytes and/or a padded f64 copy
 int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const double* d_shard_rgb, bool bgra, bool rgb,
-                 hipStream_t st) {
+                 const uint64_t* d_counters, hipStream_t st) {
   DeviceGuard g(s->device);
+  int e = rpk::launch_counters_stage(d_counters, gp.plan_hash, w->d_ctr_send, st);
+  if (e != 0) return fail(RP_EHIP, std::string("counter stage launch: ") + hipGetErrorString((hipError_t)e));
   if (bgra && gp.t.n_slots) {
-    int e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_gs_bgra), st);
+    e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_gs_bgra), st);
     if (e != 0) return fail(RP_EHIP, std::string("output stage launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (rgb && gp.t.n_slots && d_shard_rgb != w->d_gs_rgb)
@@ -652,24 +747,29 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
   return RP_OK;
 }
 
-int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb,
-                       uint64_t* d_counters, hipStream_t st) {
+// (2) the collectives, in a fixed sequence: the counter blocks are always all-gathered (status bits must be OR-ed,
+// not summed: an even number of ranks with the same bit set would clear it -- and the plan hashes compared), then
+// the BGRA8 and/or f64 shards (rp.h: every rank passes the same NULL / non-NULL outputs)
+int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb, hipStream_t st) {
+  RP_NCCL(ncclAllGather(w->d_ctr_send, w->d_ctr_gather, rpk::GATHER_CTR, ncclUint64, comm, st));
   if (bgra) RP_NCCL(ncclAllGather(w->d_gs_bgra, w->d_gather_bgra, gp.stride, ncclUint32, comm, st));
   if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
-  if (d_counters) RP_NCCL(ncclAllReduce(d_counters, d_counters, RP_COUNTERS_LEN, ncclUint64, ncclSum, comm, st));
   return RP_OK;
 }
 
+// (3) counters reduced (sums, status OR), shards de-interleaved into frame order
 int gather_assemble(rp_scene* s, rp_workspace* w, const GatherPlan& gp, uint8_t* d_frame_bgra, double* d_frame_rgb,
-                    hipStream_t st) {
+                    uint64_t* d_counters, hipStream_t st) {
   DeviceGuard g(s->device);
+  int e = rpk::launch_counters_reduce(w->d_ctr_gather, gp.geom.nranks, d_counters ? d_counters : w->d_ctr, st);
+  if (e != 0) return fail(RP_EHIP, std::string("counter reduce launch: ") + hipGetErrorString((hipError_t)e));
   if (d_frame_bgra) {
-    int e = rpk::launch_frame_assemble(gp.geom, w->d_gather_bgra, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
+    e = rpk::launch_frame_assemble(gp.geom, w->d_gather_bgra, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
     if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (d_frame_rgb) {
-    int e = rpk::launch_frame_assemble(gp.geom, reinterpret_cast<const uint32_t*>(w->d_gather_rgb), 6,
-                                       reinterpret_cast<uint32_t*>(d_frame_rgb), st);
+    e = rpk::launch_frame_assemble(gp.geom, reinterpret_cast<const uint32_t*>(w->d_gather_rgb), 6,
+                                   reinterpret_cast<uint32_t*>(d_frame_rgb), st);
     if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
   }
   return RP_OK;
@@ -699,6 +799,11 @@ int rp_shard_to_bgra8(rp_scene* s, const rp_render_params* p, const double* d_sh
 }
 
 int rp_abi_version(void) { return RP_ABI_VERSION; }
+
+#ifndef RP_BUILD_ID
+#define RP_BUILD_ID "unknown"
+#endif
+const char* rp_build_id(void) { return RP_BUILD_ID; }
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 
@@ -763,22 +868,44 @@ int rp_shard_unpack(const rp_render_params* p, const double* shard_buf, uint32_t
   int rc = make_tiling(p, t);
   if (rc) return rc;
   if (!shard_buf || !frame || channels == 0) return fail(RP_EINVAL, "NULL buffer or zero channels");
-  const uint64_t tile_px = (uint64_t)t.tw * t.th;
-  for (uint32_t k = 0; k < t.n_shard_tiles; k++) {
-    uint32_t tile = t.shard + k * t.shards;
-    uint32_t ox = (tile % t.tiles_x) * t.tw, oy = (tile / t.tiles_x) * t.th;
-    for (uint32_t lj = 0; lj < t.th; lj++) {
-      uint32_t j = oy + lj;
-      if (j >= p->height) break;
-      for (uint32_t li = 0; li < t.tw; li++) {
-        uint32_t i = ox + li;
-        if (i >= p->width) break;
-        const double* src = shard_buf + (k * tile_px + (uint64_t)lj * t.tw + li) * channels;
-        double* dst = frame + ((uint64_t)j * p->width + i) * channels;
-        for (uint32_t c = 0; c < channels; c++) dst[c] = src[c];
-      }
+  if (t.balanced) return fail(RP_EINVAL, "balanced frame: unpack with rp_shard_unpack_map and rp_workspace_tile_map");
+  unpack_host(p, t, nullptr, shard_buf, sizeof(double), channels, frame);
+  return RP_OK;
+}
+
+int rp_shard_unpack_map(const rp_render_params* p, const uint32_t* tile_map, const double* shard_buf, uint32_t channels,
+                        double* frame) {
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!shard_buf || !frame || channels == 0) return fail(RP_EINVAL, "NULL buffer or zero channels");
+  if (tile_map) {
+    std::vector<uint8_t> seen(t.n_tiles, 0);
+    for (uint32_t i = 0; i < t.n_tiles; i++) {
+      if (tile_map[i] >= t.n_tiles || seen[tile_map[i]]) return fail(RP_EINVAL, "tile_map is not a permutation of the frame's tiles");
+      seen[tile_map[i]] = 1;
     }
   }
+  unpack_host(p, t, tile_map, shard_buf, sizeof(double), channels, frame);
+  return RP_OK;
+}
+
+int rp_workspace_tile_map(rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t* tile_map, uint32_t n) {
+  if (!s || !tile_map) return fail(RP_EINVAL, "scene and tile_map must be non-NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (n < t.n_tiles) return fail(RP_EINVAL, "tile_map holds fewer entries than the frame has tiles");
+  if (!t.balanced) {
+    for (uint32_t i = 0; i < t.n_tiles; i++) tile_map[i] = i;
+    return RP_OK;
+  }
+  if (!plan_matches(w, p, t)) return fail(RP_EINVAL, "no balanced plan for this frame in the workspace: render it first");
+  DeviceGuard g(s->device);
+  RP_HIP(hipDeviceSynchronize());
+  RP_HIP(hipMemcpy(tile_map, w->d_plan, sizeof(uint32_t) * t.n_tiles, hipMemcpyDeviceToHost));
   return RP_OK;
 }
 
@@ -873,17 +1000,13 @@ int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, doub
   if (result) return result;
   if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
   if (t.n_slots) {
-    rp_shard_unpack(p, shard.data(), 3, out_rgb);
-    if (out_fg) {
-      const uint64_t tile_px = (uint64_t)t.tw * t.th;
-      for (uint32_t k = 0; k < t.n_shard_tiles; k++) {
-        uint32_t tile = t.shard + k * t.shards;
-        uint32_t ox = (tile % t.tiles_x) * t.tw, oy = (tile / t.tiles_x) * t.th;
-        for (uint32_t lj = 0; lj < t.th && oy + lj < p->height; lj++)
-          for (uint32_t li = 0; li < t.tw && ox + li < p->width; li++)
-            out_fg[(uint64_t)(oy + lj) * p->width + ox + li] = shard_fg[k * tile_px + (uint64_t)lj * t.tw + li];
-      }
+    std::vector<uint32_t> map;
+    if (t.balanced) {
+      map.resize(t.n_tiles);
+      if ((result = rp_workspace_tile_map(s, &s->ws0, p, map.data(), t.n_tiles))) return result;
     }
+    unpack_host(p, t, t.balanced ? map.data() : nullptr, shard.data(), sizeof(double), 3, out_rgb);
+    if (out_fg) unpack_host(p, t, t.balanced ? map.data() : nullptr, shard_fg.data(), sizeof(float), 1, out_fg);
   }
   if (stats) {
     stats->rays = ctr[rpk::CTR_RAYS];
@@ -957,7 +1080,29 @@ int rp_frame_assemble(const rp_render_params* p, const void* d_gathered, uint32_
   int rc = make_tiling(p, t);
   if (rc) return rc;
   if (!d_gathered || !d_frame || words == 0) return fail(RP_EINVAL, "NULL buffer or zero words per slot");
-  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t)};
+  if (t.balanced) return fail(RP_EINVAL, "balanced frame: assemble with rp_frame_assemble_ws (the workspace holds the plan)");
+  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), nullptr};
+  int e = rpk::launch_frame_assemble(g, static_cast<const uint32_t*>(d_gathered), words, static_cast<uint32_t*>(d_frame),
+                                     stream);
+  if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
+  return RP_OK;
+}
+
+int rp_frame_assemble_ws(rp_scene* s, rp_workspace* w, const rp_render_params* p, const void* d_gathered,
+                         uint32_t words, void* d_frame, void* stream) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (!d_gathered || !d_frame || words == 0) return fail(RP_EINVAL, "NULL buffer or zero words per slot");
+  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), nullptr};
+  if (t.balanced) {
+    if (!plan_matches(w, p, t)) return fail(RP_EINVAL, "no balanced plan for this frame in the workspace: render it first");
+    g.tile_pos = w->d_plan + t.n_tiles;
+  }
+  DeviceGuard dg(s->device);
   int e = rpk::launch_frame_assemble(g, static_cast<const uint32_t*>(d_gathered), words, static_cast<uint32_t*>(d_frame),
                                      stream);
   if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
@@ -1022,18 +1167,21 @@ int rp_frame_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_pa
   hipStream_t st = (hipStream_t)stream;
   const bool bgra = d_frame_bgra != nullptr, rgb = d_frame_rgb != nullptr;
   DeviceGuard g(s->device);
-  if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, rgb, st))) return rc;
-  if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, d_counters, st))) return rc;
-  return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, st);
+  if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, rgb, d_counters, st))) return rc;
+  if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, st))) return rc;
+  return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, d_counters, st);
 }
 
 int rp_render_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,
                      uint8_t* d_frame_bgra, double* d_frame_rgb, uint64_t* d_counters, void* stream) {
   if (!c || !s) return fail(RP_EINVAL, "comm and scene must be non-NULL");
   if (!w) w = &s->ws0;
-  GatherPlan gp;
-  int rc = gather_plan(s, w, c->nranks, c->rank, p, gp);
+  Tiling t;
+  int rc = make_tiling(p, t);
   if (rc) return rc;
+  if ((int)t.shards != c->nranks || (int)t.shard != c->rank)
+    return fail(RP_EINVAL, "params.shard / num_shards must be the communicator's rank / size");
+  if (stage_slots(t) > w->gs_slots) return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
   if ((rc = render_shard(s, w, cam, p, w->d_gs_rgb, nullptr, d_counters, stream))) return rc;
   return rp_frame_gather(c, s, w, p, w->d_gs_rgb, d_frame_bgra, d_frame_rgb, d_counters, stream);
 }
@@ -1106,7 +1254,6 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
     ps[k].num_shards = (uint32_t)n;
     int rc = ws_reserve(m->scenes[k], &m->scenes[k]->ws0, &ps[k], true);
     if (rc) return rc;
-    if ((rc = gather_plan(m->scenes[k], &m->scenes[k]->ws0, n, k, &ps[k], plans[k]))) return rc;
   }
   const uint64_t frame_px = (uint64_t)p_in->width * p_in->height;
   if (frame_px > m->frame_px) {
@@ -1125,13 +1272,14 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
     rp_scene* s = m->scenes[k];
     int rc = render_shard(s, &s->ws0, cam, &ps[k], s->ws0.d_gs_rgb, nullptr, m->d_ctr[k], m->streams[k]);
     if (rc) return rc;
-    if ((rc = gather_stage(s, &s->ws0, plans[k], s->ws0.d_gs_rgb, bgra, rgb, m->streams[k]))) return rc;
+    if ((rc = gather_plan(s, &s->ws0, n, k, &ps[k], plans[k]))) return rc;
+    if ((rc = gather_stage(s, &s->ws0, plans[k], s->ws0.d_gs_rgb, bgra, rgb, m->d_ctr[k], m->streams[k]))) return rc;
   }
   // one thread drives every device: the collectives of all ranks form one group
   RP_NCCL(ncclGroupStart());
   for (int k = 0; k < n; k++) {
     DeviceGuard g(m->devices[k]);
-    int rc = gather_collectives(m->comms[k], &m->scenes[k]->ws0, plans[k], bgra, rgb, m->d_ctr[k], m->streams[k]);
+    int rc = gather_collectives(m->comms[k], &m->scenes[k]->ws0, plans[k], bgra, rgb, m->streams[k]);
     if (rc) {
       (void)ncclGroupEnd();
       return rc;
@@ -1140,7 +1288,7 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
   RP_NCCL(ncclGroupEnd());
   rp_scene* s0 = m->scenes[0];
   int rc = gather_assemble(s0, &s0->ws0, plans[0], bgra ? reinterpret_cast<uint8_t*>(m->d_frame_bgra) : nullptr,
-                           rgb ? m->d_frame_rgb : nullptr, m->streams[0]);
+                           rgb ? m->d_frame_rgb : nullptr, m->d_ctr[0], m->streams[0]);
   if (rc) return rc;
   for (int k = 0; k < n; k++) {
     DeviceGuard g(m->devices[k]);
@@ -1151,7 +1299,10 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
   DeviceGuard g(m->devices[0]);
   uint64_t ctr[rpk::CTR_N];
   RP_HIP(hipMemcpy(ctr, m->d_ctr[0], sizeof ctr, hipMemcpyDeviceToHost));
+  // status bits OR-ed over the devices (gather_assemble)
   if (ctr[rpk::CTR_STATUS] & rpk::STATUS_STACK_OVERFLOW) return fail(RP_EINTERNAL, "traversal stack overflow");
+  if (ctr[rpk::CTR_STATUS] & rpk::STATUS_PLAN_MISMATCH) return fail(RP_EINTERNAL, "devices made different tile plans");
+  if (ctr[rpk::CTR_STATUS]) return fail(RP_EINTERNAL, "render kernel reported status " + std::to_string(ctr[rpk::CTR_STATUS]));
   if (rgb) RP_HIP(hipMemcpy(out_rgb, m->d_frame_rgb, sizeof(double) * 3 * frame_px, hipMemcpyDeviceToHost));
   if (bgra) RP_HIP(hipMemcpy(out_bgra, m->d_frame_bgra, 4 * frame_px, hipMemcpyDeviceToHost));
   if (stats) {

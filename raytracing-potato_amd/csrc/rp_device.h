@@ -638,7 +638,7 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
   };
   w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);
   // ---- inner nodes
-  while ((gx & W8_GROUP) && (gy & 0xFFu)) {
+  while ((gx & W8_GROUP) && (gy & 0xFFu) && (!COUNT || py == 0u)) {
     DIAG(if (td) td->visits++;)
     if constexpr (COUNT) *work += WORK_VISIT;
     DREG(DREG_NODE)
@@ -707,7 +707,7 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
     gx = W8_GROUP | (c1.z & rpl::W8_INDEX);
     gy = ih | imask << 8;
     w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);
-    if ((uint32_t)__popcll(__ballot(py == 0u)) <= S.leaf_break) break;
+    if (!COUNT && (uint32_t)__popcll(__ballot(py == 0u)) <= S.leaf_break) break;
   }
   // ---- leaves: one primitive per lane per iteration from the parked group, then a waiting one
   while (py != 0u) {
@@ -721,7 +721,7 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
       px = 0u;
       if (!(gx & W8_GROUP)) w8_settle<SPILL>(S, stk, stride, spl, gx, gy, px, py, sp);  // park the waiting group
     }
-    if (PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(py != 0u)) <= PRIM_BREAK) break;
+    if (!COUNT && PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(py != 0u)) <= PRIM_BREAK) break;
   }
   ts.cur = gx;
   ts.gy = gy;
@@ -861,14 +861,18 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     if (n_hit) cur = cc[0];
     else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
-    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.
-    if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
-      leaf = cur;
-      cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
+    // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
+    // every rank of a balanced multi-GPU frame computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
+    if constexpr (!COUNT) {
+      if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+        leaf = cur;
+        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+      }
+      // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
+      // last few descents ran with most of the wave idle (those lanes resume their descent next step)
+      if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
     }
-    // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
-    // last few descents ran with most of the wave idle (those lanes resume their descent next step)
-    if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
@@ -894,7 +898,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
         leaf = 0u;
       }
     }
-    if (PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= PRIM_BREAK) {
+    if (!COUNT && PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= PRIM_BREAK) {
       // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
       if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
       break;
@@ -1321,7 +1325,7 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     batch = 0;
     const uint32_t n = A->P.probe_n;
     const uint32_t k = slot / A->P.probe_px, sub = slot % A->P.probe_px;
-    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
     const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
     pi = min(tx * tw + min((sub % n) * tw / n + tw / (2u * n), tw - 1u), A->P.W - 1u);
     pj = min(ty * th + min((sub / n) * th / n + th / (2u * n), th - 1u), A->P.H - 1u);
@@ -1363,7 +1367,7 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     batch = rem - local * A->P.nbatch;
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
     slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
-    const uint32_t t = A->P.shard + k * A->P.nshards;
+    const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
     const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
     pi = tx * tw + local % tw;
     pj = ty * th + local / tw;

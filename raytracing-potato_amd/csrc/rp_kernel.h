@@ -74,6 +74,8 @@ struct KParams {
   double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
   uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
+  const uint32_t* tile_map;    // the frame's tile deal order (RP_SHARD_BALANCED plan): shard tile k is frame tile
+                               // tile_map[shard + k * nshards] (NULL = interleave: tile shard + k * nshards)
   uint32_t* tile_cost;         // probe: [k] cost (rp_device.h WORK_*: node visits, primitive tests, rays)
                                // summed over the tile's probed samples, [TILE_SORT_MAX + k] the costliest
                                // probed sample (zeroed by the caller)
@@ -103,7 +105,10 @@ enum { QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_S
 
 // Counter block layout (RP_COUNTERS_LEN x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_N = 4 };
-enum : uint64_t { STATUS_STACK_OVERFLOW = 1 };
+enum : uint64_t { STATUS_STACK_OVERFLOW = 1, STATUS_PLAN_MISMATCH = 2 };
+// Counter block one rank contributes to a frame gather: its CTR_N counters, then its tile plan's hash (0 for the
+// interleave), padded to GATHER_CTR words.
+enum { GATHER_CTR = 8, GATHER_CTR_HASH = 4 };
 
 // Launch the persistent render kernel on `stream` (hipStream_t).  `counters` and the unit-queue word
 // `queue` (workspace-owned) must have been zeroed on the same stream.  Returns a hipError_t as int.
@@ -116,6 +121,9 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
 // so tiles processed at the same time are neighbours (the scene's cache working set stays small).
 struct TileGeom {
   uint32_t tiles_x, shard, nshards;
+  const uint32_t* map;    // a launch_tile_plan plan (order, then its inverse) of map_tiles frame tiles, NULL = interleave
+  uint32_t map_tiles;
+  uint32_t cost_by_tile;  // 1: cost[] is indexed by frame tile (a whole-frame probe), 0: by shard tile
 };
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
                      void* stream);
@@ -137,7 +145,22 @@ int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_
 struct FrameGeom {
   uint32_t W, H, tw, th, tiles_x, nranks;
   uint64_t stride;
+  const uint32_t* tile_pos;  // frame tile -> its position in the deal order (rank = pos % nranks, shard tile k =
+                             // pos / nranks); NULL = interleave (pos = the tile index)
 };
+
+// Balanced tile plan (rp.h RP_SHARD_BALANCED): from a whole-frame cost probe (cost[t] = summed probed work of frame
+// tile t, deterministic: the probe traverses without the speculative and early-exit steps), the n frame tiles are
+// sorted by cost (descending, ties by tile index) and dealt longest-processing-time first to the least-loaded of
+// `nranks` ranks that still has room for a tile, every rank receiving exactly the interleave's tile count.  Writes
+// plan[0, n) = the deal order (tile of shard s, shard tile k at plan[s + k * nranks]), plan[n, 2n) = its inverse
+// and plan[2n, 2n+2) = a 64-bit hash of the order (compared across ranks in the frame gather).  One block.
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, void* stream);
+// Counters of a frame gather: stage this rank's block (ctr may be NULL = zeros; hash may be NULL = 0) for the
+// all-gather, and reduce the gathered blocks of nranks ranks into out (sums; status bits OR-ed, plus
+// STATUS_PLAN_MISMATCH when two ranks' plan hashes differ).
+int launch_counters_stage(const uint64_t* ctr, const uint32_t* hash, uint64_t* send, void* stream);
+int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t* out, void* stream);
 int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t words, uint32_t* frame,
                           void* stream);
 

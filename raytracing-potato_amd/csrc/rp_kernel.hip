@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(256) reduce_batches_kernel(const KParams P, do
   const uint64_t slot = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (slot >= P.n_slots) return;
   const uint32_t tile_px = P.tw * P.th, k = (uint32_t)(slot / tile_px), local = (uint32_t)(slot % tile_px);
-  const uint32_t t = P.shard + k * P.nshards;
+  const uint32_t dk = P.shard + k * P.nshards, t = P.tile_map ? P.tile_map[dk] : dk;
   if ((t % P.tiles_x) * P.tw + local % P.tw >= P.W || (t / P.tiles_x) * P.th + local / P.tw >= P.H) return;
   const double* part = P.partial + 3 * slot * P.nbatch;
   const uint32_t* ph = P.partial_hits + slot * P.nbatch;
@@ -439,7 +439,8 @@ __global__ void __launch_bounds__(256) frame_assemble_kernel(const FrameGeom g, 
   for (uint64_t px = (uint64_t)blockIdx.x * 256 + threadIdx.x; px < n; px += (uint64_t)gridDim.x * 256) {
     const uint32_t j = (uint32_t)(px / g.W), i = (uint32_t)(px - (uint64_t)j * g.W);
     const uint32_t t = (j / g.th) * g.tiles_x + i / g.tw;
-    const uint32_t r = t % g.nranks, k = t / g.nranks;
+    const uint32_t pos = g.tile_pos ? g.tile_pos[t] : t;
+    const uint32_t r = pos % g.nranks, k = pos / g.nranks;
     const uint64_t slot = (uint64_t)k * g.tw * g.th + (uint64_t)(j % g.th) * g.tw + i % g.tw;
     const uint32_t* s = src + ((uint64_t)r * g.stride + slot) * words;
     for (uint32_t w = 0; w < words; w++) frame[px * words + w] = s[w];
@@ -484,13 +485,14 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
   for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
     uint32_t kk = 0xFFFFFFFFu;
     if (i < n) {
-      const uint32_t t = g.shard + i * g.nshards, tx = t % g.tiles_x, ty = t / g.tiles_x;
+      const uint32_t dk = g.shard + i * g.nshards, t = g.map ? g.map[dk] : dk, tx = t % g.tiles_x, ty = t / g.tiles_x;
       uint32_t ql = 0, qm = 0;
       if (cost) {
         // quarter-octave buckets of the costliest probed sample's cost and of the mean cost (C3: 2^(1/4)
         // steps 248.1 ms, 2^(1/32) steps 250.1 ms, the round-1 ray-count cost 254.7 ms per frame)
-        const float mean = (float)cost[i] / (float)probe_px;
-        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + i] + 1.0f) * SORT_Q), 63u);
+        const uint32_t c = g.cost_by_tile ? t : i;
+        const float mean = (float)cost[c] / (float)probe_px;
+        ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + c] + 1.0f) * SORT_Q), 63u);
         qm = min((uint32_t)(log2f(mean + 1.0f) * SORT_Q), 63u);
       }
       kk = ((63u - ql) << 22) | ((63u - qm) << 16) | (spread8(ty) << 1) | spread8(tx);
@@ -511,9 +513,12 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
       __syncthreads();
     }
   }
+  // back from the frame tile to its shard tile index: the inverse deal order (plan[n_tiles + t], laid out by
+  // launch_tile_plan right behind the order) or the interleave's (t - shard) / nshards
+  const uint32_t n_tiles = g.map ? g.map_tiles : 0u;
   for (uint32_t i = threadIdx.x; i < n; i += SORT_BLOCK) {
-    const uint32_t m = key[i] & 0xFFFFu, tx = compact8(m), ty = compact8(m >> 1);
-    order[i] = (ty * g.tiles_x + tx - g.shard) / g.nshards;
+    const uint32_t m = key[i] & 0xFFFFu, tx = compact8(m), ty = compact8(m >> 1), t = ty * g.tiles_x + tx;
+    order[i] = g.map ? g.map[n_tiles + t] / g.nshards : (t - g.shard) / g.nshards;
   }
 }
 
@@ -524,6 +529,104 @@ int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const 
   while (np2 < n) np2 <<= 1;
   hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(SORT_BLOCK), 0, (hipStream_t)stream, cost, n, probe_px, np2, g,
                      order);
+  return (int)hipGetLastError();
+}
+
+// Balanced tile plan (rp_kernel.h launch_tile_plan).  One block: the n frame tiles sorted in LDS by 64-bit key
+// (~cost << 32 | tile: descending cost, ties by tile index; 16384 tiles = 128 KB of the 160 KB a workgroup may
+// hold), then dealt in rounds of nranks tiles, alternating direction ("snake": round k gives its tiles to ranks
+// 0..N-1 when k is even, N-1..0 when odd, so each pair of rounds gives every rank one tile from the costly end and
+// one from the cheap end of the pair's 2N-tile range), the last partial round forward -- every rank gets exactly
+// the interleave's tile count, so shard sizes and gather strides do not change.  The deal is parallel (position p
+// of the sorted order -> deal slot k * N + rank), its imbalance is second order in the cost curve (a greedy LPT
+// step per tile would be a serial loop of n wave reductions).  Deterministic: integer keys, no atomics but the
+// order-free hash sum.
+static constexpr int PLAN_BLOCK = 1024;
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(PLAN_BLOCK) tile_plan_kernel(const uint32_t* __restrict__ cost, uint32_t n,
+                                                               uint32_t np2, uint32_t N, uint32_t* __restrict__ plan) {
+  __shared__ unsigned long long key[TILE_SORT_MAX];
+  __shared__ unsigned long long hash;
+  if (threadIdx.x == 0) hash = 0;
+  for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK)
+    key[i] = i < n ? ((uint64_t)(0xFFFFFFFFu - cost[i]) << 32) | i : ~0ull;
+  __syncthreads();
+  for (uint32_t size = 2; size <= np2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK) {
+        const uint32_t j = i ^ stride;
+        if (j > i) {
+          const unsigned long long a = key[i], b = key[j];
+          const bool up = (i & size) == 0;
+          if ((a > b) == up) { key[i] = b; key[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint32_t full = n / N;  // complete rounds
+  uint64_t h = 0;
+  for (uint32_t p = threadIdx.x; p < n; p += PLAN_BLOCK) {
+    const uint32_t t = (uint32_t)key[p], k = p / N, i = p - k * N;
+    const uint32_t rank = (k < full && (k & 1u)) ? N - 1u - i : i;
+    const uint32_t pos = k * N + rank;
+    plan[pos] = t;
+    plan[n + t] = pos;
+    h += mix64(((uint64_t)pos << 32) | t);
+  }
+  atomicAdd(&hash, (unsigned long long)h);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t v = mix64(hash ^ ((uint64_t)n << 32 | N)) | 1ull;  // never 0 (0 = the interleave)
+    plan[2 * n] = (uint32_t)v;
+    plan[2 * n + 1] = (uint32_t)(v >> 32);
+  }
+}
+
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, void* stream) {
+  if (n == 0 || n > TILE_SORT_MAX || nranks == 0) return (int)hipErrorInvalidValue;
+  uint32_t np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  hipLaunchKernelGGL(tile_plan_kernel, dim3(1), dim3(PLAN_BLOCK), 0, (hipStream_t)stream, cost, n, np2, nranks, plan);
+  return (int)hipGetLastError();
+}
+
+// Counters of a frame gather (rp_kernel.h launch_counters_stage / _reduce): one tiny block each.
+__global__ void counters_stage_kernel(const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ hash,
+                                      uint64_t* __restrict__ send) {
+  const uint32_t i = threadIdx.x;
+  if (i >= GATHER_CTR) return;
+  uint64_t v = 0;
+  if (i < CTR_N) v = ctr ? ctr[i] : 0ull;
+  else if (i == GATHER_CTR_HASH) v = hash ? ((uint64_t)hash[1] << 32 | hash[0]) : 0ull;
+  send[i] = v;
+}
+__global__ void counters_reduce_kernel(const uint64_t* __restrict__ g, uint32_t nranks, uint64_t* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  uint64_t rays = 0, samples = 0, pixels = 0, status = 0;
+  for (uint32_t r = 0; r < nranks; r++) {
+    const uint64_t* b = g + (uint64_t)r * GATHER_CTR;
+    rays += b[CTR_RAYS];
+    samples += b[CTR_SAMPLES];
+    pixels += b[CTR_PIXELS];
+    status |= b[CTR_STATUS];
+    if (b[GATHER_CTR_HASH] != g[GATHER_CTR_HASH]) status |= STATUS_PLAN_MISMATCH;
+  }
+  out[CTR_RAYS] = rays;
+  out[CTR_SAMPLES] = samples;
+  out[CTR_PIXELS] = pixels;
+  out[CTR_STATUS] = status;
+}
+int launch_counters_stage(const uint64_t* ctr, const uint32_t* hash, uint64_t* send, void* stream) {
+  hipLaunchKernelGGL(counters_stage_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr, hash, send);
+  return (int)hipGetLastError();
+}
+int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t* out, void* stream) {
+  hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, nranks, out);
   return (int)hipGetLastError();
 }
 

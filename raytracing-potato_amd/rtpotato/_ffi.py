@@ -31,6 +31,9 @@ RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
 RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON = 0, 1, 2, 3
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
+RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
+RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
+RP_ABI_VERSION = 5
 
 
 class rp_hittable(Structure):
@@ -81,7 +84,7 @@ class rp_camera(Structure):
 class rp_render_params(Structure):
     _fields_ = [("width", c_uint32), ("height", c_uint32), ("spp", c_uint32), ("max_bounce", c_uint32),
                 ("seed", c_uint64), ("tile_w", c_uint32), ("tile_h", c_uint32), ("shard", c_uint32),
-                ("num_shards", c_uint32), ("samples_per_stream", c_uint32), ("reserved", c_uint32)]
+                ("num_shards", c_uint32), ("samples_per_stream", c_uint32), ("shard_map", c_uint32)]
 
 
 class rp_scene_options(Structure):
@@ -89,7 +92,7 @@ class rp_scene_options(Structure):
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
                 ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
-                ("unit_queues", c_uint32), ("queue_chunk", c_uint32)]
+                ("unit_queues", c_uint32), ("queue_chunk", c_uint32), ("debug_stack_depth", c_uint32)]
 
 
 class rp_stats(Structure):
@@ -124,7 +127,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_render_device_ws", "rp_shard_to_bgra8", "rp_srgb_thresholds", "rp_scene_options_init",
               "rp_scene_create_ex", "rp_workspace_reserve", "rp_comm_unique_id", "rp_comm_create", "rp_comm_destroy",
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
-              "rp_render_multi"]
+              "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64"]
@@ -154,6 +157,7 @@ def rp() -> ctypes.CDLL:
     lib = ctypes.CDLL(path)
     lib.rp_abi_version.restype = c_int
     lib.rp_last_error.restype = c_char_p
+    lib.rp_build_id.restype = c_char_p
     lib.rp_device_count.argtypes = [POINTER(c_int)]
     lib.rp_scene_create.argtypes = [POINTER(rp_scene_desc), c_int, POINTER(c_void_p)]
     lib.rp_scene_destroy.argtypes = [c_void_p]
@@ -195,8 +199,12 @@ def rp() -> ctypes.CDLL:
     lib.rp_multi_destroy.restype = None
     lib.rp_render_multi.argtypes = [c_void_p, POINTER(rp_camera), POINTER(rp_render_params), c_void_p, c_void_p,
                                     POINTER(rp_stats)]
-    if lib.rp_abi_version() != 4:
-        raise RuntimeError(f"{path}: ABI version {lib.rp_abi_version()}, bindings expect 4 (rebuild)")
+    lib.rp_shard_unpack_map.argtypes = [POINTER(rp_render_params), c_void_p, c_void_p, c_uint32, c_void_p]
+    lib.rp_workspace_tile_map.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
+    lib.rp_frame_assemble_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32, c_void_p,
+                                         c_void_p]
+    if lib.rp_abi_version() != RP_ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI version {lib.rp_abi_version()}, bindings expect {RP_ABI_VERSION} (rebuild)")
     _rp = lib
     return lib
 

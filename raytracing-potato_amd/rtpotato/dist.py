@@ -1,5 +1,5 @@
-"""Multi-GPU frames: one process per GPU, image tiles interleaved across ranks (tile t goes to rank t %
-world), one RCCL all-gather per frame over xGMI inside librp.so (rp_frame_gather / rp_render_gather), then
+"""Multi-GPU frames: one process per GPU, image tiles dealt across ranks (interleaved -- tile t goes to rank t %
+world -- or by the balanced cost plan, RP_SHARD_BALANCED), one RCCL all-gather per frame over xGMI inside librp.so (rp_frame_gather / rp_render_gather), then
 a device-side de-interleave into frame order.  The scene is replicated per GPU.
 
 The reference's only parallelism is its thread tile queue (main.rs:36-98, `Arc<Mutex<Vec<Tile>>>`); this
@@ -27,19 +27,41 @@ def max_slots(params: RenderParams, world: int) -> int:
     return shard_slot_count(replace(params, shard=0, num_shards=world))
 
 
-def assemble_frame(gathered: np.ndarray, params: RenderParams, world: int) -> np.ndarray:
+def assemble_frame(gathered: np.ndarray, params: RenderParams, world: int, tile_map=None) -> np.ndarray:
     """NumPy restatement of the device frame assembly (rp_kernel.hip frame_assemble_kernel, rp_frame_assemble):
     gathered = (world * stride, C) slots, rank r's shard at r * stride; returns (H, W, C) in frame order.
-    Pixel (i, j) is in tile t = (j / th) * tiles_x + i / tw, owned by rank t % world as its shard tile
-    k = t / world, slot k * tw * th + (j % th) * tw + i % tw."""
+    Pixel (i, j) is in tile t = (j / th) * tiles_x + i / tw at position pos of the deal order (pos = t for the
+    interleave; tile_map = the deal order of a balanced frame, rp_workspace_tile_map), owned by rank pos % world as
+    its shard tile k = pos / world, slot k * tw * th + (j % th) * tw + i % tw."""
     tw, th = params.tile_w, params.tile_h
     tiles_x = -(-params.width // tw)
     stride = max_slots(params, world)
     j, i = np.mgrid[0:params.height, 0:params.width]
     t = (j // th) * tiles_x + i // tw
+    if tile_map is not None:
+        inv = np.empty(len(tile_map), dtype=np.int64)
+        inv[np.asarray(tile_map, dtype=np.int64)] = np.arange(len(tile_map))
+        t = inv[t]
     r, k = t % world, t // world
     slot = r * stride + k * tw * th + (j % th) * tw + i % tw
     return gathered[slot]
+
+
+def deal_tiles(cost, world: int) -> np.ndarray:
+    """NumPy restatement of the balanced tile plan's deal (rp_kernel.hip tile_plan_kernel, RP_SHARD_BALANCED):
+    tiles sorted by cost descending (ties by tile index), dealt in rounds of `world` alternating direction (round k
+    to ranks 0..world-1 when k is even, world-1..0 when odd; the last partial round forward).  Returns the deal
+    order: shard s's k-th tile is order[s + k * world]."""
+    cost = np.asarray(cost, dtype=np.int64)
+    n = len(cost)
+    srt = np.lexsort((np.arange(n), -cost))  # cost descending, then tile index
+    p = np.arange(n)
+    k, i = p // world, p % world
+    full = n // world
+    rank = np.where((k < full) & (k % 2 == 1), world - 1 - i, i)
+    order = np.empty(n, dtype=np.int64)
+    order[k * world + rank] = srt
+    return order
 
 
 def share_unique_id(rank: int, world: int, group=None) -> bytes:

@@ -93,6 +93,16 @@ class DeviceScene:
         p = params.to_c()
         F.check(F.rp().rp_workspace_reserve(self.handle, workspace.handle if workspace else None, ctypes.byref(p)))
 
+    def tile_map(self, params: RenderParams, workspace: "Workspace | None" = None) -> np.ndarray:
+        """rp_workspace_tile_map: the frame's deal order (shard s's k-th tile = map[s + k * num_shards]) -- the
+        balanced plan the last render of this frame in `workspace` made, or the interleave's identity."""
+        tiles = -(-params.width // params.tile_w) * -(-params.height // params.tile_h)
+        out = np.empty(tiles, dtype=np.uint32)
+        p = params.to_c()
+        F.check(F.rp().rp_workspace_tile_map(self.handle, workspace.handle if workspace else None, ctypes.byref(p),
+                                             out.ctypes.data, tiles))
+        return out
+
     # ---- synchronous host-buffer render -----------------------------------------------------------
     def render(self, params: RenderParams, camera=None, foreground: bool = False):
         """Full frame (only the shard's pixels written, others zero): (rgb (h, w, 3) f64,
@@ -271,13 +281,19 @@ class MultiScene:
 
 
 def unpack_shard(params: RenderParams, shard_buf: np.ndarray, channels: int = 3,
-                 frame: np.ndarray | None = None) -> np.ndarray:
-    """Scatter a compact shard buffer into a full (h, w, channels) frame (rp_shard_unpack)."""
+                 frame: np.ndarray | None = None, tile_map=None) -> np.ndarray:
+    """Scatter a compact shard buffer into a full (h, w, channels) frame (rp_shard_unpack; with `tile_map`, the
+    deal order of a balanced frame, rp_shard_unpack_map)."""
     if frame is None:
         frame = np.zeros((params.height, params.width, channels), dtype=np.float64)
     src = np.ascontiguousarray(shard_buf, dtype=np.float64)
     p = params.to_c()
-    F.check(F.rp().rp_shard_unpack(ctypes.byref(p), src.ctypes.data, channels, frame.ctypes.data))
+    if tile_map is None:
+        F.check(F.rp().rp_shard_unpack(ctypes.byref(p), src.ctypes.data, channels, frame.ctypes.data))
+    else:
+        m = np.ascontiguousarray(tile_map, dtype=np.uint32)
+        F.check(F.rp().rp_shard_unpack_map(ctypes.byref(p), m.ctypes.data, src.ctypes.data, channels,
+                                           frame.ctypes.data))
     return frame
 
 

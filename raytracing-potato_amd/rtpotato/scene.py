@@ -350,6 +350,7 @@ class RenderParams:
     shard: int = 0
     num_shards: int = 1
     samples_per_stream: int = 0  # RNG contract batch size (0 -> RP_SAMPLES_PER_STREAM = 32; >= spp: one stream)
+    shard_map: int = 0  # RP_SHARD_INTERLEAVE (tile t -> shard t % num_shards) or RP_SHARD_BALANCED (cost plan)
 
     def to_c(self) -> F.rp_render_params:
         p = F.rp_render_params()
@@ -357,6 +358,7 @@ class RenderParams:
         p.seed = self.seed & 0xFFFFFFFFFFFFFFFF
         p.tile_w, p.tile_h, p.shard, p.num_shards = self.tile_w, self.tile_h, self.shard, self.num_shards
         p.samples_per_stream = self.samples_per_stream
+        p.shard_map = self.shard_map
         return p
 
 
@@ -369,14 +371,17 @@ def shard_slot_count(params: RenderParams) -> int:
     return n_shard_tiles * params.tile_w * params.tile_h
 
 
-def shard_slot_pixels(params: RenderParams) -> np.ndarray:
-    """(slot -> flat pixel index j*W + i, or -1 for slots outside the frame) for the compact shard buffer."""
+def shard_slot_pixels(params: RenderParams, tile_map=None) -> np.ndarray:
+    """(slot -> flat pixel index j*W + i, or -1 for slots outside the frame) for the compact shard buffer.
+    tile_map: the frame's deal order (rp_workspace_tile_map) of a balanced frame, None = the interleave."""
     tw, th = params.tile_w, params.tile_h
     tiles_x = -(-params.width // tw)
     n = shard_slot_count(params)
     slot = np.arange(n, dtype=np.int64)
     k, local = slot // (tw * th), slot % (tw * th)
     t = params.shard + k * params.num_shards
+    if tile_map is not None:
+        t = np.asarray(tile_map, dtype=np.int64)[t]
     i = (t % tiles_x) * tw + local % tw
     j = (t // tiles_x) * th + local // tw
     ok = (i < params.width) & (j < params.height)

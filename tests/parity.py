@@ -43,11 +43,21 @@ def compare(gpu_rgb: np.ndarray, ref_rgb: np.ndarray, mask: np.ndarray | None = 
     both_nan = np.isnan(a) & np.isnan(b)
     diff = np.where(both_nan, 0.0, diff)
     per_px = diff.reshape(-1, 3).max(axis=1)
+    nan_px = np.isnan(per_px)  # NaN on one side only (both-NaN channels count 0 above)
     return {
-        "linf": float(np.nanmax(per_px)) if per_px.size else 0.0,
+        # a one-sided NaN is an infinite error: it fails the L-inf bar by itself
+        "linf": (float("inf") if nan_px.any() else float(per_px.max())) if per_px.size else 0.0,
         "nan_mismatch": int(np.sum(np.isnan(per_px))),
         "pixels": int(per_px.size),
         "bad": int(np.sum(per_px >= TOL_LINF)),
         "not_exact": int(np.sum(per_px > TOL_EXACT)),
         "exact_frac": float(np.mean(per_px <= TOL_EXACT)) if per_px.size else 1.0,
     }
+
+
+def assert_parity(c: dict, min_exact: float = 0.999) -> None:
+    """The parity bar on a compare() result: no one-sided NaN, per-pixel L-inf < TOL_LINF, and at least
+    `min_exact` of the pixels equal to 1e-12 (the same paths)."""
+    assert c["nan_mismatch"] == 0, c
+    assert c["linf"] < TOL_LINF, c
+    assert c["exact_frac"] >= min_exact, c

@@ -92,3 +92,86 @@ def test_max_slots_and_shard_partition():
         allpix = np.concatenate([shard_slot_pixels(shard_params(p, r, world)) for r in range(world)])
         allpix = np.sort(allpix[allpix >= 0])
         assert np.array_equal(allpix, np.arange(1920 * 1080))
+
+
+def test_deal_tiles_balances_and_keeps_counts():
+    """The balanced plan's deal (rtpotato.dist.deal_tiles, the restatement of tile_plan_kernel): a permutation of
+    the frame's tiles, every rank holding exactly the interleave's tile count (so shard buffers and gather strides
+    are unchanged), and per-rank cost totals within a few percent on a skewed cost field -- where the interleave,
+    whose columns of tiles follow the frame's structure, is far off."""
+    from rtpotato.dist import deal_tiles, shard_params
+    from rtpotato.scene import RenderParams, shard_slot_count
+    rng = np.random.default_rng(5)
+    p = RenderParams(1920, 1080, 1, 8, 0)
+    tx, ty = 60, 34
+    n = tx * ty
+    # a bright object in the middle third (costly), cheap sky elsewhere, noisy
+    xs, ys = np.meshgrid(np.arange(tx), np.arange(ty))
+    cost = (100 + 900 * ((abs(xs - 30) < 10) & (ys < 20)) * (1 + (xs % 8 == 3))) * rng.uniform(0.7, 1.3, (ty, tx))
+    cost = cost.astype(np.int64).reshape(-1)
+    for world in (1, 2, 3, 4, 8):
+        order = deal_tiles(cost, world)
+        assert np.array_equal(np.sort(order), np.arange(n))
+        loads = np.zeros(world)
+        for r in range(world):
+            mine = order[r::world]
+            assert len(mine) * 32 * 32 == shard_slot_count(shard_params(p, r, world))
+            loads[r] = cost[mine].sum()
+        assert loads.max() / loads.mean() < 1.01, (world, loads)
+        inter = np.array([cost[r::world].sum() for r in range(world)])
+        if world == 8:
+            assert inter.max() / inter.mean() > 1.05  # the interleave is not balanced on this field
+
+
+def _worker_balanced(rank, world, port, result_dir):
+    """Ranks deal the tiles by the balanced plan (costs: the frame's per-tile ray counts, the same on every rank),
+    render their shards (pixels of the oracle frame: per-pixel seeding), all-gather and assemble with the plan."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path[:0] = [here, os.path.dirname(here), os.path.join(os.path.dirname(here), "raytracing-potato_amd")]
+    from dataclasses import replace
+    import torch
+    import torch.distributed as dist
+    from parity import oracle_render
+    from rtpotato import scenes
+    from rtpotato.dist import assemble_frame, deal_tiles, max_slots, shard_params
+    from rtpotato.scene import RenderParams, shard_slot_pixels
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    scene = scenes.configure(scenes.bunny_full(), 75, 41)
+    params = RenderParams(75, 41, 2, 8, 77, 16, 16, shard_map=1)
+    tiles_x, tiles_y = 5, 3
+    cost = np.zeros(tiles_x * tiles_y, dtype=np.int64)
+    for t in range(tiles_x * tiles_y):  # per-tile cost: the tile's rays (a shard of one tile)
+        _, _, c = oracle_render(scene, replace(params, shard=t, num_shards=tiles_x * tiles_y, shard_map=0), threads=1)
+        cost[t] = c["rays"]
+    order = deal_tiles(cost, world)
+    full, _, _ = oracle_render(scene, replace(params, shard_map=0), threads=2)
+    sp = shard_params(params, rank, world)
+    stride = max_slots(params, world)
+    buf = torch.zeros(stride, 3, dtype=torch.float64)
+    pix = shard_slot_pixels(sp, order)
+    ok = pix >= 0
+    buf[:len(pix)][torch.as_tensor(ok)] = torch.as_tensor(full.reshape(-1, 3)[pix[ok]])
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    out = assemble_frame(torch.cat(parts).numpy(), params, world, order)
+    orders = [None] * world
+    dist.all_gather_object(orders, order.tolist())
+    if rank == 0:
+        np.save(os.path.join(result_dir, "frame.npy"), out)
+        np.save(os.path.join(result_dir, "orders.npy"), np.array(orders))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_balanced_gather_rebuilds_frame(tmp_path, world):
+    from dataclasses import replace
+    from parity import oracle_render
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    mp.spawn(_worker_balanced, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    scene = scenes.configure(scenes.bunny_full(), 75, 41)
+    ref, _, _ = oracle_render(scene, RenderParams(75, 41, 2, 8, 77, 16, 16), threads=4)
+    assert np.array_equal(np.load(tmp_path / "frame.npy"), ref)
+    orders = np.load(tmp_path / "orders.npy")
+    assert (orders == orders[0]).all() and not np.array_equal(orders[0], np.arange(15))

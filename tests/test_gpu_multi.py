@@ -1,0 +1,192 @@
+"""GPU tests of the multi-GPU boundary added in ABI v5 (include/rp.h): the balanced tile plan (RP_SHARD_BALANCED)
+and the frame gather's status reduction, plus the error path of a traversal-stack overflow made reachable by the
+test-only option rp_scene_options.debug_stack_depth.
+
+The reference splits a frame over its worker threads with one shared tile queue (main.rs:41,55-59), so no
+worker idles while tiles remain; across GPUs the split is static, and the balanced plan deals the tiles by a
+probed cost instead of tile t -> rank t % N.  Every plan is checked to rebuild the single-device frame bit for bit.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+from dataclasses import replace
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _params(w, h, spp, **kw):
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    return RenderParams(w, h, spp, 8, scenes.DEFAULT_SEED, 16, 16, **kw)
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_balanced_plan_rebuilds_frame(gpu, world):
+    """Every rank's render (here: `world` workspaces on one GPU) makes the same plan -- a permutation of the
+    frame's tiles with the interleave's tile count per rank, different from the interleave -- and the shards,
+    laid out as the all-gather leaves them and assembled with rp_frame_assemble_ws, are the rp_render frame bit
+    for bit; so is the NumPy restatement of the assembly with the plan (rtpotato.dist.assemble_frame)."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.dist import assemble_frame, max_slots, shard_params
+    from rtpotato.scene import shard_slot_count
+    sc = scenes.configure(scenes.bunny_full(), 150, 90)
+    p = _params(150, 90, 6, shard_map=F.RP_SHARD_BALANCED)
+    ref, _, st = gpu.render(sc, replace(p, shard_map=0))
+    S = max_slots(p, world)
+    gathered = torch.zeros(world * S * 3, dtype=torch.float64, device="cuda")
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+    rays = 0
+    n_tiles = 10 * 6
+    with gpu.DeviceScene(sc) as ds:
+        wss = [ds.workspace() for _ in range(world)]
+        maps = []
+        for r in range(world):
+            sp = shard_params(p, r, world)
+            n = shard_slot_count(sp)
+            ds.reserve(sp, wss[r])
+            ds.render_device(sp, gathered[r * S * 3:(r * S + n) * 3], ctr, workspace=wss[r])
+            torch.cuda.synchronize()
+            rays += int(ctr[0])
+            assert int(ctr[3]) == 0
+            maps.append(ds.tile_map(sp, wss[r]))
+        for m in maps:
+            assert np.array_equal(m, maps[0])
+        order = maps[0]
+        assert np.array_equal(np.sort(order), np.arange(n_tiles)) and not np.array_equal(order, np.arange(n_tiles))
+        frame = torch.zeros(p.width * p.height * 3, dtype=torch.float64, device="cuda")
+        pc = shard_params(p, 0, world).to_c()
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        F.check(F.rp().rp_frame_assemble_ws(ds.handle, wss[0].handle, ctypes.byref(pc), gathered.data_ptr(), 6,
+                                            frame.data_ptr(), s))
+        with pytest.raises(F.RPError):  # the plan-less assembly refuses a balanced frame
+            F.check(F.rp().rp_frame_assemble(ctypes.byref(pc), gathered.data_ptr(), 6, frame.data_ptr(), s))
+        torch.cuda.synchronize()
+    got = frame.cpu().numpy().reshape(p.height, p.width, 3)
+    assert np.array_equal(got, ref)
+    assert np.array_equal(assemble_frame(gathered.cpu().numpy().reshape(-1, 3), p, world, order), ref)
+    assert rays == st["rays"]
+
+
+def test_balanced_host_render_and_unpack(gpu):
+    """rp_render of a balanced shard writes exactly the pixels of its planned tiles, equal to the full frame's; the
+    interleave-only rp_shard_unpack refuses a balanced frame, rp_shard_unpack_map takes its plan."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.dist import shard_params
+    from rtpotato.render import unpack_shard
+    from rtpotato.scene import shard_slot_pixels
+    sc = scenes.configure(scenes.bunny_full(), 96, 64)
+    p = _params(96, 64, 5, shard_map=F.RP_SHARD_BALANCED)
+    with gpu.DeviceScene(sc) as ds:
+        full, _, st = ds.render(replace(p, shard_map=0))
+        total = 0
+        for r in range(4):
+            sp = shard_params(p, r, 4)
+            rgb, _, sst = ds.render(sp)
+            order = ds.tile_map(sp)
+            pix = shard_slot_pixels(sp, order)
+            m = np.zeros(96 * 64, dtype=bool)
+            m[pix[pix >= 0]] = True
+            m = m.reshape(64, 96)
+            assert np.array_equal(rgb[m], full[m]) and not rgb[~m].any()
+            assert sst["pixels"] == m.sum()
+            total += sst["rays"]
+            shard = np.zeros((len(pix), 3))
+            shard[pix >= 0] = full.reshape(-1, 3)[pix[pix >= 0]]
+            with pytest.raises(F.RPError):
+                unpack_shard(sp, shard)
+            assert np.array_equal(unpack_shard(sp, shard, tile_map=order)[m], full[m])
+        assert total == st["rays"]
+
+
+def test_balanced_plan_balances_c3_costs(gpu):
+    """On config C3's frame the balanced plan's 8 shards carry nearly equal work: the per-shard ray counts of the
+    real 256-spp frame are within 3 % of their mean (the interleave's are compared for the record)."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.dist import shard_params
+    scene, params = scenes.config_scene("C3")
+    params = replace(params, spp=32)  # one RNG batch per pixel: the same paths as the frame's first 32 samples
+    rays = {}
+    with gpu.DeviceScene(scene) as ds:
+        for mode in (F.RP_SHARD_INTERLEAVE, F.RP_SHARD_BALANCED):
+            rays[mode] = [ds.render(shard_params(replace(params, shard_map=mode), r, 8))[2]["rays"] for r in range(8)]
+    bal, inter = np.array(rays[F.RP_SHARD_BALANCED]), np.array(rays[F.RP_SHARD_INTERLEAVE])
+    assert bal.sum() == inter.sum()
+    assert bal.max() / bal.mean() < 1.03, (bal, inter)
+
+
+def test_multi_balanced_single_device(gpu):
+    """rp_render_multi with the balanced plan over device 0 equals rp_render."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.render import MultiScene
+    sc = scenes.configure(scenes.bunny_full(), 64, 40)
+    p = _params(64, 40, 12, shard_map=F.RP_SHARD_BALANCED)
+    ref, _, st = gpu.render(sc, replace(p, shard_map=0))
+    with MultiScene(sc, [0]) as ms:
+        rgb, bgra, mst = ms.render(p, bgra=True)
+    assert np.array_equal(rgb, ref) and mst["rays"] == st["rays"]
+
+
+def _overflow_scene():
+    from rtpotato import scenes
+    return scenes.configure(scenes.random_mesh(200_000), 48, 32)
+
+
+def test_stack_overflow_is_reported(gpu):
+    """debug_stack_depth = 8 (cap 5 entries) on a tree needing ~31: every entry point reports the overflow --
+    rp_render and rp_render_multi return RP_EINTERNAL, rp_render_device and rp_render_gather (1-rank RCCL
+    communicator: the status word goes through the counter all-gather and its OR reduction) leave the bit in
+    the counters.  The kernels never write past the stack (the frame is wrong, the process is fine)."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.render import Comm, MultiScene, comm_unique_id
+    from rtpotato.scene import shard_slot_count
+    sc = _overflow_scene()
+    p = _params(48, 32, 4)
+    opts = {"debug_stack_depth": 8}
+    with gpu.DeviceScene(sc, options=opts) as ds:
+        with pytest.raises(F.RPError) as e:
+            ds.render(p)
+        assert e.value.code == F.RP_EINTERNAL and "overflow" in str(e.value)
+        out = torch.zeros(3 * shard_slot_count(p), dtype=torch.float64, device="cuda")
+        ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+        ds.render_device(p, out, ctr)
+        torch.cuda.synchronize()
+        assert int(ctr[3]) & F.RP_STATUS_STACK_OVERFLOW
+        with Comm(comm_unique_id(), 1, 0, 0) as comm:
+            for mode in (F.RP_SHARD_INTERLEAVE, F.RP_SHARD_BALANCED):
+                q = replace(p, shard_map=mode)
+                ds.reserve(q)
+                frame = torch.zeros(4 * p.width * p.height, dtype=torch.uint8, device="cuda")
+                ctr.zero_()
+                ds.render_gather(comm, q, frame_bgra=frame, counters=ctr)
+                torch.cuda.synchronize()
+                assert int(ctr[3]) == F.RP_STATUS_STACK_OVERFLOW and int(ctr[0]) > 0
+    with MultiScene(sc, [0], options=opts) as ms:
+        with pytest.raises(F.RPError) as e:
+            ms.render(p)
+        assert e.value.code == F.RP_EINTERNAL and "overflow" in str(e.value)
+    # the same scene with the stack the tree needs: no status
+    with gpu.DeviceScene(sc) as ds:
+        _, _, st = ds.render(p)
+        assert st["rays"] > 0
+
+
+def test_bench_refuses_overflowing_frame():
+    """bench.py checks every frame's status word and refuses to report a rate for a frame that overflowed."""
+    env = dict(os.environ)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--config", "C1", "--steps", "1", "--warmup", "0",
+                        "--no-cpu-baseline", "--opt", "debug_stack_depth=8"], capture_output=True, text=True,
+                       timeout=300, env=env, cwd=REPO)
+    assert r.returncode != 0 and "status" in r.stderr, (r.returncode, r.stderr[-2000:])
+    assert '"metric"' not in r.stdout

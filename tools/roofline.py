@@ -12,6 +12,17 @@ The record bench.py prices its `roofline` with (kernel_record()): per ray of the
 and for the frame: the SQ cycle budget (WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY = WAVE_CYCLES, all in
 quad-cycles), the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / kernel duration), the VALU-issue fraction at
 that clock and at 2.4 GHz (a wave64 VALU instruction holds a SIMD-32 for 2 cycles), and the instruction mix.
+
+With --diag (a tools/diag.py record of the same build over the same frame) the record also carries the kernel's
+own ALGORITHMIC bytes per ray -- what its traversal and shading must touch, wherever it is served from:
+  node visits x bytes a visit loads (Node4 f32: 6 plane rows + children = 112 B; Node4Q: 64 B)
+  + primitive tests x 80 B (rpl::Prim)
+  + shaded hits x 232 B (PrimRef 16 + 3 vertex normals 72 + 3 vertex uvs 48 + Material 96)
+  + texture samples x 4 B (one RGBA8 texel)
+  + keystream blocks made x 128 B (64 B written to the slab, read back once by the draws)
+  + frame output (batch sums 28 B per unit written and read, the framebuffer 24 B per pixel) / rays
+and traffic / algorithmic, the fraction of those bytes the caches did NOT serve.  build_id = rp_build_id() of the
+library that ran the passes: bench.py refuses a record of another build.
 """
 import argparse
 import collections
@@ -46,11 +57,39 @@ def read_pass(d):
     return dict(per[did]), dur[did]
 
 
+def lanes_per_ray(diag, region):
+    r = diag["regions"][region]
+    return r["wave_execs_per_kray"] * r["lane_util"] * 64.0 / 1000.0
+
+
+def algorithmic(diag, node_bytes, bench):
+    """Algorithmic bytes per ray of the render kernel (module docstring) from a diagnostic record."""
+    cfg = bench["config"]
+    W, H, spp = cfg["width"], cfg["height"], cfg["spp"]
+    rays = float(cfg["rays_per_frame"])
+    nbatch = -(-spp // 32)
+    out_bytes = (W * H * nbatch * 28 * (2 if nbatch > 1 else 0) + W * H * 24) / rays
+    parts = {
+        "nodes": diag["visits_per_ray"] * node_bytes,
+        "prims": diag["prim_tests_per_ray"] * 80.0,
+        "hit_records": lanes_per_ray(diag, "surface") * 232.0,
+        "texels": lanes_per_ray(diag, "texture") * 4.0,
+        "keystream": lanes_per_ray(diag, "refill") * 128.0,
+        "output": out_bytes,
+    }
+    return {"algorithmic_bytes_per_ray": sum(parts.values()),
+            "algorithmic_breakdown": {k: round(v, 2) for k, v in parts.items()},
+            "diag": {"visits_per_ray": diag["visits_per_ray"], "prim_tests_per_ray": diag["prim_tests_per_ray"],
+                     "node_bytes": node_bytes, "spp": diag.get("spp"), "phase_share": diag.get("phase_share")}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--bench", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--diag", help="tools/diag.py record of the same build and frame")
+    ap.add_argument("--node-bytes", type=int, default=0, help="bytes one node visit loads (0: C5 -> 64 (q8), else 112)")
     ap.add_argument("passes", nargs="+")
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
@@ -61,7 +100,8 @@ def main():
         c.update(vals)
         durs[os.path.basename(d.rstrip("/"))] = ns
     rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
-    rec = {"kernel": KERNEL, "config": a.config, "git": rev, "rays": rays, "counters": c,
+    build = bench.get("roofline", {}).get("build_id")
+    rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays, "counters": c,
            "kernel_ns_per_pass": durs, "bench_ms_per_step": bench.get("ms_per_step")}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fetch, write = 2.0 * c["FETCH_SIZE"] * 1024.0, c["WRITE_SIZE"] * 1024.0
@@ -96,6 +136,10 @@ def main():
         rec["valu_thread_cycles_per_active_quad"] = round(c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"], 3)
     if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
         rec["l2_hit_rate"] = round(c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"]), 4)
+    if a.diag:
+        rec.update(algorithmic(json.load(open(a.diag)), a.node_bytes or (64 if a.config == "C5" else 112), bench))
+        if "traffic_bytes_per_ray" in rec:
+            rec["traffic_over_algorithmic"] = round(rec["traffic_bytes_per_ray"] / rec["algorithmic_bytes_per_ray"], 4)
     json.dump(rec, open(a.out, "w"), indent=1)
     print(json.dumps({k: v for k, v in rec.items() if k != "counters"}))
 
