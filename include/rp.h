@@ -314,6 +314,20 @@ int rp_render_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camer
  * uses for this frame size.  Synchronous (allocates; may free a smaller reservation); idempotent for a
  * shape it already covers.  rp_render reserves for itself. */
 int rp_workspace_reserve(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params);
+/* Scheduling costs.  Every render of the megakernel measures its units' durations per tile; a workspace that
+ * rendered a whole frame on one device (num_shards = 1), or gathered one with rp_frame_gather, keeps them as a
+ * learned per-tile cost table, and its next frame of the same geometry orders its tiles -- and deals them
+ * (RP_SHARD_BALANCED) -- from that table instead of tracing a cost probe.  A balanced plan over N ranks only uses a
+ * table gathered from N ranks (identical bytes on every rank, hence identical plans).  Callers that move shards
+ * with their own collective get a render's measured costs with rp_workspace_tile_costs (2 x the shard's tile
+ * count: summed unit durations per shard tile, then the longest unit; synchronises the device) and install a
+ * frame's table, assembled through the deal order, with rp_workspace_set_tile_costs (2 x the frame's tile count:
+ * sums, then longest units, by frame tile; `ranks` = how many ranks' renders it combines).  Results never
+ * depend on any of it. */
+int rp_workspace_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                            uint32_t* costs, uint32_t n);
+int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                                const uint32_t* costs, uint32_t ranks);
 /* The deal order of params' frame (one entry per frame tile; shard s's k-th tile is tile_map[s + k*num_shards]):
  * for RP_SHARD_BALANCED the plan the last render of this frame in `workspace` (NULL = the scene's) made, for the
  * interleave 0, 1, 2, ...  n >= the frame's tile count.  Synchronises the device. */

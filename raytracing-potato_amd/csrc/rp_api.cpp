@@ -117,6 +117,17 @@ struct rp_workspace {
   uint32_t* d_plan = nullptr;
   bool plan_on = false;
   uint32_t plan_geom[5] = {0, 0, 0, 0, 0};  // width, height, tile_w, tile_h, num_shards
+  // Measured tile costs (rp_kernel.h tile_meas / launch_learn_costs): the last render's per-shard-tile unit
+  // durations, every rank's of them after a frame gather, and the learned per-frame-tile table the next frame of
+  // the same geometry schedules with instead of a cost probe.
+  uint32_t* d_meas = nullptr;     // 2 x TILE_SORT_MAX: [k] summed, [TILE_SORT_MAX + k] longest unit of shard tile k
+  uint32_t* d_meas_g = nullptr;   // frame gather: 2 x nranks x stride_tiles (sums, then maxima; rank-major)
+  uint64_t meas_g_words = 0;
+  uint32_t* d_fcost = nullptr;    // learned table: 2 x TILE_SORT_MAX, by frame tile
+  bool meas_on = false;           // the last render measured (megakernel)
+  bool fcost_valid = false;
+  uint32_t fcost_geom[4] = {0, 0, 0, 0};  // width, height, tile_w, tile_h of the learned table
+  uint32_t fcost_ranks = 0;               // ranks whose gather made it (1: a whole-frame render on one device)
   rpk::WfBuffers wf{};               // the stage-split engine's path-slot pool (engine = wavefront only)
 };
 
@@ -169,7 +180,8 @@ void ws_release(rp_workspace* w) {
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
-                  (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan})
+                  (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
+                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost})
     dfree(p);
   *w = rp_workspace{};
 }
@@ -182,7 +194,8 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
   const uint64_t lanes = s->lanes();
   if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, rpk::QUEUE_WORDS) ||
       !dalloc(&w->d_tile_cost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_tile_order, rpk::TILE_SORT_MAX) ||
-      !dalloc(&w->d_plan, 2 * rpk::TILE_SORT_MAX + 2) ||
+      !dalloc(&w->d_plan, 2 * rpk::TILE_SORT_MAX + 2) || !dalloc(&w->d_meas, 2 * rpk::TILE_SORT_MAX) ||
+      !dalloc(&w->d_fcost, 2 * rpk::TILE_SORT_MAX) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
     ws_release(w);
@@ -252,6 +265,19 @@ void unpack_host(const rp_render_params* p, const Tiling& t, const uint32_t* map
         std::memcpy(dst + ((uint64_t)(oy + lj) * p->width + ox + li) * channels * elem,
                     src + (k * tile_px + (uint64_t)lj * t.tw + li) * channels * elem, channels * elem);
   }
+}
+
+// The workspace's learned cost table describes frames of params' geometry.
+bool fcost_matches(const rp_workspace* w, const rp_render_params* p, const Tiling& t) {
+  return w->fcost_valid && w->fcost_geom[0] == p->width && w->fcost_geom[1] == p->height && w->fcost_geom[2] == t.tw &&
+         w->fcost_geom[3] == t.th;
+}
+
+void set_fcost(rp_workspace* w, const rp_render_params* p, const Tiling& t, uint32_t ranks) {
+  w->fcost_valid = true;
+  const uint32_t geom[4] = {p->width, p->height, t.tw, t.th};
+  std::memcpy(w->fcost_geom, geom, sizeof geom);
+  w->fcost_ranks = ranks;
 }
 
 // The workspace's plan applies to frames of params' geometry (the render of this frame's shard made it).
@@ -376,6 +402,14 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
       if (!dalloc(&w->d_ctr_send, rpk::GATHER_CTR) || !dalloc(&w->d_ctr_gather, (uint64_t)rpk::GATHER_CTR * t.shards))
         return fail(RP_ENOMEM, "hipMalloc gather counters");
       w->ctr_ranks = t.shards;
+    }
+    const uint64_t mw = 2ull * t.shards * ((t.n_tiles + t.shards - 1) / t.shards);
+    if (mw > w->meas_g_words) {
+      dfree(w->d_meas_g);
+      w->d_meas_g = nullptr;
+      w->meas_g_words = 0;
+      if (!dalloc(&w->d_meas_g, mw)) return fail(RP_ENOMEM, "hipMalloc gather tile costs");
+      w->meas_g_words = mw;
     }
   }
   return RP_OK;
@@ -652,23 +686,39 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
                         tiles_y <= 256;
   rpk::TileGeom tg{t.tiles_x, kp.shard, kp.nshards, nullptr, 0, 0};
   uint32_t probe_px = 0;
-  bool frame_costs = false;
+  const uint32_t* frame_cost = nullptr;  // per-frame-tile costs (sum, max) the plan and the shard order use
   w->plan_on = false;
+  // Scheduling costs.  The megakernel measures every unit's duration into its tile's cost (kp.tile_meas); once a
+  // frame of this geometry has been rendered whole on one device, or gathered from all ranks, the workspace holds a
+  // learned per-tile table and the next frame schedules from it -- no probe launch.  For a balanced plan over
+  // N > 1 ranks the table must come from a gather over the same N ranks: every rank then holds the same bytes and
+  // deals the same plan.  Otherwise a probe (the first frame, the stage-split engine) supplies the costs.
+  const bool measure = s->opt.engine == RP_ENGINE_MEGAKERNEL;
+  const bool learned = measure && fcost_matches(w, p, t);
+  const uint32_t learned_px = t.tw * t.th * std::max(1u, t.nbatch);  // units per tile: sum / units = mean unit
   if (t.balanced) {
-    // RP_SHARD_BALANCED: probe the whole frame (deterministic costs, rp_device.h trav_step COUNT), and deal its tiles
-    // to the ranks by cost (rpk::launch_tile_plan) -- every rank computes the same plan from the same probe.  Scenes
-    // past the Infinity Cache (Z-order tiles, no cost order inside the shard) probe a sparser 4 x 4 lattice.
-    const uint32_t lattice = order_mode == RP_TILES_COST ? s->opt.probe_n : std::min(s->opt.probe_n, 4u);
-    if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
-    int e = rpk::launch_tile_plan(w->d_tile_cost, t.n_tiles, t.shards, w->d_plan, stream);
+    // RP_SHARD_BALANCED: deal the frame's tiles to the ranks by cost (rpk::launch_tile_plan).  Without a learned
+    // table, probe the whole frame (deterministic costs, rp_device.h trav_step COUNT); scenes past the Infinity
+    // Cache (Z-order tiles, no cost order inside the shard) probe a sparser 4 x 4 lattice.
+    if (learned && (t.shards == 1 || w->fcost_ranks == t.shards)) {
+      frame_cost = w->d_fcost;
+      probe_px = learned_px;
+    } else {
+      const uint32_t lattice = order_mode == RP_TILES_COST ? s->opt.probe_n : std::min(s->opt.probe_n, 4u);
+      if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
+      frame_cost = w->d_tile_cost;
+    }
+    int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, w->d_plan, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile plan launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_map = w->d_plan;
     tg.map = w->d_plan;
     tg.map_tiles = t.n_tiles;
-    frame_costs = true;
     w->plan_on = true;
     const uint32_t geom[5] = {p->width, p->height, t.tw, t.th, t.shards};
     std::memcpy(w->plan_geom, geom, sizeof geom);
+  } else if (learned) {
+    frame_cost = w->d_fcost;  // the shard order only: no agreement between ranks needed
+    probe_px = learned_px;
   }
   if (order_mode == RP_TILES_MORTON && sortable) {
     int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
@@ -676,13 +726,17 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     kp.tile_order = w->d_tile_order;
   }
   if (order_mode == RP_TILES_COST && sortable) {
-    // the shard's tiles by cost: from the frame probe of a balanced plan, else a probe of the shard
-    if (!frame_costs && (rc = probe(kp.shard, kp.nshards, t.n_shard_tiles, s->opt.probe_n, probe_px))) return rc;
-    tg.cost_by_tile = frame_costs ? 1u : 0u;
-    int e = rpk::launch_tile_sort(w->d_tile_cost, t.n_shard_tiles, probe_px, tg, w->d_tile_order, stream);
+    // the shard's tiles by cost: the learned table or the balanced plan's frame probe, else a probe of the shard
+    if (!frame_cost && (rc = probe(kp.shard, kp.nshards, t.n_shard_tiles, s->opt.probe_n, probe_px))) return rc;
+    tg.cost_by_tile = frame_cost ? 1u : 0u;
+    int e = rpk::launch_tile_sort(frame_cost ? frame_cost : w->d_tile_cost, t.n_shard_tiles, probe_px, tg,
+                                  w->d_tile_order, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
+  RP_HIP(hipMemsetAsync(w->d_meas, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
+  kp.tile_meas = measure ? w->d_meas : nullptr;
+  w->meas_on = measure;
   int e = s->opt.engine == RP_ENGINE_WAVEFRONT
               ? rpk::launch_wavefront(ks, kp, d_rgb, d_fg, ctr, w->d_queue, w->wf, (int)resident, stream)
               : rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
@@ -690,6 +744,13 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   if (kp.nbatch > 1) {
     e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);
     if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  // a whole frame on one device: its measured costs are the next frame's table (several ranks: the frame gather's)
+  if (measure && t.shards == 1 && t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX) {
+    e = rpk::launch_learn_costs(w->d_meas, w->d_meas + rpk::TILE_SORT_MAX, 0, 1, t.n_tiles, kp.tile_map, w->d_fcost,
+                                stream);
+    if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
+    set_fcost(w, p, t, 1);
   }
   return RP_OK;
 }
@@ -701,6 +762,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
 struct GatherPlan {
   Tiling t;
   uint64_t stride;  // slots per rank buffer
+  uint32_t stride_tiles;  // tiles per rank buffer (shard 0's count)
   rpk::FrameGeom geom;
   const uint32_t* plan_hash;  // the workspace's plan hash (balanced frames), NULL = interleave
 };
@@ -712,7 +774,9 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   if ((int)gp.t.shards != nranks || (int)gp.t.shard != rank)
     return fail(RP_EINVAL, "params.shard / num_shards must be the communicator's rank / size");
   gp.stride = stage_slots(gp.t);
-  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || (uint32_t)nranks > w->ctr_ranks)
+  gp.stride_tiles = (gp.t.n_tiles + gp.t.shards - 1) / gp.t.shards;
+  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || (uint32_t)nranks > w->ctr_ranks ||
+      2ull * nranks * gp.stride_tiles > w->meas_g_words)
     return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
   gp.geom.W = p->width;
   gp.geom.H = p->height;
@@ -752,8 +816,27 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
 // the BGRA8 and/or f64 shards (rp.h: every rank passes the same NULL / non-NULL outputs)
 int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb, hipStream_t st) {
   RP_NCCL(ncclAllGather(w->d_ctr_send, w->d_ctr_gather, rpk::GATHER_CTR, ncclUint64, comm, st));
+  // every rank's measured tile costs (sums, then maxima): the next frame's learned table, the same on every rank
+  const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
+  RP_NCCL(ncclAllGather(w->d_meas, w->d_meas_g, gp.stride_tiles, ncclUint32, comm, st));
+  RP_NCCL(ncclAllGather(w->d_meas + rpk::TILE_SORT_MAX, w->d_meas_g + n, gp.stride_tiles, ncclUint32, comm, st));
   if (bgra) RP_NCCL(ncclAllGather(w->d_gs_bgra, w->d_gather_bgra, gp.stride, ncclUint32, comm, st));
   if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
+  return RP_OK;
+}
+
+// (3a) the gathered tile costs -> the workspace's learned table (on every device of the frame)
+int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_render_params* p, hipStream_t st) {
+  DeviceGuard g(s->device);
+  if (!w->meas_on || gp.t.n_tiles > (uint32_t)rpk::TILE_SORT_MAX) {
+    w->fcost_valid = false;
+    return RP_OK;
+  }
+  const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
+  int e = rpk::launch_learn_costs(w->d_meas_g, w->d_meas_g + n, gp.stride_tiles, gp.geom.nranks, gp.t.n_tiles,
+                                  gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
+  if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
+  set_fcost(w, p, gp.t, gp.geom.nranks);
   return RP_OK;
 }
 
@@ -1088,6 +1171,42 @@ int rp_frame_assemble(const rp_render_params* p, const void* d_gathered, uint32_
   return RP_OK;
 }
 
+int rp_workspace_tile_costs(rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t* costs, uint32_t n) {
+  if (!s || !costs) return fail(RP_EINVAL, "scene and costs must be non-NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (n < 2 * t.n_shard_tiles) return fail(RP_EINVAL, "costs holds fewer than 2 x the shard's tiles");
+  if (!w->meas_on) return fail(RP_EINVAL, "the workspace's last render did not measure tile costs");
+  if (t.n_shard_tiles > (uint32_t)rpk::TILE_SORT_MAX) return fail(RP_EINVAL, "more than 16384 shard tiles");
+  DeviceGuard g(s->device);
+  RP_HIP(hipDeviceSynchronize());
+  RP_HIP(hipMemcpy(costs, w->d_meas, sizeof(uint32_t) * t.n_shard_tiles, hipMemcpyDeviceToHost));
+  RP_HIP(hipMemcpy(costs + t.n_shard_tiles, w->d_meas + rpk::TILE_SORT_MAX, sizeof(uint32_t) * t.n_shard_tiles,
+                   hipMemcpyDeviceToHost));
+  return RP_OK;
+}
+
+int rp_workspace_set_tile_costs(rp_scene* s, rp_workspace* w, const rp_render_params* p, const uint32_t* costs,
+                                uint32_t ranks) {
+  if (!s || !costs || ranks == 0) return fail(RP_EINVAL, "scene and costs must be non-NULL, ranks >= 1");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  if (t.n_tiles > (uint32_t)rpk::TILE_SORT_MAX) return fail(RP_EINVAL, "more than 16384 frame tiles");
+  DeviceGuard g(s->device);
+  RP_HIP(hipDeviceSynchronize());
+  RP_HIP(hipMemcpy(w->d_fcost, costs, sizeof(uint32_t) * t.n_tiles, hipMemcpyHostToDevice));
+  RP_HIP(hipMemcpy(w->d_fcost + rpk::TILE_SORT_MAX, costs + t.n_tiles, sizeof(uint32_t) * t.n_tiles,
+                   hipMemcpyHostToDevice));
+  set_fcost(w, p, t, ranks);
+  return RP_OK;
+}
+
 int rp_frame_assemble_ws(rp_scene* s, rp_workspace* w, const rp_render_params* p, const void* d_gathered,
                          uint32_t words, void* d_frame, void* stream) {
   if (!s) return fail(RP_EINVAL, "scene is NULL");
@@ -1169,6 +1288,7 @@ int rp_frame_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_pa
   DeviceGuard g(s->device);
   if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, rgb, d_counters, st))) return rc;
   if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, st))) return rc;
+  if ((rc = gather_learn(s, w, gp, p, st))) return rc;
   return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, d_counters, st);
 }
 
@@ -1286,6 +1406,10 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
     }
   }
   RP_NCCL(ncclGroupEnd());
+  for (int k = 0; k < n; k++) {
+    int rc = gather_learn(m->scenes[k], &m->scenes[k]->ws0, plans[k], &ps[k], m->streams[k]);
+    if (rc) return rc;
+  }
   rp_scene* s0 = m->scenes[0];
   int rc = gather_assemble(s0, &s0->ws0, plans[0], bgra ? reinterpret_cast<uint8_t*>(m->d_frame_bgra) : nullptr,
                            rgb ? m->d_frame_rgb : nullptr, m->d_ctr[0], m->streams[0]);

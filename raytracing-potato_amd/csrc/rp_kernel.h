@@ -76,6 +76,8 @@ struct KParams {
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
   const uint32_t* tile_map;    // the frame's tile deal order (RP_SHARD_BALANCED plan): shard tile k is frame tile
                                // tile_map[shard + k * nshards] (NULL = interleave: tile shard + k * nshards)
+  uint32_t* tile_meas;         // render (NULL = off): measured cost of shard tile k -- [k] its units' summed durations,
+                               // [TILE_SORT_MAX + k] the longest, in MEAS_SHIFT-scaled 100 MHz ticks (zeroed by the caller)
   uint32_t* tile_cost;         // probe: [k] cost (rp_device.h WORK_*: node visits, primitive tests, rays)
                                // summed over the tile's probed samples, [TILE_SORT_MAX + k] the costliest
                                // probed sample (zeroed by the caller)
@@ -90,6 +92,14 @@ struct KParams {
 // run sequentially on one lane, so one expensive unit fetched late becomes a latency-bound tail by itself.
 // Results do not depend on the order (per-pixel seeding).
 enum { PROBE_LATTICE_N = 16, TILE_SORT_MAX = 16384 };
+// Measured tile costs: unit durations in 100 MHz ticks >> MEAS_SHIFT (0.64 us): a C4 tile's 32768 units of ~100 us
+// sum to ~5e6, far from 2^32; the sort's log2 buckets of the longest unit stay below their cap up to ~40 ms.
+enum { MEAS_SHIFT = 6 };
+// Learned cost table: frame tile t's measured cost ([t] sum, [TILE_SORT_MAX + t] longest unit) from the measured
+// shard-tile costs of nranks ranks (rank r's [k] at sum[r * rank_stride + k], max[r * rank_stride + k]; shard tile k
+// of rank r is frame tile plan[r + k * nranks], or r + k * nranks without a plan).  One thread per tile.
+int launch_learn_costs(const uint32_t* sum, const uint32_t* max, uint32_t rank_stride, uint32_t nranks, uint32_t n_tiles,
+                       const uint32_t* plan, uint32_t* fcost, void* stream);
 
 // RNG streams per (pixel, batch of SPP_BATCH samples) -- include/rp.h RP_SAMPLES_PER_STREAM.  The queue
 // hands out units (pixel, batch), so one pixel's samples run on several lanes at once; a unit of a

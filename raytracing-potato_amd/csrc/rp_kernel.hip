@@ -230,6 +230,13 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             part[3 * u + 2] = sum_z;
             A->P.partial_hits[u] = hits;
           }
+          if (!PROBE && A->P.tile_meas) {  // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas)
+            const uint32_t t0 = reinterpret_cast<const uint32_t*>(rng.slab + RngT<RingFor<NF>>::meta)[0];
+            const uint32_t dur = ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0) >> MEAS_SHIFT;
+            const uint32_t k = slot / (A->P.tw * A->P.th);
+            atomicAdd(&A->P.tile_meas[k], dur);
+            atomicMax(&A->P.tile_meas[TILE_SORT_MAX + k], dur);
+          }
           ended_pixel = batch == 0;
           DIAG(if (!PROBE) {
             const uint32_t b = tbin(t_pix);
@@ -627,6 +634,24 @@ int launch_counters_stage(const uint64_t* ctr, const uint32_t* hash, uint64_t* s
 }
 int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t* out, void* stream) {
   hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, nranks, out);
+  return (int)hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) learn_costs_kernel(const uint32_t* __restrict__ sum, const uint32_t* __restrict__ mx,
+                                                         uint32_t rank_stride, uint32_t N, uint32_t n,
+                                                         const uint32_t* __restrict__ plan, uint32_t* __restrict__ fcost) {
+  const uint32_t pos = blockIdx.x * 256 + threadIdx.x;
+  if (pos >= n) return;
+  const uint32_t r = pos % N, k = pos / N, t = plan ? plan[pos] : pos;
+  fcost[t] = sum[r * rank_stride + k];
+  fcost[TILE_SORT_MAX + t] = mx[r * rank_stride + k];
+}
+
+int launch_learn_costs(const uint32_t* sum, const uint32_t* max, uint32_t rank_stride, uint32_t nranks, uint32_t n_tiles,
+                       const uint32_t* plan, uint32_t* fcost, void* stream) {
+  if (n_tiles == 0 || n_tiles > TILE_SORT_MAX || nranks == 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(learn_costs_kernel, dim3((n_tiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, sum, max,
+                     rank_stride, nranks, n_tiles, plan, fcost);
   return (int)hipGetLastError();
 }
 

@@ -127,7 +127,8 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_render_device_ws", "rp_shard_to_bgra8", "rp_srgb_thresholds", "rp_scene_options_init",
               "rp_scene_create_ex", "rp_workspace_reserve", "rp_comm_unique_id", "rp_comm_create", "rp_comm_destroy",
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
-              "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id"]
+              "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
+              "rp_workspace_tile_costs", "rp_workspace_set_tile_costs"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64"]
@@ -201,6 +202,8 @@ def rp() -> ctypes.CDLL:
                                     POINTER(rp_stats)]
     lib.rp_shard_unpack_map.argtypes = [POINTER(rp_render_params), c_void_p, c_void_p, c_uint32, c_void_p]
     lib.rp_workspace_tile_map.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
+    lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
+    lib.rp_workspace_set_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_frame_assemble_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32, c_void_p,
                                          c_void_p]
     if lib.rp_abi_version() != RP_ABI_VERSION:

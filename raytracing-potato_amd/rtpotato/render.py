@@ -103,6 +103,25 @@ class DeviceScene:
                                              out.ctypes.data, tiles))
         return out
 
+    def tile_costs(self, params: RenderParams, workspace: "Workspace | None" = None) -> np.ndarray:
+        """rp_workspace_tile_costs: (2, shard tiles) measured costs of the last render in `workspace` -- summed unit
+        durations per shard tile, then the longest unit."""
+        from .scene import shard_slot_count
+        n = shard_slot_count(params) // (params.tile_w * params.tile_h)
+        out = np.zeros(2 * max(n, 1), dtype=np.uint32)
+        p = params.to_c()
+        F.check(F.rp().rp_workspace_tile_costs(self.handle, workspace.handle if workspace else None, ctypes.byref(p),
+                                               out.ctypes.data, len(out)))
+        return out[:2 * n].reshape(2, n)
+
+    def set_tile_costs(self, params: RenderParams, costs: np.ndarray, ranks: int,
+                       workspace: "Workspace | None" = None) -> None:
+        """rp_workspace_set_tile_costs: install a frame's learned cost table, (2, frame tiles) by frame tile."""
+        c = np.ascontiguousarray(costs, dtype=np.uint32).reshape(-1)
+        p = params.to_c()
+        F.check(F.rp().rp_workspace_set_tile_costs(self.handle, workspace.handle if workspace else None,
+                                                   ctypes.byref(p), c.ctypes.data, ranks))
+
     # ---- synchronous host-buffer render -----------------------------------------------------------
     def render(self, params: RenderParams, camera=None, foreground: bool = False):
         """Full frame (only the shard's pixels written, others zero): (rgb (h, w, 3) f64,

@@ -190,3 +190,24 @@ def test_bench_refuses_overflowing_frame():
                        timeout=300, env=env, cwd=REPO)
     assert r.returncode != 0 and "status" in r.stderr, (r.returncode, r.stderr[-2000:])
     assert '"metric"' not in r.stdout
+
+
+def test_learned_tile_costs(gpu):
+    """The megakernel measures every unit's duration per tile; a whole-frame render leaves a learned table the next
+    frame schedules from (no probe) -- bitwise the same frame -- and an installed table (rp_workspace_set_tile_costs,
+    e.g. all-zero, or reversed) changes the order only, never a pixel."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    sc = scenes.configure(scenes.bunny_full(), 128, 96)
+    p = _params(128, 96, 8)
+    with gpu.DeviceScene(sc) as ds:
+        a, _, sa = ds.render(p)          # probe-ordered (fresh workspace), learns
+        costs = ds.tile_costs(p)
+        assert costs.shape == (2, 48) and (costs[0] > 0).all() and (costs[0] >= costs[1]).all()
+        b, _, sb = ds.render(p)          # scheduled from the learned table
+        ds.set_tile_costs(p, np.stack([costs[0][::-1], costs[1][::-1]]), 1)
+        c, _, sc_ = ds.render(p)
+        ds.set_tile_costs(p, np.zeros((2, 48), dtype=np.uint32), 1)
+        d, _, sd = ds.render(replace(p, shard_map=F.RP_SHARD_BALANCED))
+    assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
+    assert sa["rays"] == sb["rays"] == sc_["rays"] == sd["rays"]

@@ -9,12 +9,73 @@ the measurement.
 """
 import argparse
 import json
+
+import numpy as np
 import os
 import sys
 from dataclasses import replace
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "raytracing-potato_amd")]
+
+
+def learned_table(ds, params, n):
+    """The cost table an N-rank job learns from its first gathered frame: each shard rendered once (probe plan) in
+    its own workspace, its measured per-shard-tile costs placed at their frame tiles through the deal order."""
+    n_tiles = -(-params.width // params.tile_w) * -(-params.height // params.tile_h)
+    table = np.zeros((2, n_tiles), dtype=np.uint32)
+    for s in range(n):
+        sp = replace(params, shard=s, num_shards=n)
+        w = ds.workspace()
+        ds.reserve(sp, w)
+        ds.render_device_sync(sp, w) if hasattr(ds, "render_device_sync") else _render_ws(ds, sp, w)
+        order = ds.tile_map(sp, w)
+        c = ds.tile_costs(sp, w)
+        tiles = order[s::n][:c.shape[1]]
+        table[:, tiles] = c
+        w.close()
+    return table
+
+
+def _render_ws(ds, sp, w):
+    import torch
+    from rtpotato.scene import shard_slot_count
+    out = torch.zeros(3 * max(1, shard_slot_count(sp)), dtype=torch.float64, device="cuda")
+    ctr = torch.zeros(4, dtype=torch.int64, device="cuda")
+    ds.render_device(sp, out, ctr, workspace=w)
+    torch.cuda.synchronize()
+
+
+def inflight_time(ds, sp, F, frames, table=None):
+    """Steady per-frame time of shard sp with F frames in flight (bench.py's loop without the gather): frames
+    alternate over F streams and workspaces; one warm-up round, then `frames` frames timed together."""
+    import time
+    import torch
+    from rtpotato.scene import shard_slot_count
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev) for _ in range(F)]
+    wss = [ds.workspace() for _ in range(F)]
+    for w in wss:
+        ds.reserve(sp, w)
+        if table is not None:
+            ds.set_tile_costs(sp, table, sp.num_shards, w)
+    n = shard_slot_count(sp)
+    bufs = [torch.zeros(3 * max(1, n), dtype=torch.float64, device=dev) for _ in range(F)]
+    ctrs = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(F)]
+    for i in range(F):
+        ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(frames):
+        i = k % F
+        ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / frames
+    rays = int(ctrs[0][0])
+    assert all(int(c[3]) == 0 for c in ctrs)
+    for w in wss:
+        w.close()
+    return dt, rays
 
 
 def main():
@@ -24,6 +85,14 @@ def main():
     ap.add_argument("--tile", type=int, default=0, help="square tile size (default: the config's)")
     ap.add_argument("--maps", default="interleave,balanced")
     ap.add_argument("--reps", type=int, default=3, help="renders per shard; the shard's time is their median")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="frames in flight (> 1: each shard renders --frames frames on this many streams and "
+                         "workspaces, as bench.py does for N > 1; its time is the steady per-frame time)")
+    ap.add_argument("--frames", type=int, default=9)
+    ap.add_argument("--learned", type=int, default=1,
+                    help="1: schedule balanced N > 1 shards from a learned cost table (what every rank holds after "
+                         "its first gathered frame: the measured costs of all shards, combined through the deal order "
+                         "and installed with rp_workspace_set_tile_costs); 0: the whole-frame probe every frame")
     a = ap.parse_args()
     from rtpotato import scenes
     from rtpotato.render import DeviceScene
@@ -39,10 +108,19 @@ def main():
         per_n, t1 = {}, None
         for n in [int(x) for x in a.ns.split(",")]:
             times, rays = [], 0
+            table = learned_table(ds, replace(params, shard_map=smap), n) if a.learned and n > 1 and smap else None
             for s in range(n):
+                sp = replace(params, shard=s, num_shards=n, shard_map=smap)
+                if table is not None:
+                    ds.set_tile_costs(sp, table, n)
+                if a.inflight > 1:
+                    t, r = inflight_time(ds, sp, a.inflight, a.frames, table)
+                    times.append(t)
+                    rays += r
+                    continue
                 reps = []
                 for _ in range(a.reps):
-                    _, _, st = ds.render(replace(params, shard=s, num_shards=n, shard_map=smap))
+                    _, _, st = ds.render(sp)
                     reps.append(st["seconds"])
                 times.append(statistics.median(reps))
                 rays += st["rays"]
