@@ -206,11 +206,12 @@ enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
  * f32 frame (half the node bytes, more ALU per visit).  AUTO = Q8 for host-built trees of >= 2^21 hittables,
  * F32 otherwise. */
 enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2, RP_NODES_W8 = 3 };
-/* Tile orders: PLAIN = shard order (row-major); COST = a probe launch traces sample 0 of a lattice of pixels
- * per tile and the costliest tiles go first (short frame tail); MORTON = Z-order of the tiles (neighbouring
- * tiles run together: a small cache working set).  AUTO = COST while the scene fits the 256 MB Infinity
- * Cache, MORTON above. */
-enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON = 3 };
+/* Tile orders: PLAIN = shard order (row-major); COST = the costliest tiles go first (short frame tail), by the
+ * workspace's learned costs of the previous frame (see rp_workspace_tile_costs) or, without them, by a probe
+ * launch that traces sample 0 of a lattice of pixels per tile; PROBE = COST always from the probe; MORTON = Z-order
+ * of the tiles (neighbouring tiles run together: a small cache working set).  AUTO = COST while the scene fits
+ * the 256 MB Infinity Cache, MORTON above. */
+enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON = 3, RP_TILES_PROBE = 4 };
 /* Unit queues: SINGLE = one device-wide queue over the tile order; XCD_TILES = eight queues, one per group of
  * render blocks sharing an XCD (and its L2), tile k of the order served by queue k mod 8 (a tile's pixels
  * run on one XCD); XCD_REGIONS = queue g serves the g-th eighth of the tile order (a compact region per XCD

@@ -346,7 +346,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.always_max < 0) o.always_max = d.always_max;
   if (o.lds_depth != 0 && o.lds_depth < 8) return fail(RP_EINVAL, "options.lds_depth must be 0 or >= 8");
   if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
-  if (o.tile_order > RP_TILES_MORTON) return fail(RP_EINVAL, "options.tile_order must be RP_TILES_*");
+  if (o.tile_order > RP_TILES_PROBE) return fail(RP_EINVAL, "options.tile_order must be RP_TILES_*");
   if (o.probe_n == 0) o.probe_n = d.probe_n;
   if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
   if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
@@ -702,7 +702,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // N > 1 ranks the table must come from a gather over the same N ranks: every rank then holds the same bytes and
   // deals the same plan.  Otherwise a probe (the first frame, the stage-split engine) supplies the costs.
   const bool measure = s->opt.engine == RP_ENGINE_MEGAKERNEL;
-  const bool learned = measure && fcost_matches(w, p, t);
+  const bool probe_order = order_mode == RP_TILES_PROBE;
+  if (probe_order) order_mode = RP_TILES_COST;
+  const bool learned = measure && !probe_order && fcost_matches(w, p, t);
   const uint32_t learned_px = t.tw * t.th * std::max(1u, t.nbatch);  // units per tile: sum / units = mean unit
   if (t.balanced) {
     // RP_SHARD_BALANCED: deal the frame's tiles to the ranks by cost (rpk::launch_tile_plan).  Without a learned

@@ -29,7 +29,7 @@ RP_COMM_ID_BYTES = 128
 RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
 RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
-RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON = 0, 1, 2, 3
+RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 0, 1, 2, 3, 4
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2

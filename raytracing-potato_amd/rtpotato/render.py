@@ -17,7 +17,7 @@ def scene_options(**kw) -> F.rp_scene_options:
     """rp_scene_options with the library defaults (rp_scene_options_init), fields overridden by keyword:
     builder ("auto" | "host" | "gpu" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
     self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
-    node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton"), leaf_break,
+    node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
     unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*)."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
@@ -28,7 +28,7 @@ def scene_options(**kw) -> F.rp_scene_options:
             v = {"megakernel": F.RP_ENGINE_MEGAKERNEL, "wavefront": F.RP_ENGINE_WAVEFRONT}[v]
         if k == "tile_order" and isinstance(v, str):
             v = {"auto": F.RP_TILES_AUTO, "plain": F.RP_TILES_PLAIN, "cost": F.RP_TILES_COST,
-                 "morton": F.RP_TILES_MORTON}[v]
+                 "morton": F.RP_TILES_MORTON, "probe": F.RP_TILES_PROBE}[v]
         if k == "node_format" and isinstance(v, str):
             v = {"auto": F.RP_NODES_AUTO, "f32": F.RP_NODES_F32, "q8": F.RP_NODES_Q8, "w8": F.RP_NODES_W8}[v]
         if k == "unit_queues" and isinstance(v, str):
