@@ -55,9 +55,7 @@ int rph_bvh_selfcheck(const rp_scene_desc* desc, uint32_t node_format, uint64_t*
 
 /* CPU model of the device traversal over the same packed tree in `node_format` (diagnostics): for n rays
  * (layout of rp_intersect) writes n x 3 {node records visited, primitive tests, closest hittable id or
- * 2^64-1}.  node_format | RPH_NO_POP_CULL: without the Node4 kernel's pop-time culling of stack entries whose
- * t_near lies beyond the closest hit (rp_device.h stk_pop). */
-#define RPH_NO_POP_CULL 0x100u
+ * 2^64-1}. */
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
                             uint64_t* per_ray);
 

@@ -537,14 +537,6 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // test-only: a stack too small for the tree (the kernels flag RP_STATUS_STACK_OVERFLOW, never write past it)
   const bool debug_stack = opt.debug_stack_depth != 0;
   if (debug_stack) s->ks.stack_depth = opt.debug_stack_depth;
-  // stack words carry t_near (rp_device.h tn_pack) when a Node4 tree's entries fit 20 bits: inner node indices below
-  // 2^(P-1), leaf first primitives below 2^(P-4) (bunny: P = 17, t_near kept to 15 bits)
-  s->ks.pack_shift = 0;
-  if (node_format == rpl::NODES_F32) {
-    auto bits = [](uint64_t n) { uint32_t b = 0; while (b < 40 && (1ull << b) < n) b++; return b; };
-    const uint32_t P = std::max<uint32_t>(1 + bits(n_tree_nodes), 4 + bits(n_tree_prims + rpl::LEAF_MAX));
-    if (P <= 20) s->ks.pack_shift = std::max<uint32_t>(P, 8);
-  }
   s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;

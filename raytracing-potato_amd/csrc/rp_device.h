@@ -596,45 +596,6 @@ RPK_INLINE uint32_t stk_get(const KScene& S, const lds_u32* stk, uint32_t stride
   return spill_ptr(S)[spl + i - S.lds_depth];
 }
 
-// Culling at pop time (Node4 trees of small scenes, KScene::pack_shift = P != 0).  A stack word holds the entry
-// compressed into its low P bits -- an inner node index < 2^(P-1), or a leaf as bit P-1 | (count - 1) << (P-4) |
-// first primitive -- and, above them, the top 32 - P bits of the child's t_near (a non-negative f32, so its bits
-// order like its value: truncating them rounds t_near down).  A popped word whose t_near already lies beyond the
-// closest hit found since the push fails the slab test against the current best -- the test the node's own visit
-// would run on each of its children, whose boxes lie inside it -- so it is skipped without loading the node (with
-// the rounding-down, only words the full test would reject are skipped: no primitive the f64 test reaches is
-// culled).  Bunny (C3): 17 entry bits, t_near to 2^-6 relative; a CPU model of the traversal counts 16 % of node
-// visits on camera rays behind the hit (random 1 M-triangle mesh: 3 %).
-RPK_INLINE uint32_t tn_pack(uint32_t e, float tn, uint32_t P) {
-  const uint32_t lo = (1u << P) - 1u;
-  const uint32_t c = (e & rpl::ENTRY_LEAF)
-                         ? (1u << (P - 1u)) | (((e >> rpl::LEAF_SHIFT) & 7u) << (P - 4u)) | (e & rpl::LEAF_FIRST_MASK)
-                         : e;
-  return (__float_as_uint(tn) & ~lo) | (c & lo);
-}
-RPK_INLINE uint32_t tn_entry(uint32_t w, uint32_t P) {
-  const uint32_t c = w & ((1u << P) - 1u);
-  return (c >> (P - 1u)) ? rpl::ENTRY_LEAF | (((c >> (P - 4u)) & 7u) << rpl::LEAF_SHIFT) | (c & ((1u << (P - 4u)) - 1u))
-                         : c;
-}
-// the slab test's acceptance on t_near alone: beyond `best32`
-RPK_INLINE bool tn_beyond(uint32_t w, uint32_t P, float best32) {
-  return __builtin_fmaf(__uint_as_float(w & ~((1u << P) - 1u)), 1.0f - 0x1p-19f, -0x1p-100f) > best32;
-}
-// Pop the next entry (ENTRY_EMPTY when the stack is empty), skipping words beyond `best` when packed.
-template <bool SPILL, uint32_t NF>
-RPK_INLINE uint32_t stk_pop(const KScene& S, const lds_u32* stk, uint32_t stride, uint32_t spl, uint32_t& sp,
-                            double best) {
-  const uint32_t P = NF == rpl::NODES_F32 ? S.pack_shift : 0u;
-  if (P == 0u) return sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
-  const float best32 = f32_up(best);
-  while (sp) {
-    const uint32_t w = stk_get<SPILL>(S, stk, stride, spl, --sp);
-    if (!tn_beyond(w, P, best32)) return tn_entry(w, P);
-  }
-  return rpl::ENTRY_EMPTY;
-}
-
 // One step: descend until a leaf is held, test the leaves.  Finished when t.cur == ENTRY_EMPTY and no leaf is
 // parked (trav_done).  `spl`: the lane's first spill entry (SPILL kernels).  `work` (COUNT instantiations: the
 // cost probe) accumulates the lane's traversal work in WORK_* units.
@@ -885,22 +846,15 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
                            (uint32_t)(tn[3] != INFF);
     const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
-    uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1], e2 = cc[1];
-    if (NF == rpl::NODES_F32 && S.pack_shift) {  // t_near rides above the entry (stk_pop)
-      const uint32_t P = S.pack_shift;
-      const float t0 = k == 3u ? tn[3] : (k == 2u ? tn[2] : tn[1]), t1 = k == 3u ? tn[2] : tn[1];
-      e0 = tn_pack(e0, t0, P);
-      e1 = tn_pack(e1, t1, P);
-      e2 = tn_pack(e2, tn[1], P);
-    }
+    const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
     if (!SPILL || sp + 2u < S.lds_depth) {
       stk[sp * stride] = e0;
       stk[(sp + 1u) * stride] = e1;
-      stk[(sp + 2u) * stride] = e2;
+      stk[(sp + 2u) * stride] = cc[1];
     } else {
       stk_put<SPILL>(S, stk, stride, spl, sp, e0);
       stk_put<SPILL>(S, stk, stride, spl, sp + 1u, e1);
-      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, e2);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, cc[1]);
     }
     sp += k;
     if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
@@ -908,7 +862,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       sp = cap;
     }
     if (n_hit) cur = cc[0];
-    else cur = stk_pop<SPILL, NF>(S, stk, stride, spl, sp, best);
+    else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
     // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
     // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
@@ -916,7 +870,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     if constexpr (!COUNT) {
       if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
         leaf = cur;
-        cur = stk_pop<SPILL, NF>(S, stk, stride, spl, sp, best);
+        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
       }
       // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
       // last few descents ran with most of the wave idle (those lanes resume their descent next step)
@@ -925,7 +879,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
   }
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
-    cur = stk_pop<SPILL, NF>(S, stk, stride, spl, sp, best);
+    cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
   // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
@@ -940,7 +894,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     if (++k == kend) {
       if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
         leaf = cur;
-        cur = stk_pop<SPILL, NF>(S, stk, stride, spl, sp, best);
+        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
         k = leaf & rpl::LEAF_FIRST_MASK;
         kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
       } else {
@@ -1349,7 +1303,6 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.leaf_break = A->S.leaf_break;
   S.stack_depth = A->S.stack_depth;
   S.lds_depth = A->S.lds_depth;
-  S.pack_shift = A->S.pack_shift;
   S.spill = A->S.spill;
   S.rng_slab = A->S.rng_slab;
   return S;

@@ -422,8 +422,6 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   std::string err;
   int rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(err);
-  const bool no_cull = (node_format & RPH_NO_POP_CULL) != 0;
-  node_format &= ~RPH_NO_POP_CULL;
   rpb::PackedScene ps;
   rpb::BuildOptions bo;
   bo.node_format = node_format;
@@ -431,22 +429,6 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   if (rc != RP_OK) return fail(err);
   const bool q8 = ps.node_format != rpl::NODES_F32;  // Node4Q or Node8Q: the frame term
   const bool w8 = ps.node_format == rpl::NODES_W8;
-  // pop-time culling of the Node4 kernel (rp_device.h stk_pop; rp_api.cpp scene_create computes the same P): a
-  // stack entry's t_near, truncated to the bits above P, against the current closest hit
-  uint32_t P = 0;
-  if (!q8) {
-    auto bits = [](uint64_t v) { uint32_t b = 0; while (b < 40 && (1ull << b) < v) b++; return b; };
-    const uint32_t need = std::max<uint32_t>(1 + bits(ps.nodes.size()), 4 + bits(ps.prims.size() + rpl::LEAF_MAX));
-    if (need <= 20 && !no_cull) P = std::max<uint32_t>(need, 8);
-  }
-  auto tn_trunc = [P](float tn) {
-    uint32_t b;
-    std::memcpy(&b, &tn, 4);
-    b &= ~((1u << P) - 1u);
-    float f;
-    std::memcpy(&f, &b, 4);
-    return f;
-  };
   auto down = [](double x) { float f = (float)x; if ((double)f > x) f = std::nextafter(f, -INFINITY); return f; };
   auto up = [](double x) { float f = (float)x; if ((double)f < x) f = std::nextafter(f, INFINITY); return f; };
   for (uint64_t r = 0; r < n; r++) {
@@ -564,17 +546,6 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
       continue;
     }
     std::vector<uint32_t> stack;
-    std::vector<float> stack_tn;
-    auto pop = [&]() -> uint32_t {
-      while (!stack.empty()) {
-        const uint32_t e = stack.back();
-        const float t = stack_tn.back();
-        stack.pop_back();
-        stack_tn.pop_back();
-        if (P == 0 || !(std::fma(tn_trunc(t), 1.0f - 0x1p-19f, -0x1p-100f) > best32)) return e;
-      }
-      return rpl::ENTRY_EMPTY;
-    };
     uint32_t cur = ps.root;
     for (;;) {
       while (!(cur & rpl::ENTRY_LEAF)) {
@@ -629,16 +600,16 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
           for (int b = a + 1; b < 4; b++)
             if (tn[b] < tn[a]) { std::swap(tn[a], tn[b]); std::swap(cc[a], cc[b]); }
         for (int c = 3; c >= 1; c--)
-          if (tn[c] != INFINITY) {
-            stack.push_back(cc[c]);
-            stack_tn.push_back(tn[c]);
-          }
-        cur = tn[0] != INFINITY ? cc[0] : pop();
+          if (tn[c] != INFINITY) stack.push_back(cc[c]);
+        if (tn[0] != INFINITY) cur = cc[0];
+        else if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+        else { cur = stack.back(); stack.pop_back(); }
       }
       if (cur == rpl::ENTRY_EMPTY) break;
       const uint32_t first = cur & rpl::LEAF_FIRST_MASK, cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
       for (uint32_t k = first; k < first + cnt; k++) test(k);
-      cur = pop();
+      if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+      else { cur = stack.back(); stack.pop_back(); }
     }
     per_ray[3 * r] = visits;
     per_ray[3 * r + 1] = tests;

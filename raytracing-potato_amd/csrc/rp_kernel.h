@@ -23,8 +23,6 @@ struct KScene {
   uint32_t leaf_break;   // trav_step leaves the inner-node loop once at most this many lanes still seek a leaf
   uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
   uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
-  uint32_t pack_shift;   // Node4 trees whose entries fit pack_shift bits (rp_device.h tn_pack): stack words carry
-                         // the child's t_near above them and a pop skips entries beyond the closest hit; 0 = off
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
   uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
   uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) entries

@@ -204,34 +204,11 @@ def test_quantized_nodes_cost_few_extra_visits():
         res = []
         for fmt in FORMATS:
             out = np.zeros((len(rays), 3), dtype=np.uint64)
-            F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt | RPH_NO_POP_CULL,
-                                                          out.ctypes.data))
+            F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt, out.ctypes.data))
             res.append(out)
         assert (res[0][:, 2] == res[1][:, 2]).all()
         assert res[1][:, 0].mean() <= 1.05 * res[0][:, 0].mean()
         assert res[1][:, 1].mean() <= 1.10 * res[0][:, 1].mean()
-
-
-RPH_NO_POP_CULL = 0x100
-
-
-def test_pop_culling_skips_entries_beyond_the_hit():
-    """The Node4 kernel's stack words carry t_near (rp_device.h tn_pack / stk_pop): entries popped after a closer
-    hit was found are skipped without a visit.  The CPU model with and without it: identical closest hits on every
-    ray (the culling is conservative), and on the bunny >= 10 % fewer node visits."""
-    from rtpotato import _ffi as F
-    from rtpotato import scenes
-    for scene, gain in ((scenes.bunny_full(), 0.90), (scenes.random_mesh(200_000), 1.0)):
-        rays = _rays_for(scene, 20000, 7, adversarial=True)
-        d = scene.desc()
-        res = []
-        for fmt in (1, 1 | RPH_NO_POP_CULL):
-            out = np.zeros((len(rays), 3), dtype=np.uint64)
-            F.check_host(F.host().rph_bvh_traversal_stats(d.ptr(), rays.ctypes.data, len(rays), fmt, out.ctypes.data))
-            res.append(out)
-        assert (res[0][:, 2] == res[1][:, 2]).all()
-        assert res[0][:, 0].mean() <= gain * res[1][:, 0].mean(), (res[0][:, 0].mean(), res[1][:, 0].mean())
-        assert (res[0][:, 1] <= res[1][:, 1]).all()
 
 
 def test_quantized_frames_refuse_huge_coordinates():
