@@ -171,6 +171,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
 
     n_rays += (uint64_t)__popcll(__ballot(alive && tdone));
     bool ended_sample = false, ended_pixel = false;
+    uint32_t meas_k = 0xFFFFFFFFu, meas_dur = 0u;  // a unit ended: its shard tile and duration
     if (alive && tdone) {
       DIAG(active++;)
       DREG(DREG_SHADE)
@@ -230,12 +231,12 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             part[3 * u + 2] = sum_z;
             A->P.partial_hits[u] = hits;
           }
-          if (!PROBE && A->P.tile_meas) {  // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas)
+          // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas), from one unit in eight (pixel and
+          // batch hashed: every tile's sample spread over its pixels and batches) -- timing all units cost 0.9 %
+          if (!PROBE && A->P.tile_meas && ((pipj ^ (pipj >> 16) ^ batch ^ (pipj >> 3)) & 7u) == 0u) {
             const uint32_t t0 = reinterpret_cast<const uint32_t*>(rng.slab + RngT<RingFor<NF>>::meta)[0];
-            const uint32_t dur = ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0) >> MEAS_SHIFT;
-            const uint32_t k = slot / (A->P.tw * A->P.th);
-            atomicAdd(&A->P.tile_meas[k], dur);
-            atomicMax(&A->P.tile_meas[TILE_SORT_MAX + k], dur);
+            meas_dur = ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0) >> MEAS_SHIFT;
+            meas_k = slot / (A->P.tw * A->P.th);
           }
           ended_pixel = batch == 0;
           DIAG(if (!PROBE) {
@@ -272,6 +273,32 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     }
     n_samples += (uint64_t)__popcll(__ballot(ended_sample));
     n_pixels += (uint64_t)__popcll(__ballot(ended_pixel));
+    if (!PROBE) {
+      // Tile costs: the wave's units that ended this round mostly belong to one tile (a wave fetches consecutive
+      // units), so the wave sums and maxes their durations for the first ending lane's tile and adds them with one
+      // atomic each -- 64 lanes' atomics on one word serialise in L2 -- and the rare lanes of other tiles add their own.
+      const uint64_t em = __ballot(meas_k != 0xFFFFFFFFu);
+      if (em != 0) {
+        const uint32_t lead = (uint32_t)__builtin_ctzll(em);
+        const uint32_t k0 = __builtin_amdgcn_readlane(meas_k, lead);
+        const bool mine = meas_k == k0;
+        uint32_t sum = mine ? meas_dur : 0u, mx = sum;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+          sum += __shfl_xor(sum, off);
+          mx = max(mx, (uint32_t)__shfl_xor(mx, off));
+        }
+        uint32_t* meas = kargs()->P.tile_meas;
+        if ((threadIdx.x & 63u) == lead) {
+          atomicAdd(&meas[k0], sum);
+          atomicMax(&meas[TILE_SORT_MAX + k0], mx);
+        }
+        if (meas_k != 0xFFFFFFFFu && !mine) {
+          atomicAdd(&meas[meas_k], meas_dur);
+          atomicMax(&meas[TILE_SORT_MAX + meas_k], meas_dur);
+        }
+      }
+    }
     DIAG({ uint64_t t = stamp(); ph[3] += t - t_prev; t_prev = t; })
   }
 
