@@ -197,7 +197,9 @@ typedef struct rp_render_params {
 /* Scene build and kernel tuning options (rp_scene_create_ex).  None of them changes an image beyond
  * exact-t ties between primitives (the closest hit does not depend on the tree).
  * Zero-initialised fields take the defaults; rp_scene_options_init fills them in explicitly. */
-enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2 };
+/* Builders: HOST = multi-threaded binned SAH on the CPU; DEVICE = LBVH on the GPU (Karras 2012: fastest build,
+ * Morton-split tree); PLOC = agglomerative clustering on the GPU (Meister & Bittner 2018: SAH-quality tree). */
+enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2, RP_BUILDER_PLOC = 3 };
 /* Render engines (same images bit for bit): the persistent megakernel (traversal and shading on the same
  * lanes) and the stage-split engine (trace and shade passes over a pool of path slots; its renders
  * synchronise the host: the pass loop polls the ray queue). */
@@ -219,7 +221,7 @@ enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON
 enum { RP_QUEUES_AUTO = 0, RP_QUEUES_SINGLE = 1, RP_QUEUES_XCD_TILES = 2, RP_QUEUES_XCD_REGIONS = 3 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
-                               build, ~24 % slower traversal on 10 M triangles) */
+                               build, ~24 % slower traversal on 10 M triangles); PLOC */
   uint32_t max_leaf;        /* primitives per leaf, 1..8 (0 -> 4) */
   double cost_traverse;     /* SAH node cost relative to a primitive test (0 -> 0.7) */
   int32_t always_max;       /* primitives tested before the tree for every ray (-1 -> 4; 0 = none) */
@@ -269,6 +271,12 @@ void rp_scene_destroy(rp_scene* scene);
 /* Acceleration-structure statistics: node count, leaf count, max depth, primitive count. */
 int rp_scene_info(const rp_scene* scene, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth,
                   uint64_t* n_prims, uint64_t* device_bytes);
+
+/* Host wall-clock seconds of rp_scene_create's phases: {validation, host tree (or the shading tables alone for a
+ * device build), device builder input (primitive records and boxes), device build (or the host tree's upload),
+ * vertex/shading tables upload, workspace}.  RP_BUILD_PHASES values; n may be smaller. */
+#define RP_BUILD_PHASES 6
+int rp_scene_build_times(const rp_scene* scene, double* seconds, uint32_t n);
 
 /* Number of pixels in shard params->shard (the length of the compact shard buffer). */
 int rp_shard_pixel_count(const rp_render_params* params, uint64_t* count);

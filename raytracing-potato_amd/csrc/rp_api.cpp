@@ -147,6 +147,7 @@ struct rp_scene {
   rp_workspace ws0;            // the scene's own workspace (rp_render, rp_render_device)
   int n_workspaces = 0;        // live workspaces from rp_workspace_create
   uint64_t n_nodes = 0, n_leaves = 0, n_prims = 0, device_bytes = 0;
+  double build_s[RP_BUILD_PHASES] = {0};  // rp_scene_build_times
   uint32_t tiles_auto = RP_TILES_COST;  // the tile order of RP_TILES_AUTO (scene_create)
   uint32_t max_depth = 0;
   int num_cu = 0;
@@ -338,7 +339,7 @@ rp_scene_options default_options() {
 int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   const rp_scene_options d = default_options();
   o = in ? *in : d;
-  if (o.builder > RP_BUILDER_DEVICE) return fail(RP_EINVAL, "options.builder must be RP_BUILDER_*");
+  if (o.builder > RP_BUILDER_PLOC) return fail(RP_EINVAL, "options.builder must be RP_BUILDER_*");
   if (o.max_leaf == 0) o.max_leaf = d.max_leaf;
   if (o.max_leaf > rpl::LEAF_MAX) return fail(RP_EINVAL, "options.max_leaf must be 1..8");
   if (o.cost_traverse == 0.0) o.cost_traverse = d.cost_traverse;
@@ -426,6 +427,14 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   int rc = resolve_options(opt_in, opt);
   if (rc) return rc;
   std::string err;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto lap = [t = t_start]() mutable {
+    const auto now = std::chrono::steady_clock::now();
+    const double d = std::chrono::duration<double>(now - t).count();
+    t = now;
+    return d;
+  };
+  double phase[RP_BUILD_PHASES] = {0};
   rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(rc, err);
   int ndev = 0;
@@ -438,9 +447,13 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
 
   rpb::PackedScene ps;
   rpb::BuildOptions bo;
-  // AUTO = the host binned SAH at every size: on C5 (10 M triangles) it builds in 2.8 s with 16 threads
-  // (the device LBVH: 1.1 s) and renders 24 % faster; the LBVH stays an option.
-  const bool gpu_build = opt.builder == RP_BUILDER_DEVICE;
+  // AUTO = the device PLOC build for scenes of >= 2^21 hittables (C5, 10 M triangles: its tree renders within
+  // 1.5 % of the host binned SAH's and builds in a fraction of the host's 2.7 s), the host binned
+  // SAH below (small scenes build in milliseconds, and only the host keeps always-tested primitives out of the
+  // tree) and for 8-wide nodes; the LBVH stays an option (fastest build, ~46 % slower tree on C5).
+  if (opt.builder == RP_BUILDER_AUTO && desc->n_hittables >= rpb::Q8_MIN_PRIMS && opt.node_format != RP_NODES_W8)
+    opt.builder = RP_BUILDER_PLOC;
+  const bool gpu_build = opt.builder == RP_BUILDER_DEVICE || opt.builder == RP_BUILDER_PLOC;
   const bool use_gpu = gpu_build && desc->n_hittables >= 2;  // the LBVH needs two primitives
   if (gpu_build && opt.node_format == RP_NODES_W8)
     return fail(RP_EINVAL, "the device builder makes 4-wide trees (options.node_format RP_NODES_F32 or RP_NODES_Q8)");
@@ -449,8 +462,10 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   bo.cost_traverse = opt.cost_traverse;
   bo.always_max = (uint32_t)opt.always_max;
   bo.node_format = opt.node_format;  // RP_NODES_AUTO (0) resolved by the builder
+  phase[0] = lap();
   rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(rc, err);
+  phase[1] = lap();
 
   DeviceGuard g(device);
   rp_scene* s = new rp_scene();
@@ -463,9 +478,14 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   if (use_gpu) {
     rpb::PrimInput pin;
     if ((rc = rpb::prim_input(desc, pin, err))) return bail(fail(rc, err));
-    node_format = opt.node_format ? opt.node_format : rpl::NODES_F32;  // AUTO: f32 for the LBVH (rp_bvh.h)
+    phase[2] = lap();
+    // AUTO: f32 for the LBVH (rp_bvh.h); the PLOC tree has the SAH tree's node count, so the host trees' size rule
+    node_format = opt.node_format ? opt.node_format
+                  : opt.builder == RP_BUILDER_PLOC ? rpb::auto_node_format(desc->n_hittables, pin.amax)
+                                                   : (uint32_t)rpl::NODES_F32;
     rpg::GpuTree gt;
-    if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, gt, err))) return bail(fail(rc, err));
+    const uint32_t algo = opt.builder == RP_BUILDER_PLOC ? rpg::GPU_PLOC : rpg::GPU_LBVH;
+    if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, algo, opt.cost_traverse, gt, err))) return bail(fail(rc, err));
     s->d_nodes = gt.d_nodes;
     s->d_prims = gt.d_prims;
     s->d_prim_refs = gt.d_prim_refs;
@@ -506,6 +526,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
              (rc = upload(ps.prim_refs, &s->d_prim_refs))) {
     return bail(rc);
   }
+  phase[3] = lap();  // the device build, or the host tree's upload
   if ((rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
       (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
@@ -573,7 +594,10 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
     if (rpk::render_blocks_per_cu(opt.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   }
   s->blocks_per_cu = bpc;
+  phase[4] = lap();
   if ((rc = ws_alloc(s, &s->ws0))) return bail(rc);
+  phase[5] = lap();
+  std::memcpy(s->build_s, phase, sizeof phase);
   *out = s;
   return RP_OK;
 }
@@ -926,6 +950,12 @@ int rp_scene_create_ex(const rp_scene_desc* desc, int device, const rp_scene_opt
 
 int rp_scene_create(const rp_scene_desc* desc, int device, rp_scene** out) {
   return scene_create(desc, device, nullptr, out);
+}
+
+int rp_scene_build_times(const rp_scene* s, double* seconds, uint32_t n) {
+  if (!s || (!seconds && n)) return fail(RP_EINVAL, "NULL argument");
+  for (uint32_t i = 0; i < n; i++) seconds[i] = i < (uint32_t)RP_BUILD_PHASES ? s->build_s[i] : 0.0;
+  return RP_OK;
 }
 
 int rp_scene_info(const rp_scene* s, uint64_t* n_nodes, uint64_t* n_leaves, uint32_t* max_depth, uint64_t* n_prims,

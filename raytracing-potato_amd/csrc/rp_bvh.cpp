@@ -998,17 +998,42 @@ int prim_input(const rp_scene_desc* d, PrimInput& out, std::string& err) {
     out.cmax[k] = -std::numeric_limits<double>::infinity();
   }
   out.amax = 0.0;
-  for (uint32_t i = 0; i < n; i++) {
-    pack_prim(d, vbase, i, out.prims[i], out.refs[i]);
-    const Box b = hittable_box(d, d->hittables[i]);
-    for (int k = 0; k < 3; k++) {
-      out.boxes[6 * (size_t)i + k] = b.lo[k];
-      out.boxes[6 * (size_t)i + 3 + k] = b.hi[k];
-      out.amax = std::fmax(out.amax, std::fmax(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
-      const double c = 0.5 * (b.lo[k] + b.hi[k]);
-      out.cmin[k] = std::fmin(out.cmin[k], c);
-      out.cmax[k] = std::fmax(out.cmax[k], c);
+  // chunks on up to 16 threads (the per-chunk bounds merge by min / max: the same values as one pass)
+  const unsigned T = n >= (1u << 16) ? std::max(1u, std::min(16u, std::thread::hardware_concurrency())) : 1u;
+  std::vector<double> part(7 * (size_t)T);
+  auto run = [&](unsigned t) {
+    const uint32_t lo = (uint32_t)((uint64_t)n * t / T), hi = (uint32_t)((uint64_t)n * (t + 1) / T);
+    double cmn[3] = {INFINITY, INFINITY, INFINITY}, cmx[3] = {-INFINITY, -INFINITY, -INFINITY}, am = 0.0;
+    for (uint32_t i = lo; i < hi; i++) {
+      pack_prim(d, vbase, i, out.prims[i], out.refs[i]);
+      const Box b = hittable_box(d, d->hittables[i]);
+      for (int k = 0; k < 3; k++) {
+        out.boxes[6 * (size_t)i + k] = b.lo[k];
+        out.boxes[6 * (size_t)i + 3 + k] = b.hi[k];
+        am = std::fmax(am, std::fmax(std::fabs(b.lo[k]), std::fabs(b.hi[k])));
+        const double c = 0.5 * (b.lo[k] + b.hi[k]);
+        cmn[k] = std::fmin(cmn[k], c);
+        cmx[k] = std::fmax(cmx[k], c);
+      }
     }
+    double* q = &part[7 * (size_t)t];
+    for (int k = 0; k < 3; k++) { q[k] = cmn[k]; q[3 + k] = cmx[k]; }
+    q[6] = am;
+  };
+  if (T == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; t++) th.emplace_back(run, t);
+    for (auto& x : th) x.join();
+  }
+  for (unsigned t = 0; t < T; t++) {
+    const double* q = &part[7 * (size_t)t];
+    for (int k = 0; k < 3; k++) {
+      out.cmin[k] = std::fmin(out.cmin[k], q[k]);
+      out.cmax[k] = std::fmax(out.cmax[k], q[3 + k]);
+    }
+    out.amax = std::fmax(out.amax, q[6]);
   }
   return RP_OK;
 }

@@ -101,7 +101,11 @@ struct GpuTree {
   double qbound = 0.0;
 };
 
-// LBVH (Karras 2012) + wide collapse on the current device.  Needs >= 2 primitives.
-int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, GpuTree& out, std::string& err);
+// Device builds on the current device (>= 2 primitives), then the wide collapse: GPU_LBVH = Karras 2012 (Morton
+// bits split), GPU_PLOC = Meister & Bittner 2018 (agglomerative, SAH quality).
+enum { GPU_LBVH = 0, GPU_PLOC = 1 };
+// cost_traverse: the SAH node cost relative to a primitive test (PLOC's leaf decisions; rp_scene_options).
+int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, uint32_t algo, double cost_traverse,
+              GpuTree& out, std::string& err);
 
 }  // namespace rpg

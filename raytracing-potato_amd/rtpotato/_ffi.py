@@ -26,7 +26,7 @@ RP_ROOT_BVH, RP_ROOT_LIST = 0, 1
 RP_COUNTERS_LEN = 4  # device counter block: rays, samples, pixels, status (include/rp.h)
 RP_SAMPLES_PER_STREAM = 32
 RP_COMM_ID_BYTES = 128
-RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE = 0, 1, 2
+RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE, RP_BUILDER_PLOC = 0, 1, 2, 3
 RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
 RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 0, 1, 2, 3, 4
@@ -128,7 +128,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_scene_create_ex", "rp_workspace_reserve", "rp_comm_unique_id", "rp_comm_create", "rp_comm_destroy",
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
               "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
-              "rp_workspace_tile_costs", "rp_workspace_set_tile_costs"]
+              "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64"]
@@ -202,6 +202,7 @@ def rp() -> ctypes.CDLL:
                                     POINTER(rp_stats)]
     lib.rp_shard_unpack_map.argtypes = [POINTER(rp_render_params), c_void_p, c_void_p, c_uint32, c_void_p]
     lib.rp_workspace_tile_map.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
+    lib.rp_scene_build_times.argtypes = [c_void_p, c_void_p, c_uint32]
     lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_workspace_set_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_frame_assemble_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32, c_void_p,

@@ -15,7 +15,7 @@ from .scene import RenderParams, Scene, shard_slot_count
 
 def scene_options(**kw) -> F.rp_scene_options:
     """rp_scene_options with the library defaults (rp_scene_options_init), fields overridden by keyword:
-    builder ("auto" | "host" | "gpu" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
+    builder ("auto" | "host" | "gpu" (LBVH) | "ploc" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
     self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
     node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
     unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*)."""
@@ -23,7 +23,8 @@ def scene_options(**kw) -> F.rp_scene_options:
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
         if k == "builder" and isinstance(v, str):
-            v = {"auto": F.RP_BUILDER_AUTO, "host": F.RP_BUILDER_HOST, "gpu": F.RP_BUILDER_DEVICE}[v]
+            v = {"auto": F.RP_BUILDER_AUTO, "host": F.RP_BUILDER_HOST, "gpu": F.RP_BUILDER_DEVICE,
+                 "ploc": F.RP_BUILDER_PLOC}[v]
         if k == "engine" and isinstance(v, str):
             v = {"megakernel": F.RP_ENGINE_MEGAKERNEL, "wavefront": F.RP_ENGINE_WAVEFRONT}[v]
         if k == "tile_order" and isinstance(v, str):
@@ -60,6 +61,13 @@ class DeviceScene:
                                      ctypes.byref(np_), ctypes.byref(nb)))
         return {"nodes": nn.value, "leaves": nl.value, "max_depth": md.value, "prims": np_.value,
                 "device_bytes": nb.value}
+
+    def build_times(self) -> dict:
+        """rp_scene_build_times: host seconds of the scene_create phases."""
+        t = np.zeros(6)
+        F.check(F.rp().rp_scene_build_times(self.handle, t.ctypes.data, 6))
+        return dict(zip(("validate", "host_tree", "device_input", "device_build_or_upload", "tables_upload",
+                         "workspace"), t.round(4).tolist()))
 
     def close(self) -> None:
         for w in list(getattr(self, "_workspaces", ())):

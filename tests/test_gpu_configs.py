@@ -53,10 +53,10 @@ def test_c4_shard_of_8(gpu, shard):
 def test_c5_10m_triangles(gpu):
     """Config C5 at its real size and sample count -- 10 M random triangles, 4096x4096 at 256 spp (8 RNG batches per
     pixel: the 3.7 GB batch-sum workspace, the q8 kernel's 4-block keystream ring wrapping) -- through the default
-    tree (host SAH, 64 B quantized nodes) and the spilling traversal stack.  The oracle's reference median-split
-    tree over all 10 M triangles re-renders 2 sampled tiles at 256 spp (parity bar, and exact ray counts against
-    the GPU's re-render of the same tiles); 20 k rays are intersected ray by ray over the default tree, the device
-    LBVH in both node formats and the host 8-wide tree."""
+    tree (the AUTO builder: the device PLOC build at this size, 64 B quantized nodes) and the spilling traversal
+    stack.  The oracle's reference median-split tree over all 10 M triangles re-renders 2 sampled tiles at 256 spp
+    (parity bar, and exact ray counts against the GPU's re-render of the same tiles); 20 k rays are intersected ray
+    by ray over the default tree, the device LBVH in both node formats, the host SAH tree and the host 8-wide tree."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     scene, params = scenes.config_scene("C5")
@@ -72,16 +72,17 @@ def test_c5_10m_triangles(gpu):
     with gpu.DeviceScene(scene) as ds:
         info = ds.info()
         assert info["prims"] == 10_000_000 and info["max_depth"] >= 12  # 43+ stack entries: the SPILL kernel
+        bt = ds.build_times()
+        assert bt["host_tree"] + bt["device_input"] + bt["device_build_or_upload"] < 5.0, bt  # PLOC, not host SAH
         rgb, _, st = ds.render(params)
         assert st["pixels"] == 4096 * 4096 and st["samples"] == 4096 * 4096 * 256 and np.isfinite(rgb).all()
         assert 1.0 < st["rays"] / st["samples"] < 8.0
         results = [ds.intersect(rays)]
         _sampled_shard_parity(gpu, scene, rgb, sub, ds=ds)
-    for fmt in ("f32", "q8"):
-        with gpu.DeviceScene(scene, options={"builder": "gpu", "node_format": fmt}) as ds:
+    for opt in ({"builder": "gpu", "node_format": "f32"}, {"builder": "gpu", "node_format": "q8"},
+                {"builder": "host"}, {"node_format": "w8"}):  # w8: the host 8-wide tree
+        with gpu.DeviceScene(scene, options=opt) as ds:
             results.append(ds.intersect(rays))
-    with gpu.DeviceScene(scene, options={"node_format": "w8"}) as ds:  # the host 8-wide tree
-        results.append(ds.intersect(rays))
     desc = scene.desc()
     os_ = O.OracleScene(desc.addr(), desc)
     ref_hits, ref_mats, _ = os_.intersect(rays)

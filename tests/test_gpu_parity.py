@@ -188,17 +188,17 @@ def test_render_device_torch(gpu):
 
 
 @pytest.mark.parametrize("fmt", ["f32", "q8", "w8"])
-@pytest.mark.parametrize("builder", ["host", "gpu"])
+@pytest.mark.parametrize("builder", ["host", "gpu", "ploc"])
 def test_intersect_rays(gpu, builder, fmt):
     """Hittable::hit on the root, ray by ray: t, position, normal, uv, material identical to the oracle --
-    over the host SAH tree and the device-built LBVH (rp_scene_options.builder), with f32 or 8-bit quantized
-    child boxes, 4-wide or (host trees) 8-wide (rp_scene_options.node_format)."""
+    over the host SAH tree and the device-built LBVH and PLOC trees (rp_scene_options.builder), with f32 or 8-bit
+    quantized child boxes, 4-wide or (host trees) 8-wide (rp_scene_options.node_format)."""
     from oracle import oracle_py as O
     from rtpotato import scenes
     from rtpotato import _ffi as F
-    if builder == "gpu" and fmt == "w8":  # the device builder makes 4-wide trees only: refused, not substituted
+    if builder != "host" and fmt == "w8":  # the device builders make 4-wide trees only: refused, not substituted
         with pytest.raises(F.RPError, match="4-wide"):
-            gpu.DeviceScene(scenes.bunny_full(), options={"builder": "gpu", "node_format": "w8"})
+            gpu.DeviceScene(scenes.bunny_full(), options={"builder": builder, "node_format": "w8"})
         return
     rng = np.random.default_rng(5)
     scene = scenes.bunny_full()
@@ -300,18 +300,20 @@ def test_workspaces_frames_in_flight(gpu):
 
 
 @pytest.mark.parametrize("fmt", ["f32", "q8"])
-@pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000), ("three_balls", None)])
-def test_device_bvh_builder(gpu, name, arg, fmt):
-    """Scenes over the device-built tree (rp_bvh_gpu.hip: LBVH + wide collapse) in both node formats, with
-    the host builder's structural self-check on the downloaded tree (options.self_check): same image and ray
-    counts as the oracle."""
+@pytest.mark.parametrize("builder", ["gpu", "ploc"])
+@pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000), ("three_balls", None),
+                                      ("one_triangle", None)])
+def test_device_bvh_builder(gpu, name, arg, fmt, builder):
+    """Scenes over the device-built trees (rp_bvh_gpu.hip: LBVH or PLOC, then the wide collapse) in both node
+    formats, with the host builder's structural self-check on the downloaded tree (options.self_check): same image
+    and ray counts as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
-    opt = {"builder": "gpu", "self_check": 1, "node_format": fmt}
+    opt = {"builder": builder, "self_check": 1, "node_format": fmt}
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
     with gpu.DeviceScene(sc, options=opt) as ds:
         info = ds.info()
-        assert info["nodes"] >= 1 and (info["max_depth"] >= 4 or name == "three_balls")
+        assert info["nodes"] >= 1 and (info["max_depth"] >= 4 or name in ("three_balls", "one_triangle"))
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 

@@ -45,7 +45,7 @@ def main():
         info = ds.info()
         ds.render(replace(params, spp=1, width=256, height=256))
         _, _, st = ds.render(params)
-        out[spec] = {"scene_create_s": round(setup, 3), "info": info, "frame_s": round(st["seconds"], 4),
+        out[spec] = {"scene_create_s": round(setup, 3), "phases_s": ds.build_times(), "info": info, "frame_s": round(st["seconds"], 4),
                   "mrays_s": round(st["rays"] / st["seconds"] / 1e6, 1), "rays": st["rays"]}
         print(f"[bvh] {spec}: {out[spec]}", file=sys.stderr, flush=True)
         ds.close()

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--shards", type=int, default=1, help="render shard 0 of N (per-rank work of an N-GPU run)")
+    ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value")
     a = ap.parse_args()
     os.environ.setdefault("RP_LIB", os.path.join(REPO, "raytracing-potato_amd", "lib", "librp_diag.so"))
     from dataclasses import replace
@@ -24,7 +25,11 @@ def main():
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
     params = replace(params, spp=a.spp, shard=0, num_shards=a.shards)
-    ds = DeviceScene(scene)
+    opts = {}
+    for kv in a.opt:
+        k, v = kv.split("=", 1)
+        opts[k] = float(v) if k == "cost_traverse" else (v if not v.lstrip("-").isdigit() else int(v))
+    ds = DeviceScene(scene, options=opts)
     ds.render(replace(params, spp=1))  # warm
     buf = (ctypes.c_uint64 * 320)()
     F.check(F.rp().rp_diagnostics(ds.handle, buf, 320, 1))
