@@ -458,6 +458,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   if (gpu_build && opt.node_format == RP_NODES_W8)
     return fail(RP_EINVAL, "the device builder makes 4-wide trees (options.node_format RP_NODES_F32 or RP_NODES_Q8)");
   bo.tables_only = use_gpu;
+  bo.vertex_tables = false;  // uploaded straight from the meshes below
   bo.max_leaf = opt.max_leaf;
   bo.cost_traverse = opt.cost_traverse;
   bo.always_max = (uint32_t)opt.always_max;
@@ -527,8 +528,18 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
     return bail(rc);
   }
   phase[3] = lap();  // the device build, or the host tree's upload
-  if ((rc = upload(ps.vnrm, &s->d_vnrm)) || (rc = upload(ps.vuv, &s->d_vuv)) ||
-      (rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
+  // vertex normals and uvs (read at a closest hit), mesh after mesh from the caller's arrays: no host copy
+  uint64_t n_vert = 0;
+  for (uint32_t i = 0; i < desc->n_meshes; i++) n_vert += desc->meshes[i].n_vertices;
+  if (!dalloc(&s->d_vnrm, 3 * n_vert + 3) || !dalloc(&s->d_vuv, 2 * n_vert + 2)) return bail(fail(RP_ENOMEM, "hipMalloc vertex tables"));
+  for (uint64_t i = 0, vb = 0; i < desc->n_meshes; vb += desc->meshes[i].n_vertices, i++) {
+    const rp_mesh& m = desc->meshes[i];
+    if (!m.n_vertices) continue;
+    if (hipMemcpy(s->d_vnrm + 3 * vb, m.normals, sizeof(double) * 3 * m.n_vertices, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(s->d_vuv + 2 * vb, m.uvs, sizeof(double) * 2 * m.n_vertices, hipMemcpyHostToDevice) != hipSuccess)
+      return bail(fail(RP_EHIP, "vertex table upload"));
+  }
+  if ((rc = upload(ps.materials, &s->d_mats)) || (rc = upload(ps.textures, &s->d_texs)) ||
       (rc = upload(ps.texels, &s->d_texels)))
     return bail(rc);
   if (!dalloc(&s->d_diag, rpk::DIAG_N) || hipMemset(s->d_diag, 0, sizeof(uint64_t) * rpk::DIAG_N) != hipSuccess)
@@ -563,7 +574,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->n_prims = desc->n_hittables;
   s->max_depth = ps.max_depth;
   s->device_bytes = rp_node_bytes(node_format) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
-                    sizeof(double) * (ps.vnrm.size() + ps.vuv.size()) + sizeof(rpl::Material) * ps.materials.size() +
+                    sizeof(double) * 5 * n_vert + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
   // Cache-resident scenes (C3: 11 MB) gain ~15 % from cost-ordered tiles (short frame tail); a scene past the
   // 256 MB Infinity Cache (C5: 2.5 GB) loses 5-7 % to any reordering that scatters the concurrently rendered

@@ -760,9 +760,11 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
   std::vector<uint64_t> vbase(d->n_meshes + 1, 0);
   for (uint32_t i = 0; i < d->n_meshes; i++) vbase[i + 1] = vbase[i] + d->meshes[i].n_vertices;
   if (vbase[d->n_meshes] > 0xffffffffull) { err = "too many vertices"; return RP_EINVAL; }
-  out.vnrm.resize(3 * vbase[d->n_meshes] + 3);
-  out.vuv.resize(2 * vbase[d->n_meshes] + 2);
-  for (uint32_t i = 0; i < d->n_meshes; i++) {
+  if (opt.vertex_tables) {
+    out.vnrm.resize(3 * vbase[d->n_meshes] + 3);
+    out.vuv.resize(2 * vbase[d->n_meshes] + 2);
+  }
+  for (uint32_t i = 0; i < d->n_meshes && opt.vertex_tables; i++) {
     const rp_mesh& m = d->meshes[i];
     // vertex runs in parallel chunks (C5: 30 M vertices, 1.2 GB)
     parallel_for(m.n_vertices, threads, [&](size_t b, size_t e) {

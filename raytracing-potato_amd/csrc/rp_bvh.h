@@ -8,6 +8,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -22,6 +23,7 @@ struct BuildOptions {
   double cost_traverse = 0.7;   // relative cost of one node (two child boxes); C3 sweep 0.35-1.5: 0.7 best (-1..2 %)
   double cost_intersect = 1.0;  // relative cost of one primitive test
   bool tables_only = false;     // shading tables only (nodes/prims left empty: the device builder makes them)
+  bool vertex_tables = true;    // vnrm / vuv (false: the caller uploads the meshes' normals and uvs itself)
   // Primitives kept out of the tree and tested first for every ray: among the always_max largest boxes
   // (surface area), those at least always_ratio times the area of the box of everything else (config C3's
   // ground sphere, r = 1000 under a bunny of size ~0.2).  always_max = 0 disables.
@@ -73,10 +75,22 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
 
 // Primitive records in hittable order (Prim, PrimRef with src = hittable id), their exact f64 boxes
 // (hittable.rs:124-147; lo xyz, hi xyz) and the bounds of the box centroids: the device builder's input.
+// A heap array without value-initialisation (PrimInput: 1.4 GB for 10 M triangles, filled in parallel)
+template <class T>
+struct RawArray {
+  std::unique_ptr<T[]> p;
+  size_t n = 0;
+  void resize(size_t k) { p.reset(new T[k]); n = k; }
+  size_t size() const { return n; }
+  T* data() { return p.get(); }
+  const T* data() const { return p.get(); }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
 struct PrimInput {
-  std::vector<rpl::Prim> prims;
-  std::vector<rpl::PrimRef> refs;
-  std::vector<double> boxes;  // 6 per primitive
+  RawArray<rpl::Prim> prims;
+  RawArray<rpl::PrimRef> refs;
+  RawArray<double> boxes;  // 6 per primitive
   double cmin[3], cmax[3];
   double amax;                // largest |coordinate| of the boxes (NaN ignored)
 };
