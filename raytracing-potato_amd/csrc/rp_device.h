@@ -60,9 +60,21 @@ __shared__ unsigned long long g_dreg[2 * DREG_N];
       atomicAdd(&g_dreg[2 * (r) + 1], (unsigned long long)__popcll(ex_));             \
     }                                                                                  \
   }
+// wave-cycles spent executing a code region (its lanes active, the others masked): s_memtime around it, added by
+// the wave's first active lane into g_dcyc[r] (flushed to diag[DIAG_CYC + r] at the kernel's end)
+__shared__ unsigned long long g_dcyc[DCYC_N];
+#define DCYC_BEGIN(v) const uint64_t v = stamp();
+#define DCYC_END(r, v)                                                                 \
+  {                                                                                    \
+    const uint64_t ex_ = __builtin_amdgcn_read_exec();                                 \
+    const uint64_t d_ = stamp() - (v);                                                 \
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex_)) atomicAdd(&g_dcyc[r], (unsigned long long)d_); \
+  }
 #else
 #define DIAG(...)
 #define DREG(r)
+#define DCYC_BEGIN(v)
+#define DCYC_END(r, v)
 #endif
 
 static constexpr int BLOCK = RENDER_BLOCK;
@@ -1178,8 +1190,10 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
   bool sph_uv;
   if (hit) {
     DREG(DREG_SURF)
+    DCYC_BEGIN(c0)
     sph_uv = surface(S, hr, o, d, h);
     m = &S.mats[h.material];
+    DCYC_END(DCYC_SURF, c0)
   } else {
     DREG(DREG_MISS)
     // background.evaluate(ray, Hit::at_infinity(dir)) (render.rs:118,144; utility.rs:93-100)
@@ -1192,9 +1206,11 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
   }
   if (sph_uv) {  // hittable.rs:59-62 for a sphere hit, utility.rs:96-97 for a miss
     DREG(DREG_SPHUV)
+    DCYC_BEGIN(c1)
     const V3 q = hit ? h.n : d;
     h.u = 0.5 - atan2(q.z, q.x) / TAU_;
     h.v = asin(q.y) / PI_ + 0.5;
+    DCYC_END(DCYC_SPHUV, c1)
   }
   // Textures: each lane reads at most one here -- the absorb map of a hit or the sky sphere of a miss
   // (or of an emissive hit); its Checker walk and Image texel load are issued BEFORE the scatter so
@@ -1207,6 +1223,7 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
   // a miss under an Image sky sphere: size and offset are kernel arguments (scalar registers), so the
   // texel load waits on no texture-table load
   const bool sky_img = !hit && S.background.img_w != 0;
+  DCYC_BEGIN(c2)
   if (t1) {
     if (sky_img) {
       rpl::Texture t;
@@ -1221,11 +1238,17 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
       if (t.kind == 3) px1 = texel(S, image_texel(t, h));
     }
   }
+  DCYC_END(DCYC_TEXISSUE, c2)
   // scatter (the only RNG consumer; material.rs order scatter, absorb, emit -- the textures draw none)
   V3 nd = v3(0.0, 0.0, 0.0);
   bool scattered = false;
-  if (hit) scattered = scatter_eval(*m, d, h, rng, nd);
+  if (hit) {
+    DCYC_BEGIN(c3)
+    scattered = scatter_eval(*m, d, h, rng, nd);
+    DCYC_END(DCYC_SCATTER, c3)
+  }
   V3 tex_ab = v3(0.0, 0.0, 0.0), tex_em = v3(0.0, 0.0, 0.0);
+  DCYC_BEGIN(c4)
   if (t1) {
     DREG(DREG_TEX)
     const V3 tv = sky_img ? v3(u8_unit(px1 & 0xffu), u8_unit((px1 >> 8) & 0xffu), u8_unit((px1 >> 16) & 0xffu))
@@ -1234,6 +1257,8 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
     else tex_em = tv;
   }
   if (ta && te) tex_em = tex_sample(S, emit_tex, h);
+  DCYC_END(DCYC_TEXVAL, c4)
+  DCYC_BEGIN(c5)
   const double* ecol = hit ? m->emit_color : S.background.color;
   const V3 em = emit_eval(emit_kind, v3(ecol[0], ecol[1], ecol[2]), tex_em, d, h);
   // emit + absorb (*) trace_path_continue (render.rs:108-115, 135-142), accumulated forward: each
@@ -1251,6 +1276,7 @@ RPK_INLINE bool shade_ray(const KScene& S, const HitRec& hr, V3& o, V3& d, R& rn
     o = h.p;
     d = nd;
   }
+  DCYC_END(DCYC_EMIT, c5)
   return scattered;
 }
 

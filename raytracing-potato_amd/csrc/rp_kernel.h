@@ -36,7 +36,13 @@ enum { RENDER_BLOCK = 256 };
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
 // lane primitive tests.
-enum { DIAG_N = 320 };
+enum { DIAG_N = 352 };
+// Cycle regions (RPK_DIAG builds), from DIAG_N index DIAG_CYC: wave-cycles spent executing each code region
+enum { DIAG_CYC = 320 };
+enum {
+  DCYC_SURF, DCYC_SPHUV, DCYC_TEXISSUE, DCYC_SCATTER, DCYC_TEXVAL, DCYC_EMIT, DCYC_START_SAMPLE, DCYC_END_SAMPLE,
+  DCYC_NEWRAY, DCYC_REFILL, DCYC_NEXT_BOUNCE, DCYC_N
+};
 // Timeline histograms (RPK_DIAG builds), 64 bins of DIAG_BIN_TICKS (100 MHz real-time clock) from the
 // block's start: [64 + b] lanes retiring in bin b, [128 + b] rays of the pixels fetched in bin b,
 // [192 + b] pixels fetched in bin b, [256 + b] the most rays of one unit fetched in bin b.

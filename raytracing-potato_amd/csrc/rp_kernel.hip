@@ -41,6 +41,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
        if (threadIdx.x < BLOCK / 64 * 8) wmax[threadIdx.x / 8][threadIdx.x % 8] = 0;)
   if (threadIdx.x < 3) blk_ctr[threadIdx.x] = 0;
   DIAG(if (threadIdx.x < 2 * DREG_N) g_dreg[threadIdx.x] = 0;)
+  DIAG(if (threadIdx.x < DCYC_N) g_dcyc[threadIdx.x] = 0;)
   // frame timeline (100 MHz real-time clock, comparable across XCDs): first block start, first failed
   // pixel fetch (queue drained), last wave exit -- minima stored bit-inverted so atomicMax serves both
   DIAG(if (!PROBE && threadIdx.x == 0) atomicMax(&kargs()->diag[10], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());)
@@ -118,11 +119,15 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
     {
       KArgsPtr A = kargs();
       const uint64_t seed = unit_seed(A, pipj & 0xFFFFu, pipj >> 16, batch);  // RNG contract
+      DCYC_BEGIN(cr)
       rng_refill(rng, alive, fresh, seed, start ? s - 1 : s, unit_spp(A, batch));
+      DCYC_END(DCYC_REFILL, cr)
     }
     if (start) {
       KArgsPtr A = kargs();
+      DCYC_BEGIN(cs)
       start_sample(rng, s, pipj & 0xFFFFu, pipj >> 16, o, d);
+      DCYC_END(DCYC_START_SAMPLE, cs)
       depth = A->P.max_bounce;
       T_x = T_y = T_z = 1.0;
       first = true;
@@ -141,11 +146,13 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       // camera rays and scattered rays started since the last round: the always-tested primitives (trav_begin),
       // at one site for both
       if (newray) {
+        DCYC_BEGIN(cn)
         double best = ts.best;
         for (uint32_t k = S.always_first; k < S.always_first + S.n_always; k++)
           prim_test(S, k, o, d, RAY_EPSILON, best, ts);
         ts.best = best;
         newray = false;
+        DCYC_END(DCYC_NEWRAY, cn)
       }
       Ray32 r;
       setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
@@ -202,6 +209,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       // ---- end of a camera sample: accumulate (main.rs:80), maybe finish the pixel, start the next
       if (end_sample) {
         DREG(DREG_END_SAMPLE)
+        DCYC_BEGIN(ce)
         KArgsPtr A = kargs();
         s++;
         ended_sample = true;
@@ -265,10 +273,13 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           }
         }
         start = alive;  // next round, after the refill pass
+        DCYC_END(DCYC_END_SAMPLE, ce)
       } else {
+        DCYC_BEGIN(cb)
         trav_init<NF>(load_scene(kargs()), INF, ts, d);
         tdone = false;
         newray = true;
+        DCYC_END(DCYC_NEXT_BOUNCE, cb)
       }
     }
     n_samples += (uint64_t)__popcll(__ballot(ended_sample));
@@ -321,6 +332,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       atomicAdd(&dg[7], wmax[w][6]);
     }
     if (threadIdx.x < 2 * DREG_N) atomicAdd(&dg[16 + threadIdx.x], g_dreg[threadIdx.x]);
+    if (threadIdx.x < DCYC_N) atomicAdd(&dg[DIAG_CYC + threadIdx.x], g_dcyc[threadIdx.x]);
     if (!PROBE && (threadIdx.x & 63) == 0) atomicMax(&dg[12], (unsigned long long)__builtin_amdgcn_s_memrealtime());
     if (!PROBE) atomicAdd(&dg[64 + tbin(t_retire)], 1ull);
   }

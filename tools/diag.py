@@ -31,10 +31,10 @@ def main():
         opts[k] = float(v) if k == "cost_traverse" else (v if not v.lstrip("-").isdigit() else int(v))
     ds = DeviceScene(scene, options=opts)
     ds.render(replace(params, spp=1))  # warm
-    buf = (ctypes.c_uint64 * 320)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 320, 1))
+    buf = (ctypes.c_uint64 * 352)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 352, 1))
     _, _, st = ds.render(params)
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 320, 1))
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, 352, 1))
     d = list(buf)
     ph = d[:5]
     tot = sum(ph)
@@ -63,6 +63,9 @@ def main():
         name: {"wave_execs_per_kray": round(1000 * d[16 + 2 * i] / st["rays"], 2),
                "lane_util": round(d[17 + 2 * i] / max(1, 64 * d[16 + 2 * i]), 3)}
         for i, name in enumerate(regions)}
+    cyc = ["surface", "sph_uv", "tex_issue", "scatter", "tex_value", "emit_accum", "start_sample", "end_sample",
+           "newray_always", "refill", "next_bounce"]
+    out["cycle_share"] = {name: round(d[320 + i] / tot, 4) for i, name in enumerate(cyc)}
     # timeline histograms (10 ms bins from each block's start): lanes retiring, pixels fetched and their rays
     last = max([b for b in range(64) if d[64 + b] or d[192 + b]] or [0])
     out["timeline_10ms"] = [{"t_ms": 10 * b, "retired_lanes": d[64 + b], "pixels": d[192 + b],
