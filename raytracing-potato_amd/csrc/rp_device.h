@@ -859,7 +859,10 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
                            (uint32_t)(tn[3] != INFF);
     const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
     const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
-    if (!SPILL || sp + 2u < S.lds_depth) {
+    // Whether every lane's pushes and pops of this visit stay in the LDS part of its stack: a wave-uniform branch
+    // (SPILL kernels), so the common case runs no per-lane exec-mask juggling for the spill path.
+    const bool lds_only = !SPILL || __ballot(sp + 2u >= S.lds_depth) == 0;
+    if (lds_only) {
       stk[sp * stride] = e0;
       stk[(sp + 1u) * stride] = e1;
       stk[(sp + 2u) * stride] = cc[1];
@@ -873,8 +876,13 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       overflow = true;
       sp = cap;
     }
+    // pops below read entries < the pushes' top (sp + 2 before the push), so an LDS-only visit pops from LDS
+    const auto pop = [&]() -> uint32_t {
+      --sp;
+      return lds_only ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
+    };
     if (n_hit) cur = cc[0];
-    else cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+    else cur = sp ? pop() : rpl::ENTRY_EMPTY;
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
     // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
     // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
@@ -882,16 +890,23 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     if constexpr (!COUNT) {
       if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
         leaf = cur;
-        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+        cur = sp ? pop() : rpl::ENTRY_EMPTY;
       }
       // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
       // last few descents ran with most of the wave idle (those lanes resume their descent next step)
       if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
     }
   }
+  // the pops from here on only shrink sp: when no lane's stack reaches into its spill run, they all read LDS (a
+  // wave-uniform branch, as in the node loop)
+  const bool lds_pop = !SPILL || __ballot(sp > S.lds_depth) == 0;
+  const auto pop = [&]() -> uint32_t {
+    --sp;
+    return lds_pop ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
+  };
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
-    cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+    cur = sp ? pop() : rpl::ENTRY_EMPTY;
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
   // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
@@ -906,7 +921,7 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     if (++k == kend) {
       if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
         leaf = cur;
-        cur = sp ? stk_get<SPILL>(S, stk, stride, spl, --sp) : rpl::ENTRY_EMPTY;
+        cur = sp ? pop() : rpl::ENTRY_EMPTY;
         k = leaf & rpl::LEAF_FIRST_MASK;
         kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
       } else {

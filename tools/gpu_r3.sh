@@ -21,7 +21,7 @@ for s in ${STEPS:-tests}; do
   case $s in
     tests)
       step tests
-      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
+      timeout -k 10 ${TESTS_LIMIT:-1200} python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -p no:cacheprovider \
         ${PYTEST_ARGS:-} > gpurun_out/${TAG}_tests.log 2>&1 || { step "tests failed"; exit 1; } ;;
     bench_*)
       cfg=${s#bench_}; st=10; wu=2; [ $cfg = C5 ] && st=3 && wu=1
