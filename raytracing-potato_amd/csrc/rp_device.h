@@ -881,17 +881,38 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
       --sp;
       return lds_only ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
     };
-    if (n_hit) cur = cc[0];
-    else cur = sp ? pop() : rpl::ENTRY_EMPTY;
     // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
     // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
     // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
     // every rank of a balanced multi-GPU frame computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
-    if constexpr (!COUNT) {
-      if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
-        leaf = cur;
-        cur = sp ? pop() : rpl::ENTRY_EMPTY;
+    if (lds_only) {
+      // the next entry without a branch: the two entries under the top are read at once (indices clamped into the
+      // column; an entry below the stack's bottom is read but never taken), then the pop for a visit that hit no
+      // child and the pop behind a parked leaf are selects
+      const uint32_t t1 = stk[min(sp - 1u, sp) * stride], t2 = stk[min(sp - 2u, sp) * stride];
+      uint32_t npop = (!n_hit && sp) ? 1u : 0u;
+      uint32_t c = n_hit ? cc[0] : (sp ? t1 : rpl::ENTRY_EMPTY);
+      if constexpr (!COUNT) {
+        const bool park = (c & rpl::ENTRY_LEAF) && c != rpl::ENTRY_EMPTY && leaf == 0u;
+        const uint32_t left = sp - npop;
+        leaf = park ? c : leaf;
+        const uint32_t c2 = left ? (npop ? t2 : t1) : rpl::ENTRY_EMPTY;
+        npop += (park && left) ? 1u : 0u;
+        c = park ? c2 : c;
       }
+      cur = c;
+      sp -= npop;
+    } else {
+      if (n_hit) cur = cc[0];
+      else cur = sp ? pop() : rpl::ENTRY_EMPTY;
+      if constexpr (!COUNT) {
+        if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+          leaf = cur;
+          cur = sp ? pop() : rpl::ENTRY_EMPTY;
+        }
+      }
+    }
+    if constexpr (!COUNT) {
       // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
       // last few descents ran with most of the wave idle (those lanes resume their descent next step)
       if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "97d47940ee42244b"
+#define RP_BUILD_ID "2cbb61fcbc0f507c"
