@@ -31,7 +31,7 @@ struct KScene {
 // Bytes of keystream cache (ChaCha key, ring of main-stream blocks, jitter blocks) per resident lane of
 // the render kernel; the render grid never exceeds the lanes the slab was sized for.
 uint64_t rng_slab_bytes_per_lane();
-enum { RENDER_BLOCK = 256 };
+enum { RENDER_BLOCK = 64 };
 
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "2cbb61fcbc0f507c"
+#define RP_BUILD_ID "bf2f1ca6e02a35e1"
