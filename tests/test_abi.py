@@ -136,3 +136,18 @@ def test_product_kernel_has_no_experiment_switches():
         r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-E", f"-D{macro}", src, "-o", os.devnull],
                            capture_output=True, text=True)
         assert r.returncode != 0 and "experiment macros" in r.stderr, macro
+
+
+def test_profile_records_are_of_this_build():
+    """bench.py prices its roofline with the per-ray records profiles/current.json names and refuses a record of
+    another build; the committed records must be the ones of the kernel the committed sources build (rp_build_id
+    hashes the render kernel's code object), so a kernel change cannot ship with stale records."""
+    import json
+    from rtpotato import _ffi as F
+    build = F.rp().rp_build_id().decode()
+    cur = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"]
+    assert set(cur) >= {"C3", "C5"}
+    for cfg, rel in cur.items():
+        rec = json.load(open(os.path.join(REPO, rel)))
+        assert rec["build_id"] == build, (cfg, rel, rec["build_id"], build)
+        assert rec["config"] == cfg and rec["rays"] > 0 and rec["traffic_bytes_per_ray"] > 0
