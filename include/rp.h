@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 5
+#define RP_ABI_VERSION 6
 
 /* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -219,6 +219,10 @@ enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON
  * run on one XCD); XCD_REGIONS = queue g serves the g-th eighth of the tile order (a compact region per XCD
  * under Z-order).  A drained queue's blocks take units from the others.  AUTO = XCD_TILES. */
 enum { RP_QUEUES_AUTO = 0, RP_QUEUES_SINGLE = 1, RP_QUEUES_XCD_TILES = 2, RP_QUEUES_XCD_REGIONS = 3 };
+/* How the binary SAH tree is collapsed into 4-wide nodes (host builder; ABI v6): AUTO = SAH; GREEDY opens the child
+ * of largest surface area until a node has 4 children; SAH takes the cut through the binary subtree that minimises
+ * the 4-wide tree's SAH cost (dynamic program).  Never changes an image beyond exact-t ties. */
+enum { RP_COLLAPSE_AUTO = 0, RP_COLLAPSE_GREEDY = 1, RP_COLLAPSE_SAH = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles); PLOC */
@@ -242,6 +246,7 @@ typedef struct rp_scene_options {
   uint32_t debug_stack_depth; /* TESTS ONLY (0 = off): traversal-stack entries per lane, 8..4096, instead of the
                                depth the tree needs.  Too small a stack drops entries -- wrong frames -- and the
                                render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */
+  uint32_t collapse;        /* RP_COLLAPSE_*: the 4-wide collapse of the host-built tree (ABI v6) */
 } rp_scene_options;
 
 typedef struct rp_stats {

@@ -358,6 +358,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.queue_chunk > 4096) return fail(RP_EINVAL, "options.queue_chunk must be 0..4096");
   if (o.debug_stack_depth != 0 && (o.debug_stack_depth < 8 || o.debug_stack_depth > 4096))
     return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
+  if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
   return RP_OK;
 }
 
@@ -462,6 +463,7 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   bo.max_leaf = opt.max_leaf;
   bo.cost_traverse = opt.cost_traverse;
   bo.always_max = (uint32_t)opt.always_max;
+  bo.collapse = opt.collapse == RP_COLLAPSE_GREEDY ? rpb::COLLAPSE_GREEDY : rpb::COLLAPSE_SAH;
   bo.node_format = opt.node_format;  // RP_NODES_AUTO (0) resolved by the builder
   phase[0] = lap();
   rc = rpb::build(desc, bo, ps, err);

@@ -393,8 +393,82 @@ void node_frame(const Box& b, N& n) {
   }
 }
 
+// SAH-optimal choice of a wide node's children (BuildOptions::collapse = COLLAPSE_SAH): the cut through the
+// binary subtree under a wide node that minimises the SAH cost of the 4-wide tree (the dynamic program of
+// Ylitie et al. 2017 §3, restricted to the binary tree's own leaves).  For a binary node n:
+//   E(n)    = its cost as ONE child entry: leaf  A(n) * count * c_prim;  inner  A(n) * c_node + G(n)
+//   G(n)    = min_{i=1..3} F(l, i) + F(r, 4 - i)        (the wide node of n: its 4 slots over l and r)
+//   F(n, j) = min( min_{i=1..j-1} F(l, i) + F(r, j - i),  E(n) )   (n covered by at most j entries)
+// A is the surface area (the parent-relative hit probability up to a constant), c_node / c_prim the builder's
+// cost_traverse / cost_intersect.  The greedy rule below (open the largest-area child) fills every slot but
+// may spend a slot where a deeper level saves more.  Ties go to the split (a shallower tree), then to the
+// smaller i, so the plan is a function of the binary tree alone (any thread count builds the same tree).
+struct CollapsePlan {
+  // per binary node: choice[j - 1] for j = 1..4 slots: 0 = one entry (n itself), i = i slots to l, j - i to r
+  std::vector<uint8_t> choice;
+  void build(const std::vector<BinNode>& bin, double c_node, double c_prim) {
+    const size_t n = bin.size();
+    std::vector<double> F(4 * n);
+    choice.assign(4 * n, 0);
+    // post-order without recursion: children before parents
+    std::vector<int32_t> stack, post;
+    post.reserve(n);
+    stack.push_back(0);
+    while (!stack.empty()) {
+      const int32_t v = stack.back();
+      stack.pop_back();
+      post.push_back(v);
+      if (!bin[v].leaf()) { stack.push_back(bin[v].left); stack.push_back(bin[v].right); }
+    }
+    for (size_t q = post.size(); q-- > 0;) {
+      const int32_t v = post[q];
+      const BinNode& b = bin[v];
+      double* f = &F[4 * (size_t)v];
+      uint8_t* c = &choice[4 * (size_t)v];
+      const double a = b.box.area();
+      if (b.leaf()) {
+        for (int j = 0; j < 4; j++) { f[j] = a * (double)b.count * c_prim; c[j] = 0; }
+        continue;
+      }
+      const double* fl = &F[4 * (size_t)b.left];
+      const double* fr = &F[4 * (size_t)b.right];
+      double g = std::numeric_limits<double>::infinity();
+      uint8_t gi = 1;
+      for (int i = 1; i <= 3; i++)
+        if (fl[i - 1] + fr[3 - i] < g) { g = fl[i - 1] + fr[3 - i]; gi = (uint8_t)i; }
+      const double e = a * c_node + g;
+      f[0] = e;
+      c[0] = gi << 4;  // j = 1: n is one entry; the high nibble keeps G's split (n's own wide node)
+      for (int j = 2; j <= 4; j++) {
+        double best = std::numeric_limits<double>::infinity();
+        uint8_t bi = 1;
+        for (int i = 1; i < j; i++)
+          if (fl[i - 1] + fr[j - i - 1] < best) { best = fl[i - 1] + fr[j - i - 1]; bi = (uint8_t)i; }
+        if (e < best) { best = e; bi = 0; }
+        f[j - 1] = best;
+        c[j - 1] = bi;
+      }
+    }
+  }
+  // the wide node of inner binary node bi: its children (binary node ids) in left-to-right order
+  int kids(const std::vector<BinNode>& bin, int32_t bi, int32_t out[4]) const {
+    int nk = 0;
+    const int g = choice[4 * (size_t)bi] >> 4;
+    expand(bin, bin[bi].left, g, out, nk);
+    expand(bin, bin[bi].right, 4 - g, out, nk);
+    return nk;
+  }
+  void expand(const std::vector<BinNode>& bin, int32_t v, int j, int32_t out[4], int& nk) const {
+    const int i = bin[v].leaf() ? 0 : (choice[4 * (size_t)v + (size_t)(j - 1)] & 15);
+    if (i == 0) { out[nk++] = v; return; }
+    expand(bin, bin[v].left, i, out, nk);
+    expand(bin, bin[v].right, j - i, out, nk);
+  }
+};
+
 // Collapse the binary tree into 4-wide nodes: each wide node takes its binary node's two children and
-// repeatedly opens the inner child of largest surface area until it has 4 children (Wald et al.).
+// repeatedly opens the inner child of largest surface area until it has 4 children (Wald et al.), or
+// (COLLAPSE_SAH) takes the SAH-optimal cut of CollapsePlan.
 // The wide nodes are written in the scene's node format (child boxes from the exact f64 boxes).
 // Numbering: the inner children of a node are consecutive records (a family), and families are laid out
 // depth-first -- a ray that enters several children of a node reads neighbouring records (the same or
@@ -408,6 +482,7 @@ struct Collapser {
   std::vector<rpl::Node4> nodes;
   std::vector<rpl::Node4Q> qnodes;
   uint32_t max_depth = 0;
+  const CollapsePlan* plan = nullptr;  // COLLAPSE_SAH (else the greedy largest-area rule)
 
   uint32_t size() const { return (uint32_t)(fmt == rpl::NODES_Q8 ? qnodes.size() : nodes.size()); }
   uint32_t* child(uint32_t i) { return fmt == rpl::NODES_Q8 ? qnodes[i].child : nodes[i].child; }
@@ -438,6 +513,8 @@ struct Collapser {
     int nk = 0;
     if (bin[bi].leaf()) {
       kids[nk++] = bi;  // root that is a single leaf
+    } else if (plan) {
+      nk = plan->kids(bin, bi, kids);
     } else {
       kids[nk++] = bin[bi].left;
       kids[nk++] = bin[bi].right;
@@ -487,7 +564,7 @@ struct Collapser {
       std::vector<std::thread> th;
       for (int c = 0; c < nk; c++) {
         if (bin[kids[c]].leaf()) continue;
-        sub.emplace_back(new Collapser{bin, fmt, std::max(1u, par / (unsigned)inner), {}, {}, 0});
+        sub.emplace_back(new Collapser{bin, fmt, std::max(1u, par / (unsigned)inner), {}, {}, 0, plan});
         Collapser* sc = sub.back().get();
         const int32_t kb = kids[c];
         th.emplace_back([sc, kb] { sc->emit_root(kb); });
@@ -931,7 +1008,9 @@ int build(const rp_scene_desc* d, const BuildOptions& opt, PackedScene& out, std
       order.swap(C.prims);  // the tree's primitives in the 8-wide leaf order
       out.max_depth = C.max_depth;
     } else {
-      Collapser C{bin, out.node_format, threads, {}, {}, 0};
+      CollapsePlan plan;
+      if (opt.collapse == COLLAPSE_SAH) plan.build(bin, opt.cost_traverse, opt.cost_intersect);
+      Collapser C{bin, out.node_format, threads, {}, {}, 0, opt.collapse == COLLAPSE_SAH ? &plan : nullptr};
       if (out.node_format == rpl::NODES_Q8) C.qnodes.reserve(bin.size() / 2 + 1);
       else C.nodes.reserve(bin.size() / 2 + 1);
       C.emit_root(0);

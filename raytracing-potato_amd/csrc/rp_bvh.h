@@ -17,6 +17,8 @@
 
 namespace rpb {
 
+enum : uint32_t { COLLAPSE_GREEDY = 0, COLLAPSE_SAH = 1 };
+
 struct BuildOptions {
   uint32_t max_leaf = 4;        // primitives per leaf at most (<= rpl::LEAF_MAX)
   uint32_t bins = 32;           // SAH bins per axis
@@ -30,6 +32,7 @@ struct BuildOptions {
   uint32_t always_max = 4;
   double always_ratio = 4.0;
   uint32_t node_format = rpl::NODES_F32;  // rpl::NODES_F32 (Node4), _Q8 (Node4Q), _W8 (Node8Q) or 0 (auto_node_format)
+  uint32_t collapse = COLLAPSE_SAH;  // 4-wide collapse: COLLAPSE_GREEDY (largest-area child first) or _SAH (rp_bvh.cpp)
   uint32_t threads = 0;                   // host build threads (0 = the machine's, at most 16); same tree for any
 };
 

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "bf2f1ca6e02a35e1"
+#define RP_BUILD_ID "debd61d00120727f"

@@ -18,7 +18,8 @@ def scene_options(**kw) -> F.rp_scene_options:
     builder ("auto" | "host" | "gpu" (LBVH) | "ploc" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
     self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
     node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
-    unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*)."""
+    unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*), collapse ("auto" | "greedy" | "sah" or
+    RP_COLLAPSE_*)."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
@@ -35,6 +36,8 @@ def scene_options(**kw) -> F.rp_scene_options:
         if k == "unit_queues" and isinstance(v, str):
             v = {"auto": F.RP_QUEUES_AUTO, "single": F.RP_QUEUES_SINGLE, "xcd_tiles": F.RP_QUEUES_XCD_TILES,
                  "xcd_regions": F.RP_QUEUES_XCD_REGIONS}[v]
+        if k == "collapse" and isinstance(v, str):
+            v = {"auto": F.RP_COLLAPSE_AUTO, "greedy": F.RP_COLLAPSE_GREEDY, "sah": F.RP_COLLAPSE_SAH}[v]
         if not hasattr(o, k):
             raise KeyError(f"unknown scene option {k!r}")
         setattr(o, k, v)

@@ -41,7 +41,7 @@ def test_librp_host_exports_all_rp_host_h_symbols():
 def test_librp_loads_and_reports_without_gpu():
     from rtpotato import _ffi as F
     L = F.rp()
-    assert L.rp_abi_version() == F.RP_ABI_VERSION == 5
+    assert L.rp_abi_version() == F.RP_ABI_VERSION == 6
     n = ctypes.c_int(-1)
     rc = L.rp_device_count(ctypes.byref(n))
     assert rc in (F.RP_OK, F.RP_ENODEV) and n.value >= 0
@@ -73,6 +73,17 @@ int main(void) {
     assert F.hittable_dtype().itemsize == ctypes.sizeof(F.rp_hittable)
 
 
+def test_integration_rust_mirror_matches_c():
+    """INTEGRATION.md's Rust #[repr(C)] mirrors of rp_render_params and rp_scene_options list the C fields in order
+    (a missing trailing field would make the library read past the caller's struct)."""
+    import re
+    from rtpotato import _ffi as F
+    text = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    for rust, c in (("RpRenderParams", F.rp_render_params), ("RpSceneOptions", F.rp_scene_options)):
+        body = re.search(r"pub struct " + rust + r" \{(.*?)\}", text, re.S).group(1)
+        assert re.findall(r"pub (\w+):", body) == [f[0] for f in c._fields_], rust
+
+
 def test_no_oracle_in_product():
     """The product (librp.so, the package) never links or imports the oracle."""
     import subprocess
@@ -94,6 +105,7 @@ def test_scene_options_defaults_without_gpu():
     assert o.node_format == 0  # RP_NODES_AUTO: q8 for host trees of >= 2^21 hittables, f32 otherwise
     assert o.leaf_break == 0   # auto: 8 for cache-resident scenes, 16 above 256 MB
     assert o.unit_queues == 0 and o.queue_chunk == 0  # RP_QUEUES_AUTO: per-XCD queues, tile by tile
+    assert o.collapse == 0  # RP_COLLAPSE_AUTO: the SAH-optimal 4-wide collapse
     o = scene_options(builder="gpu", lds_depth=17, node_format="q8")
     assert o.builder == 2 and o.lds_depth == 17 and o.node_format == 2
 

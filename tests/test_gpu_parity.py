@@ -317,6 +317,21 @@ def test_device_bvh_builder(gpu, name, arg, fmt, builder):
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
+@pytest.mark.parametrize("fmt", ["f32", "q8"])
+@pytest.mark.parametrize("collapse", ["greedy", "sah"])
+def test_host_tree_collapse(gpu, collapse, fmt):
+    """Both 4-wide collapses of the host SAH tree (rp_scene_options.collapse, rp_bvh.cpp CollapsePlan): the SAH-optimal
+    cut gives the bunny fewer wide nodes than the greedy rule, and both render the oracle's image and ray counts."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    opt = {"builder": "host", "collapse": collapse, "node_format": fmt}
+    sc = scenes.configure(scenes.bunny_full(), 64, 40)
+    with gpu.DeviceScene(sc, options=opt) as ds:
+        nodes = ds.info()["nodes"]
+    assert (nodes < 1600) if collapse == "sah" else (nodes > 1600), nodes  # 1,451 vs 1,729 wide nodes
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options=opt)
+
+
 @pytest.mark.parametrize("fmt", ["f32", "q8", "w8"])
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
 def test_spilled_traversal_stack(gpu, name, arg, fmt):
