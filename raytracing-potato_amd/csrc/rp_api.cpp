@@ -124,6 +124,7 @@ struct rp_workspace {
   uint32_t* d_meas_g = nullptr;   // frame gather: 2 x nranks x stride_tiles (sums, then maxima; rank-major)
   uint64_t meas_g_words = 0;
   uint32_t* d_fcost = nullptr;    // learned table: 2 x TILE_SORT_MAX, by frame tile
+  uint64_t* d_sort = nullptr;     // the tile sorts' keys (rpk::SORT_SCRATCH words: global memory, not LDS)
   bool meas_on = false;           // the last render measured (megakernel)
   bool fcost_valid = false;
   uint32_t fcost_geom[4] = {0, 0, 0, 0};  // width, height, tile_w, tile_h of the learned table
@@ -182,7 +183,7 @@ void ws_release(rp_workspace* w) {
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
                   (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
-                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost})
+                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort})
     dfree(p);
   *w = rp_workspace{};
 }
@@ -196,7 +197,7 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
   if (!dalloc(&w->d_ctr, rpk::CTR_N) || !dalloc(&w->d_probe_ctr, rpk::CTR_N) || !dalloc(&w->d_queue, rpk::QUEUE_WORDS) ||
       !dalloc(&w->d_tile_cost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_tile_order, rpk::TILE_SORT_MAX) ||
       !dalloc(&w->d_plan, 2 * rpk::TILE_SORT_MAX + 2) || !dalloc(&w->d_meas, 2 * rpk::TILE_SORT_MAX) ||
-      !dalloc(&w->d_fcost, 2 * rpk::TILE_SORT_MAX) ||
+      !dalloc(&w->d_fcost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_sort, rpk::SORT_SCRATCH) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
     ws_release(w);
@@ -747,7 +748,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
       if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
       frame_cost = w->d_tile_cost;
     }
-    int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, w->d_plan, stream);
+    int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, w->d_plan, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile plan launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_map = w->d_plan;
     tg.map = w->d_plan;
@@ -760,7 +761,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     probe_px = learned_px;
   }
   if (order_mode == RP_TILES_MORTON && sortable) {
-    int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, stream);
+    int e = rpk::launch_tile_sort(nullptr, t.n_shard_tiles, 1, tg, w->d_tile_order, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
@@ -769,7 +770,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     if (!frame_cost && (rc = probe(kp.shard, kp.nshards, t.n_shard_tiles, s->opt.probe_n, probe_px))) return rc;
     tg.cost_by_tile = frame_cost ? 1u : 0u;
     int e = rpk::launch_tile_sort(frame_cost ? frame_cost : w->d_tile_cost, t.n_shard_tiles, probe_px, tg,
-                                  w->d_tile_order, stream);
+                                  w->d_tile_order, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }

@@ -141,8 +141,10 @@ struct TileGeom {
   uint32_t map_tiles;
   uint32_t cost_by_tile;  // 1: cost[] is indexed by frame tile (a whole-frame probe), 0: by shard tile
 };
+// scratch: SORT_SCRATCH words of device memory (the sort's keys; not LDS, see rp_kernel.hip SORT_BLOCK).
+enum { SORT_SCRATCH = TILE_SORT_MAX + 1 };
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
-                     void* stream);
+                     uint64_t* scratch, void* stream);
 
 // Final pass of a multi-batch frame: per shard slot, the batch sums added in batch order, / spp.
 int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void* stream);
@@ -171,7 +173,7 @@ struct FrameGeom {
 // `nranks` ranks that still has room for a tile, every rank receiving exactly the interleave's tile count.  Writes
 // plan[0, n) = the deal order (tile of shard s, shard tile k at plan[s + k * nranks]), plan[n, 2n) = its inverse
 // and plan[2n, 2n+2) = a 64-bit hash of the order (compared across ranks in the frame gather).  One block.
-int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, void* stream);
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, uint64_t* scratch, void* stream);
 // Counters of a frame gather: stage this rank's block (ctr may be NULL = zeros; hash may be NULL = 0) for the
 // all-gather, and reduce the gathered blocks of nranks ranks into out (sums; status bits OR-ed, plus
 // STATUS_PLAN_MISMATCH when two ranks' plan hashes differ).

@@ -450,9 +450,9 @@ int launch_reduce_batches(const KParams& p, double* out_rgb, float* out_fg, void
 // no threshold (Rust's saturating `as u8` maps NaN to 0), values above 1 reach all 255.
 __global__ void __launch_bounds__(256) srgb_bgra_kernel(const SrgbTable tab, const double* __restrict__ rgb,
                                                        uint64_t n, uint32_t* __restrict__ bgra) {
-  __shared__ double thr[256];
-  thr[threadIdx.x] = tab.thr[threadIdx.x];
-  __syncthreads();
+  // the thresholds straight from the kernel-argument segment (constant memory, L1/K$-resident), not an LDS copy: a frame
+  // gather runs while other frames' persistent render kernels hold every CU's LDS (see SORT_BLOCK)
+  const double* thr = tab.thr;
   for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
     uint32_t px = 0xff000000u;
 #pragma unroll
@@ -502,10 +502,30 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
   return (int)hipGetLastError();
 }
 
-// Bitonic sort of the probed tiles in LDS, one block: key = inverted (longest sample: 4 bits, mean rays per
-// probed pixel x 16: 14 bits) << 14 | k, so an ascending sort orders by descending cost, ties by shard
-// tile index.  Padding keys sort last.
-static constexpr int SORT_BLOCK = 1024;
+// The tile sorts below are one-block bitonic sorts over a workspace scratch array in GLOBAL memory (L2-resident, at
+// most 128 KB), with no LDS and few registers.  They run in front of a frame's render, and with frames in flight
+// another frame's persistent render kernel holds every CU's LDS: a block that needs LDS (the first form sorted in
+// 64-128 KB of it) waited 20-78 ms for a CU to drain (profiles/r3 shard trace), so the next frame could not start
+// filling the CUs the previous one released.  A 256-thread block without LDS fits beside the render waves at once.
+// __syncthreads() orders the block's global accesses (workgroup-scope fence: the waves share one CU's L1).
+static constexpr int SORT_BLOCK = 256;
+template <class T>
+__device__ __forceinline__ void bitonic_global(T* __restrict__ key, uint32_t np2) {
+  for (uint32_t size = 2; size <= np2; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
+        const uint32_t j = i ^ stride;
+        if (j > i) {
+          const T a = key[i], b = key[j];
+          const bool up = (i & size) == 0;
+          if ((a > b) == up) { key[i] = b; key[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
 static constexpr float SORT_Q = 4.0f;  // buckets per octave of cost
 __device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every other bit of 16
@@ -526,8 +546,7 @@ __device__ __forceinline__ uint32_t compact8(uint32_t v) {  // inverse of spread
 // ms); without costs (cost == NULL) plain Z-order.
 __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* __restrict__ cost, uint32_t n,
                                                                uint32_t probe_px, uint32_t np2, TileGeom g,
-                                                               uint32_t* __restrict__ order) {
-  __shared__ uint32_t key[TILE_SORT_MAX];
+                                                               uint32_t* __restrict__ order, uint32_t* __restrict__ key) {
   for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
     uint32_t kk = 0xFFFFFFFFu;
     if (i < n) {
@@ -546,19 +565,7 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
     key[i] = kk;
   }
   __syncthreads();
-  for (uint32_t size = 2; size <= np2; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < np2; i += SORT_BLOCK) {
-        const uint32_t j = i ^ stride;
-        if (j > i) {
-          const uint32_t a = key[i], b = key[j];
-          const bool up = (i & size) == 0;
-          if ((a > b) == up) { key[i] = b; key[j] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  bitonic_global(key, np2);
   // back from the frame tile to its shard tile index: the inverse deal order (plan[n_tiles + t], laid out by
   // launch_tile_plan right behind the order) or the interleave's (t - shard) / nshards
   const uint32_t n_tiles = g.map ? g.map_tiles : 0u;
@@ -569,51 +576,39 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
 }
 
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
-                     void* stream) {
+                     uint64_t* scratch, void* stream) {
   if (n == 0 || n > TILE_SORT_MAX) return (int)hipErrorInvalidValue;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
   hipLaunchKernelGGL(tile_sort_kernel, dim3(1), dim3(SORT_BLOCK), 0, (hipStream_t)stream, cost, n, probe_px, np2, g,
-                     order);
+                     order, reinterpret_cast<uint32_t*>(scratch));
   return (int)hipGetLastError();
 }
 
-// Balanced tile plan (rp_kernel.h launch_tile_plan).  One block: the n frame tiles sorted in LDS by 64-bit key
-// (~cost << 32 | tile: descending cost, ties by tile index; 16384 tiles = 128 KB of the 160 KB a workgroup may
-// hold), then dealt in rounds of nranks tiles, alternating direction ("snake": round k gives its tiles to ranks
+// Balanced tile plan (rp_kernel.h launch_tile_plan).  One block: the n frame tiles sorted by 64-bit key
+// (~cost << 32 | tile: descending cost, ties by tile index; 16384 tiles = 128 KB of global scratch), then dealt in rounds of nranks tiles, alternating direction ("snake": round k gives its tiles to ranks
 // 0..N-1 when k is even, N-1..0 when odd, so each pair of rounds gives every rank one tile from the costly end and
 // one from the cheap end of the pair's 2N-tile range), the last partial round forward -- every rank gets exactly
 // the interleave's tile count, so shard sizes and gather strides do not change.  The deal is parallel (position p
 // of the sorted order -> deal slot k * N + rank), its imbalance is second order in the cost curve (a greedy LPT
 // step per tile would be a serial loop of n wave reductions).  Deterministic: integer keys, no atomics but the
 // order-free hash sum.
-static constexpr int PLAN_BLOCK = 1024;
+static constexpr int PLAN_BLOCK = SORT_BLOCK;
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   return z ^ (z >> 31);
 }
 __global__ void __launch_bounds__(PLAN_BLOCK) tile_plan_kernel(const uint32_t* __restrict__ cost, uint32_t n,
-                                                               uint32_t np2, uint32_t N, uint32_t* __restrict__ plan) {
-  __shared__ unsigned long long key[TILE_SORT_MAX];
-  __shared__ unsigned long long hash;
-  if (threadIdx.x == 0) hash = 0;
+                                                               uint32_t np2, uint32_t N, uint32_t* __restrict__ plan,
+                                                               unsigned long long* __restrict__ key) {
+  // key[TILE_SORT_MAX]: the plan hash's accumulator (global, like the keys: no LDS, see SORT_BLOCK)
+  unsigned long long* hash = key + TILE_SORT_MAX;
+  if (threadIdx.x == 0) *hash = 0;
   for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK)
     key[i] = i < n ? ((uint64_t)(0xFFFFFFFFu - cost[i]) << 32) | i : ~0ull;
   __syncthreads();
-  for (uint32_t size = 2; size <= np2; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK) {
-        const uint32_t j = i ^ stride;
-        if (j > i) {
-          const unsigned long long a = key[i], b = key[j];
-          const bool up = (i & size) == 0;
-          if ((a > b) == up) { key[i] = b; key[j] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  bitonic_global(key, np2);
   const uint32_t full = n / N;  // complete rounds
   uint64_t h = 0;
   for (uint32_t p = threadIdx.x; p < n; p += PLAN_BLOCK) {
@@ -624,20 +619,21 @@ __global__ void __launch_bounds__(PLAN_BLOCK) tile_plan_kernel(const uint32_t* _
     plan[n + t] = pos;
     h += mix64(((uint64_t)pos << 32) | t);
   }
-  atomicAdd(&hash, (unsigned long long)h);
+  atomicAdd(hash, (unsigned long long)h);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint64_t v = mix64(hash ^ ((uint64_t)n << 32 | N)) | 1ull;  // never 0 (0 = the interleave)
+    const uint64_t v = mix64(atomicAdd(hash, 0ull) ^ ((uint64_t)n << 32 | N)) | 1ull;  // never 0 (0 = the interleave)
     plan[2 * n] = (uint32_t)v;
     plan[2 * n + 1] = (uint32_t)(v >> 32);
   }
 }
 
-int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, void* stream) {
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, uint64_t* scratch, void* stream) {
   if (n == 0 || n > TILE_SORT_MAX || nranks == 0) return (int)hipErrorInvalidValue;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
-  hipLaunchKernelGGL(tile_plan_kernel, dim3(1), dim3(PLAN_BLOCK), 0, (hipStream_t)stream, cost, n, np2, nranks, plan);
+  hipLaunchKernelGGL(tile_plan_kernel, dim3(1), dim3(PLAN_BLOCK), 0, (hipStream_t)stream, cost, n, np2, nranks, plan,
+                     reinterpret_cast<unsigned long long*>(scratch));
   return (int)hipGetLastError();
 }
 

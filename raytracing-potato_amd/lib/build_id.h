@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "debd61d00120727f"
+#define RP_BUILD_ID "5537149adc242ddd"
