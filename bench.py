@@ -11,10 +11,10 @@ persistent HIP kernel (librp.so) from scene data resident in HBM, followed by li
 (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
 xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
 output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the
-RCCL communicator and takes the barrier and max-time reduction.  With N > 1 three frames are in flight (frame
-k renders on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the
-next (--inflight).  The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both
-sides; the max over ranks is used.
+RCCL communicator and takes the barrier and max-time reduction.  Three frames are in flight (frame k renders
+on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the next (--inflight).
+The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is
+used.
 
 Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays / time.
 roofline: per ray of the render kernel, from the committed profile record of THIS build
@@ -153,14 +153,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=3)  # one frame per in-flight workspace: each learns its tile costs
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
     ap.add_argument("--cpu-spp", type=int, default=0, help="override the CPU baseline runs' spp (0 = per run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
-                         "(0 = 1 on one GPU, 3 on several)")
+                         "(0 = 3)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic, one GPU: render only shard --shard of this many (the per-rank work of an N-GPU "
                          "run), no gather; not a bench line")
@@ -207,9 +207,11 @@ def main():
     # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
     # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.
-    # Per-rank work of an 8-GPU C3 frame (shard 0 of 8 on one GPU, --shard-of 8): 35.8 ms with one frame in
-    # flight, 29.9 with two, 29.3 with three, against 26.8 ms of work (profiles/r2/c3_v40_shard_inflight.json)
-    F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
+    # Per-rank work of an 8-GPU C3 frame (8-way shards on one GPU): 26.7 ms mean with three frames in flight against
+    # 25.8 ms of work (profiles/r3/c3_v47_shards_inflight_traced.json); one GPU, whole frames: C3 209.6 -> 207.0 ms,
+    # C5 1,611 -> 1,592 ms with three (two: 209.0 ms; profiles/r3/ab/if2_*) -- the next frames fill the CUs the
+    # finishing frame's tail releases
+    F_ = args.inflight if args.inflight > 0 else 3
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
     wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
