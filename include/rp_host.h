@@ -58,6 +58,10 @@ int rph_bvh_selfcheck(const rp_scene_desc* desc, uint32_t node_format, uint64_t*
  * 2^64-1}. */
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
                             uint64_t* per_ray);
+/* The two above with the 4-wide collapse chosen (RP_COLLAPSE_*, include/rp.h: the library's AUTO is SAH). */
+int rph_bvh_selfcheck_ex(const rp_scene_desc* desc, uint32_t node_format, uint32_t collapse, uint64_t* stats);
+int rph_bvh_traversal_stats_ex(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
+                               uint32_t collapse, uint64_t* per_ray);
 
 /* Hash (FNV-1a) of the packed host tree (node records and leaf-ordered primitive references) built with
  * `threads` build threads (0 = the machine's, at most 16): the tree does not depend on the thread count. */

@@ -413,6 +413,11 @@ int rph_sky_panorama(uint32_t width, uint32_t height, uint8_t* rgba) {
 
 int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
                             uint64_t* per_ray) {
+  return rph_bvh_traversal_stats_ex(desc, rays, n, node_format, RP_COLLAPSE_AUTO, per_ray);
+}
+
+int rph_bvh_traversal_stats_ex(const rp_scene_desc* desc, const double* rays, uint64_t n, uint32_t node_format,
+                               uint32_t collapse, uint64_t* per_ray) {
   // CPU model of rp_device.h's traversal over the same packed 4-wide tree: child boxes tested in f32 with
   // per-axis outward bounds (t = fma(P, inv, nb|fb), quantized: fma(q, s inv, fma(o, inv, nb|fb))), rcp
   // emulated by a correctly rounded 1/x, the min/max slab form instead of the device's octant selection
@@ -425,6 +430,7 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
   rpb::PackedScene ps;
   rpb::BuildOptions bo;
   bo.node_format = node_format;
+  bo.collapse = collapse == RP_COLLAPSE_GREEDY ? rpb::COLLAPSE_GREEDY : rpb::COLLAPSE_SAH;
   rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(err);
   const bool q8 = ps.node_format != rpl::NODES_F32;  // Node4Q or Node8Q: the frame term
@@ -619,12 +625,17 @@ int rph_bvh_traversal_stats(const rp_scene_desc* desc, const double* rays, uint6
 }
 
 int rph_bvh_selfcheck(const rp_scene_desc* desc, uint32_t node_format, uint64_t* stats) {
+  return rph_bvh_selfcheck_ex(desc, node_format, RP_COLLAPSE_AUTO, stats);
+}
+
+int rph_bvh_selfcheck_ex(const rp_scene_desc* desc, uint32_t node_format, uint32_t collapse, uint64_t* stats) {
   std::string err;
   int rc = rpb::validate(desc, err);
   if (rc != RP_OK) return fail(err);
   rpb::PackedScene ps;
   rpb::BuildOptions bo;
   bo.node_format = node_format;
+  bo.collapse = collapse == RP_COLLAPSE_GREEDY ? rpb::COLLAPSE_GREEDY : rpb::COLLAPSE_SAH;
   rc = rpb::build(desc, bo, ps, err);
   if (rc != RP_OK) return fail(err);
   rc = rpb::check(ps, err);
