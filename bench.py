@@ -11,8 +11,10 @@ persistent HIP kernel (librp.so) from scene data resident in HBM, followed by li
 (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
 xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
 output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the
-RCCL communicator and takes the barrier and max-time reduction.  Three frames are in flight (frame k renders
-on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the next (--inflight).
+RCCL communicator and takes the barrier and max-time reduction.  With N > 1 three frames are in flight (frame k
+renders on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the next
+(--inflight); one GPU renders one frame at a time, so the render kernel's launch duration (HIP events, the rocprofv3
+kernel trace) is the frame time the roofline is priced on (--inflight 3 there: -1.2 %).
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is
 used.
 
@@ -160,7 +162,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
-                         "(0 = 3)")
+                         "(0 = 1 on one GPU, 3 on several)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic, one GPU: render only shard --shard of this many (the per-rank work of an N-GPU "
                          "run), no gather; not a bench line")
@@ -208,10 +210,10 @@ def main():
     # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.
     # Per-rank work of an 8-GPU C3 frame (8-way shards on one GPU): 26.7 ms mean with three frames in flight against
-    # 25.8 ms of work (profiles/r3/c3_v47_shards_inflight_traced.json); one GPU, whole frames: C3 209.6 -> 207.0 ms,
-    # C5 1,611 -> 1,592 ms with three (two: 209.0 ms; profiles/r3/ab/if2_*) -- the next frames fill the CUs the
-    # finishing frame's tail releases
-    F_ = args.inflight if args.inflight > 0 else 3
+    # 25.8 ms of work (profiles/r3/c3_v47_shards_inflight_traced.json).  One GPU, whole frames: C3 209.6 -> 207.0 ms,
+    # C5 1,611 -> 1,592 ms with three (profiles/r3/ab/if2_*), but overlapping launches no longer have a launch duration
+    # equal to the frame time, which the roofline (HIP events, rocprofv3 kernel trace) is priced on: one at a time there
+    F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
     wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
