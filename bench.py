@@ -20,17 +20,21 @@ used.
 
 Rays = root scene.hit() calls (render.rs:105,133), counted on the device; value = all ranks' rays / time.
 roofline: per ray of the render kernel, from the committed profile record of THIS build
-(profiles/current.json -> tools/roofline.py output, refused when its build id differs from rp_build_id()):
-  achieved = the kernel's algorithmic bytes (its own node visits x node bytes + primitive tests x 80 B + the
-             closest hit's records + texels + keystream, from the diagnostic build's counts) x this launch's rays /
-             the launch's duration (HIP events on its stream), against the 8 TB/s HBM peak;
-  traffic  = memory-side bytes of the launch from the PMC counters (2 x FETCH_SIZE + WRITE_SIZE, gfx950);
-  binding  = the larger of the VALU-issue fraction and the traffic fraction (what limits the kernel);
-and, for reference, the rate the reference's own traversal would need (its event counts x SURVEY.md 8d bytes
-per event).  cpu_baseline: the CPU oracle's -O3 restatement of the reference driver (main.rs:36-106: LIFO tile
-queue, worker threads with their own StdRng) on a bounded sample of the same scene, at the reference's 4 workers
-and at 16 (the box's CPU share per GPU), rank 0, N = 1 only; the full host is extrapolated from the 16-worker
-run, not run (the pool's rule: a GPU job sizes its worker pools to its 16-core share).
+(profiles/current.json -> tools/roofline.py output, refused when its build id differs from rp_build_id()), times this
+launch's rays, over the launch's duration (HIP events on its stream):
+  achieved / frac = memory-side bytes from the PMC counters (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
+             MI355X_MICROARCH.md; Infinity-Cache hits are counted, so an upper bound of HBM traffic) against the 8 TB/s
+             HBM peak -- the HBM roofline fraction; traffic = those bytes per launch;
+  binding_frac = the fraction of its own roof of what binds the kernel: the larger of the VALU-issue fraction and frac;
+  l2_level = the kernel's ALGORITHMIC bytes (its node visits x node bytes + primitive tests x 80 B + the closest hit's
+             records + texels + keystream, from the diagnostic build's counts) at this rate, against the guide's
+             measured L2-shared gather rate (16.8-18.8 TB/s): these bytes are served by L2 and the Infinity Cache;
+and, for reference, the rate the reference's own traversal would need (its event counts x SURVEY.md 8d bytes per
+event).  cpu_baseline: the CPU oracle's -O3 restatement of the reference driver (main.rs:36-106: LIFO tile queue,
+worker threads with their own StdRng) on a bounded sample of the same scene at 1, 4 (the reference's main.rs:27
+default), 8 and 16 workers (16 = the box's CPU share per GPU; a GPU job on this pool sizes its worker pools to it),
+rank 0, N = 1 only; the full host is a least-squares line through those four measured points, evaluated at the
+host's physical core count (an extrapolation, labelled so).
 """
 from __future__ import annotations
 
@@ -52,8 +56,11 @@ CLOCK_HZ = 2.4e9             # MI355X_MICROARCH.md max clock
 VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
 # SURVEY.md 8d algorithmic bytes per event of the REFERENCE traversal (reference tree, f64 layout)
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
-# (workers, spp) of the CPU baseline runs, ~13 s each: main.rs:27 num_workers = 4; 16 = the GPU box's CPU share
-CPU_RUNS = ((4, 8), (16, 32))
+# MI355X_MICROARCH.md "Indexed rows": rows shared by every workgroup, gathered from the XCD's L2: 16.8-18.8 TB/s
+L2_GATHER_GBS = 18800.0
+# (workers, spp) of the CPU baseline runs, ~13 s each: 1 worker; main.rs:27 num_workers = 4; 8; 16 = the GPU box's CPU
+# share (the line through all four is the full-host extrapolation)
+CPU_RUNS = ((1, 2), (4, 8), (8, 16), (16, 32))
 
 
 def log(*a):
@@ -114,6 +121,22 @@ def host_cpu():
             "affinity_cpus": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
+def fit_workers(runs):
+    """Least-squares line rate = intercept + per_worker * workers through the measured CPU runs (not forced
+    through 0), its R^2, and each run's rate per worker (how linear the scaling is)."""
+    xs = [r["workers"] for r in runs]
+    ys = [r["value"] for r in runs]
+    n = len(xs)
+    mx, my = sum(xs) / n, sum(ys) / n
+    sxx = sum((x - mx) ** 2 for x in xs)
+    b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sxx
+    a = my - b * mx
+    ss_res = sum((y - (a + b * x)) ** 2 for x, y in zip(xs, ys))
+    ss_tot = sum((y - my) ** 2 for y in ys)
+    return {"intercept": round(a, 4), "per_worker": round(b, 4), "r2": round(1 - ss_res / ss_tot, 6) if ss_tot else 1.0,
+            "points": n, "per_worker_at": {str(x): round(y / x, 4) for x, y in zip(xs, ys)}}
+
+
 def cpu_baseline(config: str, runs_plan, spp_override: int = 0):
     """The reference driver restated (oracle, -O3, no per-event counters): 1920x1080 at each run's spp."""
     from oracle import oracle_py as O
@@ -141,12 +164,12 @@ def cpu_baseline(config: str, runs_plan, spp_override: int = 0):
                      f"box's CPU share); Rust reference unbuildable here",
            "runs": runs, "host": host}
     phys = host.get("physical_cores")
-    if phys:
-        per = main["value"] / main["workers"]
+    if phys and len(runs) >= 3:
+        fit = fit_workers(runs)
         out["full_host_extrapolated"] = {
-            "value": round(per * phys, 2), "cores": phys,
-            "basis": f"{main['workers']}-worker rate x {phys} physical cores / {main['workers']} (linear: 4 -> 16 "
-                     f"workers scaled {runs[-1]['value'] / runs[0]['value']:.2f}x for 4x); not run -- a GPU job on this "
+            "value": round(fit["intercept"] + fit["per_worker"] * phys, 2), "cores": phys, "fit": fit,
+            "basis": f"least-squares line through the {fit['points']} measured worker counts "
+                     f"{[r['workers'] for r in runs]} evaluated at {phys} physical cores; not run -- a GPU job on this "
                      f"pool sizes its worker pools to its {main['workers']}-core share"}
     return out
 
@@ -158,6 +181,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)  # one frame per in-flight workspace: each learns its tile costs
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
+    ap.add_argument("--samples-per-stream", type=int, default=0,
+                    help="rp_render_params.samples_per_stream, the RNG contract (0 = RP_SAMPLES_PER_STREAM = 32; "
+                         ">= spp: one stream per pixel, SURVEY.md 8c)")
     ap.add_argument("--cpu-spp", type=int, default=0, help="override the CPU baseline runs' spp (0 = per run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
@@ -196,6 +222,8 @@ def main():
     scene, params = scenes.config_scene(args.config)
     if args.spp:
         params = replace(params, spp=args.spp)
+    if args.samples_per_stream:
+        params = replace(params, samples_per_stream=args.samples_per_stream)
     t = time.time()
     ds = DeviceScene(scene, device=local, options=options)
     info = ds.info()
@@ -285,21 +313,28 @@ def main():
 
     if rank == 0:
         local_rays = rays_step / world  # this rank's launch (shards carry near-equal work under the balanced plan)
-        rec = kernel_record(args.config) if args.spp == 0 else None
+        # the per-ray record is of the default workload (its spp and RNG batches)
+        rec = kernel_record(args.config) if args.spp == 0 and args.samples_per_stream == 0 else None
         build = F.rp().rp_build_id().decode()
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
                 "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3), "build_id": build}
         if rec and rec.get("build_id") != build:
             roof["stale_record"] = f"{rec['source']} was measured on build {rec.get('build_id')}; not used"
             rec = None
+        binding = None
         if rec:
             traffic = rec["traffic_bytes_per_ray"] * local_rays
             tr_gbs = traffic / kernel_s / 1e9
+            tr_frac = tr_gbs / HBM_PEAK_GBS
             issue = rec["valu_per_ray"] * local_rays / kernel_s
             valu_frac = issue / VALU_ISSUE_PEAK
             roof.update({
-                "traffic": round(traffic), "traffic_bytes_per_ray": round(rec["traffic_bytes_per_ray"], 1),
-                "traffic_GBps": round(tr_gbs, 1), "traffic_frac": round(tr_gbs / HBM_PEAK_GBS, 4),
+                "achieved": round(tr_gbs, 1), "frac": round(tr_frac, 4), "traffic": round(traffic),
+                "basis": "memory-side bytes of the launch (PMC: 2 x FETCH_SIZE + WRITE_SIZE per ray x this launch's "
+                         "rays) / its HIP-event duration; Infinity-Cache hits included (an upper bound of HBM bytes)",
+                "traffic_bytes_per_ray": round(rec["traffic_bytes_per_ray"], 1),
+                "fetch_bytes_per_ray": round(rec["fetch_bytes_per_ray"], 1) if "fetch_bytes_per_ray" in rec else None,
+                "write_bytes_per_ray": round(rec["write_bytes_per_ray"], 1) if "write_bytes_per_ray" in rec else None,
                 "valu_issue": {"achieved": round(issue / 1e9, 1), "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
                                "unit": "Gwave-inst/s", "frac": round(valu_frac, 4),
                                "valu_per_ray": round(rec["valu_per_ray"], 2)},
@@ -308,15 +343,17 @@ def main():
                           f"figures x this launch's rays / its HIP-event duration)"})
             alg = rec.get("algorithmic_bytes_per_ray")
             if alg:
-                achieved = alg * local_rays / kernel_s / 1e9
-                roof.update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                             "algorithmic_bytes_per_ray": round(alg, 1),
-                             "algorithmic_breakdown": rec.get("algorithmic_breakdown"),
-                             "traffic_over_algorithmic": round(rec["traffic_bytes_per_ray"] / alg, 4)})
-            bind = ("valu_issue", valu_frac) if valu_frac >= tr_gbs / HBM_PEAK_GBS else ("hbm_traffic", tr_gbs / HBM_PEAK_GBS)
-            roof["binding"] = {"resource": bind[0], "frac": round(bind[1], 4),
+                l2 = alg * local_rays / kernel_s / 1e9
+                roof["l2_level"] = {
+                    "achieved": round(l2, 1), "peak": L2_GATHER_GBS, "unit": "GB/s", "frac": round(l2 / L2_GATHER_GBS, 4),
+                    "bytes_per_ray": round(alg, 1), "breakdown": rec.get("algorithmic_breakdown"),
+                    "traffic_over_algorithmic": round(rec["traffic_bytes_per_ray"] / alg, 4),
+                    "note": "the kernel's own algorithmic bytes (what its loads touch), served by L2 / Infinity Cache; "
+                            "peak = MI355X_MICROARCH.md's L2-shared row gather, 16.8-18.8 TB/s (upper end used)"}
+            binding = ("valu_issue", valu_frac) if valu_frac >= tr_frac else ("hbm_traffic", tr_frac)
+            roof["binding"] = {"resource": binding[0], "frac": round(binding[1], 4),
                                "note": "the kernel is latency-bound (cycle_budget: waves wait on memory ~45 % of their "
-                                       "cycles); its algorithmic bytes are mostly served by L2 / Infinity Cache"}
+                                       "cycles at 4 waves/SIMD); neither VALU issue nor memory traffic is near its roof"}
         ref_bpr = reference_equivalent(args.config)
         roof["reference_equivalent"] = {
             "bytes_per_ray": round(ref_bpr, 1), "GBps": round(ref_bpr * local_rays / kernel_s / 1e9, 1),
@@ -330,6 +367,7 @@ def main():
             "config": {"workload": f"{args.config}: {scenes.CONFIGS[args.config].description}",
                        "width": params.width, "height": params.height, "spp": params.spp,
                        "max_bounce": params.max_bounce, "seed": params.seed,
+                       "samples_per_stream": params.samples_per_stream or 32,
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
                        "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
@@ -338,6 +376,8 @@ def main():
                        **({"simulated_shard": f"shard {args.shard} of {args.shard_of}, no gather (diagnostic)"}
                           if args.shard_of else {})},
             "roofline": roof,
+            "binding_frac": round(binding[1], 4) if binding else None,
+            "binding_resource": binding[0] if binding else None,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline and not args.shard_of:

@@ -396,10 +396,16 @@ int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
  * bytes = to_srgb_u8 in tga::save byte order (rp_shard_to_bgra8) -- the body of output.tga; d_frame_rgb
  * width*height*3 linear f64.  Every rank must pass the same NULL / non-NULL combination of d_frame_bgra and
  * d_frame_rgb: the collectives issued are, in this order, an all-gather of every rank's counter block (always),
- * of the BGRA8 shards (d_frame_bgra) and of the f64 shards (d_frame_rgb).  d_counters (nullable): the rank's
+ * two of its measured tile costs (frames of <= 16384 tiles), of the BGRA8 shards (d_frame_bgra) and of the f64
+ * shards (d_frame_rgb).  d_counters (nullable): the rank's
  * RP_COUNTERS_LEN counters in, the frame's out -- rays, samples and pixels summed over the ranks, status bits
  * OR-ed over them, plus RP_STATUS_PLAN_MISMATCH when the ranks' balanced plans differ.  A caller that does not
- * pass counters does not learn the status. */
+ * pass counters does not learn the status.  Tile costs (the collectives also all-gather every rank's measured
+ * tile costs for frames of <= 16384 tiles) and the balanced plan live in the workspace: the gather reads the
+ * workspace's plan and measured costs and writes its learned cost table on `stream`, and the next render with the
+ * same workspace rewrites the first two and reads the third on ITS stream -- so that render must be stream-ordered
+ * after this gather (same stream, or an event; bench.py waits on the gather's event before reusing a workspace).
+ * Frames in flight use one workspace per frame. */
 int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                     const double* d_shard_rgb, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, void* stream);

@@ -99,6 +99,7 @@ struct rp_workspace {
   uint32_t* d_tile_order = nullptr;  // cost-ordered shard tiles, rpk::TILE_SORT_MAX entries
   uint32_t* d_slab = nullptr;        // keystream cache, one slab per resident render lane
   uint32_t* d_spill = nullptr;       // traversal-stack overflow entries of every resident lane (deep trees)
+  uint32_t* d_t0 = nullptr;          // start time of each resident lane's measured unit (tile costs)
   // reserved by rp_workspace_reserve:
   double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames
   uint32_t* d_partial_hits = nullptr;
@@ -183,7 +184,7 @@ void ws_release(rp_workspace* w) {
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
                   (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
-                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort})
+                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0})
     dfree(p);
   *w = rp_workspace{};
 }
@@ -199,7 +200,8 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
       !dalloc(&w->d_plan, 2 * rpk::TILE_SORT_MAX + 2) || !dalloc(&w->d_meas, 2 * rpk::TILE_SORT_MAX) ||
       !dalloc(&w->d_fcost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_sort, rpk::SORT_SCRATCH) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
-      !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth))) {
+      !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth)) ||
+      !dalloc(&w->d_t0, lanes)) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
   }
@@ -682,6 +684,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   rpk::KScene ks = s->ks;
   ks.rng_slab = w->d_slab;
   ks.spill = w->d_spill;
+  ks.unit_t0 = w->d_t0;
   auto grid_for = [&](uint64_t slots) {
     const uint64_t want = (slots + rpk::RENDER_BLOCK - 1) / rpk::RENDER_BLOCK;
     return (int)std::max<uint64_t>(1, std::min(want, resident));
@@ -731,7 +734,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // learned per-tile table and the next frame schedules from it -- no probe launch.  For a balanced plan over
   // N > 1 ranks the table must come from a gather over the same N ranks: every rank then holds the same bytes and
   // deals the same plan.  Otherwise a probe (the first frame, the stage-split engine) supplies the costs.
-  const bool measure = s->opt.engine == RP_ENGINE_MEGAKERNEL;
+  // (the measured table holds TILE_SORT_MAX tiles: a shard of more tiles -- 8 x 8 tiles at 1080p, say -- is not
+  // measured, and its frame keeps the probe / interleave)
+  const bool measure = s->opt.engine == RP_ENGINE_MEGAKERNEL && t.n_shard_tiles <= (uint32_t)rpk::TILE_SORT_MAX;
   const bool probe_order = order_mode == RP_TILES_PROBE;
   if (probe_order) order_mode = RP_TILES_COST;
   const bool learned = measure && !probe_order && fcost_matches(w, p, t);
@@ -857,9 +862,13 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
 int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb, hipStream_t st) {
   RP_NCCL(ncclAllGather(w->d_ctr_send, w->d_ctr_gather, rpk::GATHER_CTR, ncclUint64, comm, st));
   // every rank's measured tile costs (sums, then maxima): the next frame's learned table, the same on every rank
-  const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
-  RP_NCCL(ncclAllGather(w->d_meas, w->d_meas_g, gp.stride_tiles, ncclUint32, comm, st));
-  RP_NCCL(ncclAllGather(w->d_meas + rpk::TILE_SORT_MAX, w->d_meas_g + n, gp.stride_tiles, ncclUint32, comm, st));
+  // -- only for frames whose tiles fit the table (gather_learn's condition; a function of the params, so the same on
+  // every rank and the collective sequence stays consistent)
+  if (gp.t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX) {
+    const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
+    RP_NCCL(ncclAllGather(w->d_meas, w->d_meas_g, gp.stride_tiles, ncclUint32, comm, st));
+    RP_NCCL(ncclAllGather(w->d_meas + rpk::TILE_SORT_MAX, w->d_meas_g + n, gp.stride_tiles, ncclUint32, comm, st));
+  }
   if (bgra) RP_NCCL(ncclAllGather(w->d_gs_bgra, w->d_gather_bgra, gp.stride, ncclUint32, comm, st));
   if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
   return RP_OK;

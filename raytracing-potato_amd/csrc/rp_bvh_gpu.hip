@@ -51,7 +51,7 @@ __global__ void morton_kernel(uint32_t n, const Box6* __restrict__ boxes, double
   uint32_t code = 0;
   for (int k = 0; k < 3; k++) {
     double q = (c[k] - m[k]) * s[k];
-    q = q < 0.0 ? 0.0 : (q > 1023.0 ? 1023.0 : q);  // NaN-free: boxes are finite (validated)
+    q = !(q >= 0.0) ? 0.0 : (q > 1023.0 ? 1023.0 : q);  // a NaN centroid (NaN geometry) sorts as 0
     code |= expand_bits10((uint32_t)q) << (2 - k);
   }
   keys[i] = ((uint64_t)code << 32) | i;
@@ -79,7 +79,7 @@ __global__ void morton63_kernel(uint32_t n, const Box6* __restrict__ boxes, doub
   uint64_t code = 0;
   for (int k = 0; k < 3; k++) {
     double q = (c[k] - m[k]) * s[k] * 2048.0;  // scale maps the centroid range to [0, 1024]
-    q = q < 0.0 ? 0.0 : (q > 2097151.0 ? 2097151.0 : q);
+    q = !(q >= 0.0) ? 0.0 : (q > 2097151.0 ? 2097151.0 : q);  // NaN centroid -> 0
     code |= expand_bits21((uint64_t)q) << (2 - k);
   }
   keys[i] = code;
@@ -480,10 +480,14 @@ __global__ void __launch_bounds__(PLOC_B) ploc_nn_kernel(uint32_t m, const Box6*
   const int lo = max(0, i - PLOC_R), hi = min((int)m - 1, i + PLOC_R);
   for (int j = lo; j <= hi; j++) {
     if (j == i) continue;
-    const double d = area(box_union(a, win[j - base]));
+    double d = area(box_union(a, win[j - base]));
+    if (d != d) d = __builtin_huge_val();
     // strict order on (distance, lower position, higher position): the global minimum pair is mutual, so every
-    // round merges at least one pair; candidates are scanned in increasing j, so `<` keeps the smaller j on ties
-    if (d < best) {
+    // round merges at least one pair; candidates are scanned in increasing j, so `<` keeps the smaller j on ties.
+    // A NaN distance (NaN geometry: fmin/fmax keep a NaN when both operands are NaN) ranks as +inf, and a cluster
+    // with no finite candidate takes its first one (if no pair is finite, clusters 0 and 1 pair up, so the round
+    // still merges) -- never the -1 that ploc_flags_kernel would index with.
+    if (d < best || bj < 0) {
       best = d;
       bj = j;
     }
@@ -497,7 +501,7 @@ __global__ void ploc_flags_kernel(uint32_t m, const uint32_t* __restrict__ nn, u
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint32_t j = nn[i];
-  const bool mutual = nn[j] == i;
+  const bool mutual = j < m && nn[j] == i;
   keep[i] = (!mutual || i < j) ? 1u : 0u;
   merge[i] = (mutual && i < j) ? 1u : 0u;
 }

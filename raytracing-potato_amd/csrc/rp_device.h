@@ -150,7 +150,9 @@ static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING;
 // The pixel sum and path throughput (6 f64 per lane, read and written at every shade) live in LDS (in the
 // slab: C3 +2.6 %, C5 +4.6 %); the host then keeps ~19 traversal-stack entries in LDS and spills deeper ones to
 // the lane's global run (render_blocks_per_cu picks the split; bunny: 19 of 31, rarely reached).
-static constexpr uint32_t SLAB_N = SLAB_JIT + 8 + 1;  // + the unit-start word (RngT::meta)
+// (v43-v47 kept the measured unit's start time in one more uint4 of the slab: 688 B per lane, and C3 wrote 70 GB per
+// frame instead of 56 -- the stamp now lives in its own lane-indexed array, KScene::unit_t0)
+static constexpr uint32_t SLAB_N = SLAB_JIT + 8;
 // A refill pass runs when some lane is at or below RNG_CRIT blocks ahead, or RNG_BATCH lanes have room.
 static constexpr uint32_t RNG_CRIT = 2, RNG_BATCH = 48;
 // Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
@@ -165,8 +167,7 @@ template <uint32_t RN>
 struct RngT {
   static constexpr uint32_t ring = RN;
   // a lane's slab for this ring: key, RN ring blocks, 2 jitter blocks (compact: 416 B for RN = 4)
-  // ... and one word (in a uint4 slot) holding the start time of the lane's unit (tile cost measurement)
-  static constexpr uint32_t jit = SLAB_RING + 4 * RN, meta = jit + 8, lane_n = meta + 1;
+  static constexpr uint32_t jit = SLAB_RING + 4 * RN, lane_n = jit + 8;
   static_assert(RN > RNG_CRIT && RN <= RING && (RN & (RN - 1)) == 0,
                 "ring: a power of two above the critical refill level (a full ring is never refilled), <= RING");
   uint4* slab;     // global: this lane's slab
@@ -223,8 +224,6 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
     if (fresh) {
       DREG(DREG_BEGIN_PIXEL)
       store_key(r, k);
-      // the unit's start (100 MHz real-time clock, the same on every XCD): its duration is its tile's measured cost
-      reinterpret_cast<uint32_t*>(r.slab + RngT<RN>::meta)[0] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
     chacha12(k, b, w);
     store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);
@@ -1367,6 +1366,7 @@ RPK_INLINE KScene load_scene(KArgsPtr A) {
   S.lds_depth = A->S.lds_depth;
   S.spill = A->S.spill;
   S.rng_slab = A->S.rng_slab;
+  S.unit_t0 = A->S.unit_t0;
   return S;
 }
 

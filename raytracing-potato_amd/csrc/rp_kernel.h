@@ -26,6 +26,7 @@ struct KScene {
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
   uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
   uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) entries
+  uint32_t* unit_t0;     // per-lane start time of the lane's measured unit (tile costs), render_lanes words
 };
 
 // Bytes of keystream cache (ChaCha key, ring of main-stream blocks, jitter blocks) per resident lane of

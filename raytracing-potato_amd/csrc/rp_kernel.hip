@@ -31,6 +31,10 @@ static constexpr int PRIO_TRAV = 2, PRIO_SHADE = 1, PRIO_REFILL = 0;
 template <uint32_t NF>
 constexpr uint32_t RingFor = NF == rpl::NODES_Q8 ? 4u : RING;
 
+// Tile costs are measured on one unit in eight (pixel and batch hashed: every tile's sample spreads over its pixels
+// and batches) -- timing all units cost 0.9 %
+RPK_INLINE bool meas_unit(uint32_t pipj, uint32_t batch) { return ((pipj ^ (pipj >> 16) ^ batch ^ (pipj >> 3)) & 7u) == 0u; }
+
 // PROBE = the cost-probe launch (rp_kernel.h, cost-ordered tile scheduling): a separate symbol so profiles
 // and timings of the frame kernel never mix with it.
 template <bool PROBE, bool SPILL, uint32_t NF>
@@ -122,6 +126,9 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       DCYC_BEGIN(cr)
       rng_refill(rng, alive, fresh, seed, start ? s - 1 : s, unit_spp(A, batch));
       DCYC_END(DCYC_REFILL, cr)
+      // a measured unit's start (100 MHz real-time clock, the same on every XCD): its duration is its tile's cost
+      if (!PROBE && fresh && A->P.tile_meas && meas_unit(pipj, batch))
+        A->S.unit_t0[blockIdx.x * BLOCK + tid] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
     if (start) {
       KArgsPtr A = kargs();
@@ -241,8 +248,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           }
           // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas), from one unit in eight (pixel and
           // batch hashed: every tile's sample spread over its pixels and batches) -- timing all units cost 0.9 %
-          if (!PROBE && A->P.tile_meas && ((pipj ^ (pipj >> 16) ^ batch ^ (pipj >> 3)) & 7u) == 0u) {
-            const uint32_t t0 = reinterpret_cast<const uint32_t*>(rng.slab + RngT<RingFor<NF>>::meta)[0];
+          if (!PROBE && A->P.tile_meas && meas_unit(pipj, batch)) {
+            const uint32_t t0 = A->S.unit_t0[blockIdx.x * BLOCK + tid];
             meas_dur = ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0) >> MEAS_SHIFT;
             meas_k = slot / (A->P.tw * A->P.th);
           }

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "5537149adc242ddd"
+#define RP_BUILD_ID "8ea710addda81833"

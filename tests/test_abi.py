@@ -163,3 +163,16 @@ def test_profile_records_are_of_this_build():
         rec = json.load(open(os.path.join(REPO, rel)))
         assert rec["build_id"] == build, (cfg, rel, rec["build_id"], build)
         assert rec["config"] == cfg and rec["rays"] > 0 and rec["traffic_bytes_per_ray"] > 0
+
+
+def test_bench_cpu_fit_is_a_least_squares_line():
+    """bench.py's full-host CPU figure is a least-squares line through >= 3 measured worker counts,
+    not a two-point ratio: exact on collinear points, and its R^2 shows a bend."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    lin = b.fit_workers([{"workers": w, "value": 0.5 + 0.9 * w} for w in (1, 4, 8, 16)])
+    assert abs(lin["intercept"] - 0.5) < 1e-9 and abs(lin["per_worker"] - 0.9) < 1e-9 and lin["r2"] == 1.0
+    bent = b.fit_workers([{"workers": w, "value": v} for w, v in ((1, 1.0), (4, 4.0), (8, 7.0), (16, 11.0))])
+    assert bent["per_worker"] < 0.75 and bent["r2"] < 1.0 and bent["points"] == 4

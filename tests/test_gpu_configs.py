@@ -117,6 +117,60 @@ def test_one_stream_per_pixel_contract(gpu):
     assert st7["rays"] == ctr7["rays"]
 
 
+@pytest.mark.slow
+def test_c3_one_stream_per_pixel_full_size(gpu):
+    """SURVEY.md 8c's contract at a BASELINE config -- C3 (1920x1080x256) with samples_per_stream =
+    256, i.e. ONE StdRng per pixel (seed + j*W + i) running the reference's per-pixel body (main.rs:70-86) over all
+    256 samples.  The whole frame on the GPU; the oracle re-renders every 64th tile (shard 5 of 64) under the same
+    contract: parity bar, and the GPU's re-render of that shard has the oracle's ray and sample counts exactly and is
+    bitwise the full frame's pixels there."""
+    from rtpotato import scenes
+    scene, params = scenes.config_scene("C3")
+    params = replace(params, samples_per_stream=256)
+    with gpu.DeviceScene(scene) as ds:
+        rgb, _, st = ds.render(params)
+        assert st["pixels"] == params.width * params.height and st["samples"] == st["pixels"] * 256
+        sub = replace(params, tile_w=32, tile_h=32, shard=5, num_shards=64)
+        _sampled_shard_parity(gpu, scene, rgb, sub, ds=ds)
+        default, _, sd = ds.render(replace(sub, samples_per_stream=0))
+    m = shard_mask(sub)
+    assert not np.array_equal(default[m], rgb[m])  # the 32-sample batches are a different (equally valid) stream set
+
+
+@pytest.mark.slow
+def test_c4_balanced_shard_against_oracle(gpu):
+    """the deal N > 1 runs (RP_SHARD_BALANCED, bench.py's default for N > 1) at C4's full size
+    (1920x1080x1024): shard 3 of 8 of a balanced plan renders its planned tiles, and the oracle re-renders the
+    interleave-of-512 shard that shares the most tiles with it -- the shared pixels meet the parity bar, and the
+    GPU's re-render of that oracle shard has the oracle's ray and sample counts exactly and the balanced shard's
+    pixels bit for bit."""
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.scene import shard_slot_pixels
+    scene, params = scenes.config_scene("C4")
+    p = replace(params, shard=3, num_shards=8, shard_map=F.RP_SHARD_BALANCED)
+    with gpu.DeviceScene(scene) as ds:
+        rgb, _, st = ds.render(p)
+        order = ds.tile_map(p)
+        n_tiles = len(order)
+        assert not np.array_equal(order, np.arange(n_tiles))
+        mine = set(int(t) for t in order[3::8])
+        s = max(range(512), key=lambda s: sum(t in mine for t in range(s, n_tiles, 512)))
+        sub = replace(params, shard=s, num_shards=512)
+        pix = shard_slot_pixels(p, order)
+        m_bal = np.zeros(params.width * params.height, dtype=bool)
+        m_bal[pix[pix >= 0]] = True
+        m_bal = m_bal.reshape(params.height, params.width)
+        assert st["pixels"] == m_bal.sum() and st["samples"] == m_bal.sum() * 1024
+        m = m_bal & shard_mask(sub)
+        assert m.sum() >= 1024
+        ref, _, ctr = oracle_render(scene, sub, threads=16)
+        assert_parity(compare(rgb, ref, m))
+        sub_rgb, _, sst = ds.render(sub)
+    assert np.array_equal(sub_rgb[m], rgb[m])
+    assert (sst["rays"], sst["samples"]) == (ctr["rays"], ctr["samples"]), (sst, ctr)
+
+
 def test_async_render_needs_reservation(gpu):
     """rp_render_device never allocates: a multi-batch frame without rp_workspace_reserve is refused with
     RP_EINVAL (nothing launched); after the reservation it renders the rp_render image bit for bit."""

@@ -211,3 +211,36 @@ def test_learned_tile_costs(gpu):
         d, _, sd = ds.render(replace(p, shard_map=F.RP_SHARD_BALANCED))
     assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
     assert sa["rays"] == sb["rays"] == sc_["rays"] == sd["rays"]
+
+
+def test_frames_past_the_tile_table(gpu):
+    """a frame of more than TILE_SORT_MAX (16384) tiles -- 4 x 4 tiles at 640 x 480 = 19,200 -- is not
+    measured (the per-tile cost table holds 16384 tiles; the kernel's atomics and the gather's cost all-gathers would
+    run past it), and still renders: rp_render, and rp_render_gather on a 1-rank RCCL communicator (both shard maps:
+    the balanced plan falls back to the interleave past the table), equal the 16 x 16-tile frame bit for bit --
+    per-pixel seeding makes a pixel independent of the tiling."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.render import Comm, comm_unique_id
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.bunny_full(), 640, 480)
+    big = RenderParams(640, 480, 1, 8, scenes.DEFAULT_SEED, 16, 16)
+    small = RenderParams(640, 480, 1, 8, scenes.DEFAULT_SEED, 4, 4)
+    with gpu.DeviceScene(sc) as ds:
+        ref, _, st = ds.render(big)
+        for _ in range(2):  # the second frame of a workspace would schedule from a learned table
+            rgb, _, st2 = ds.render(small)
+            assert np.array_equal(rgb, ref) and st2["rays"] == st["rays"]
+        with Comm(comm_unique_id(), 1, 0, 0) as comm:
+            for mode in (F.RP_SHARD_INTERLEAVE, F.RP_SHARD_BALANCED):
+                q = replace(small, shard_map=mode)
+                ds.reserve(q)
+                frame = torch.zeros(640 * 480 * 3, dtype=torch.float64, device="cuda")
+                ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+                for _ in range(2):
+                    ctr.zero_()
+                    ds.render_gather(comm, q, frame_rgb=frame, counters=ctr)
+                    torch.cuda.synchronize()
+                    assert int(ctr[3]) == 0 and int(ctr[0]) == st["rays"]
+                    assert np.array_equal(frame.cpu().numpy().reshape(480, 640, 3), ref)

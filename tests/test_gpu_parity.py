@@ -317,6 +317,24 @@ def test_device_bvh_builder(gpu, name, arg, fmt, builder):
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
+@pytest.mark.parametrize("builder", ["ploc", "gpu", "host"])
+def test_nan_vertex_triangles_build_and_render(gpu, builder):
+    """NaN geometry: a mesh with a run of adjacent triangles whose vertices are all NaN.  Their boxes sort
+    together (Morton code 0), so PLOC's search window holds only NaN candidates; the nearest-neighbour pass ranks a NaN
+    distance as +inf and still names a neighbour (it used to leave -1, which the flags pass then read out of bounds).
+    The reference itself panics on such a mesh (bvh.rs:62 `partial_cmp().unwrap()` of a NaN centroid), so there is no
+    image to match: every builder must build the tree and render the frame with a clean status."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.random_mesh(200_000), 32, 32)
+    mesh = sc.scene_data.mesh_table[0]
+    mesh.positions[3 * 1000:3 * 1012] = np.nan  # triangles 1000..1011
+    with gpu.DeviceScene(sc, options={"builder": builder}) as ds:
+        assert ds.info()["nodes"] >= 1
+        rgb, _, st = ds.render(RenderParams(32, 32, 2, 8, scenes.DEFAULT_SEED))
+    assert st["rays"] > 0 and st["pixels"] == 32 * 32 and rgb.shape == (32, 32, 3)
+
+
 @pytest.mark.parametrize("fmt", ["f32", "q8"])
 @pytest.mark.parametrize("collapse", ["greedy", "sah"])
 def test_host_tree_collapse(gpu, collapse, fmt):

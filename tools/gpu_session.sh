@@ -1,0 +1,115 @@
+#!/bin/bash
+# The one GPU session script (run on the box through gpurun; every profiles/rN record names the step that made it).
+#
+#   TAG=r4a STEPS="tests bench_C3 trace_C3 pmc_C3" tools/gpu_session.sh
+#
+# STEPS, run in order, each under its own time limit; the first failure (a crash, abort or time limit) ends the session:
+#   tests              pytest -m gpu (PYTEST_ARGS, e.g. "-k c3 -m 'gpu and not slow'")
+#   bench_<CFG>        bench.py --config CFG (BENCH_ARGS appended; the CPU baseline only for C3 unless NO_CPU=1)
+#   shards_<CFG>       tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps
+#   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
+#   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
+#   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
+#   ab                 interleaved A/B timing: RUNS = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
+#                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
+#   abpmc              per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
+# Outputs: gpurun_out/${TAG}_*; gpurun_out/${TAG}_manifest.txt lists every output file with the command that made it.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-s}
+CFG=${CFG:-C3}
+P=gpurun_out/${TAG}_progress.txt
+M=gpurun_out/${TAG}_manifest.txt
+echo "start $(date +%T)" > $P
+: > $M
+step() { echo "$1 $(date +%T)" >> $P; }
+made() { echo "$1: $2" >> $M; }  # output file: command
+frames() { case $1 in C5) echo "3 1" ;; C4) echo "4 1" ;; *) echo "10 2" ;; esac; }
+pmc() {  # lib cfg name counters...
+  local lib=$1 cfg=$2 name=$3; shift 3
+  local out=gpurun_out/${TAG}_${cfg}_pmc_$name cmd
+  cmd="rocprofv3 --pmc $* -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline"
+  step "pmc $cfg $name"
+  made "$out" "RP_LIB=$lib $cmd"
+  RP_LIB=$lib timeout -s KILL 300 rocprofv3 --pmc "$@" -d $out -o run --output-format csv -- \
+    python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline > $out.json 2> $out.err
+}
+LIB=raytracing-potato_amd/lib/librp.so
+libpath() { [ "$1" = main ] && echo $LIB || echo raytracing-potato_amd/lib/librp_$1.so; }
+for s in ${STEPS:-tests}; do
+  case $s in
+    tests)
+      step tests
+      made gpurun_out/${TAG}_tests.log "pytest tests -m gpu ${PYTEST_ARGS:-}"
+      timeout -k 10 ${TESTS_LIMIT:-1200} python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
+        -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/${TAG}_tests.log 2>&1 || { step "tests failed"; exit 1; } ;;
+    bench_*)
+      cfg=${s#bench_}; read st wu <<< "$(frames $cfg)"
+      cpu=""; { [ $cfg != C3 ] || [ -n "${NO_CPU:-}" ]; } && cpu=--no-cpu-baseline
+      step "bench $cfg"
+      made gpurun_out/${TAG}_${cfg}_bench.json "python3 bench.py --config $cfg --steps $st --warmup $wu $cpu ${BENCH_ARGS:-}"
+      timeout -k 10 600 python3 bench.py --config $cfg --steps $st --warmup $wu $cpu ${BENCH_ARGS:-} \
+        > gpurun_out/${TAG}_${cfg}_bench.json 2> gpurun_out/${TAG}_${cfg}_bench.err || exit 1 ;;
+    shards_*)
+      cfg=${s#shards_}
+      step "shards $cfg"
+      made gpurun_out/${TAG}_${cfg}_shards.json "python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} ${SHARD_ARGS:-}"
+      timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} ${SHARD_ARGS:-} \
+        > gpurun_out/${TAG}_${cfg}_shards.json 2> gpurun_out/${TAG}_${cfg}_shards.err || exit 1 ;;
+    diag_*)
+      cfg=${s#diag_}
+      step "diag $cfg"
+      made gpurun_out/${TAG}_${cfg}_diag.json "RP_LIB=raytracing-potato_amd/lib/librp_diag.so python3 tools/diag.py --config $cfg --spp 256"
+      RP_LIB=raytracing-potato_amd/lib/librp_diag.so timeout -k 10 300 python3 tools/diag.py --config $cfg --spp 256 \
+        > gpurun_out/${TAG}_${cfg}_diag.json 2> gpurun_out/${TAG}_${cfg}_diag.err || exit 1 ;;
+    trace_*)
+      cfg=${s#trace_}; read st wu <<< "$(frames $cfg)"
+      step "trace $cfg"
+      made gpurun_out/${TAG}_${cfg}_trace "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline ${BENCH_ARGS:-}"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${cfg}_trace -o run --output-format csv -- \
+        python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline ${BENCH_ARGS:-} \
+        > gpurun_out/${TAG}_${cfg}_bench_under_rocprof.json 2> gpurun_out/${TAG}_${cfg}_trace.err || exit 1 ;;
+    pmc_*)
+      cfg=${s#pmc_}
+      pmc $LIB $cfg sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
+        SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT &&
+      pmc $LIB $cfg mix64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 \
+        SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_THREAD_CYCLES_VALU &&
+      pmc $LIB $cfg mix32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_TRANS_F32 \
+        SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS &&
+      pmc $LIB $cfg fetch FETCH_SIZE &&
+      pmc $LIB $cfg write WRITE_SIZE &&
+      pmc $LIB $cfg l2 TCC_HIT_sum TCC_MISS_sum || exit 1
+      lc=$(echo $cfg | tr A-Z a-z)
+      made gpurun_out/${TAG}_${lc}_roofline.json "python3 tools/roofline.py --config $cfg over the six pmc passes above"
+      python3 tools/roofline.py --config $cfg --bench gpurun_out/${TAG}_${cfg}_pmc_sq.json \
+        $([ -f gpurun_out/${TAG}_${cfg}_diag.json ] && echo --diag gpurun_out/${TAG}_${cfg}_diag.json) \
+        --out gpurun_out/${TAG}_${lc}_roofline.json \
+        gpurun_out/${TAG}_${cfg}_pmc_sq gpurun_out/${TAG}_${cfg}_pmc_mix64 gpurun_out/${TAG}_${cfg}_pmc_mix32 \
+        gpurun_out/${TAG}_${cfg}_pmc_fetch gpurun_out/${TAG}_${cfg}_pmc_write gpurun_out/${TAG}_${cfg}_pmc_l2 \
+        > gpurun_out/${TAG}_${cfg}_roofline.log 2>&1 || exit 1 ;;
+    ab)
+      read st wu <<< "$(frames $CFG)"
+      for rep in $(seq 1 ${REPS:-2}); do
+        for run in $RUNS; do
+          name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}; opts=${rest#*:}
+          args=""
+          for o in $(echo $opts | tr ',' ' '); do args="$args --opt $o"; done
+          out=gpurun_out/${TAG}_${name}_$rep.json
+          step "ab $rep $name"
+          made $out "RP_LIB=$(libpath $lib) python3 bench.py --config $CFG --steps ${STEPS_AB:-$st} --warmup $wu --no-cpu-baseline $args ${BENCH_ARGS:-}"
+          RP_LIB=$(libpath $lib) timeout -k 10 300 python3 bench.py --config $CFG --steps ${STEPS_AB:-$st} --warmup $wu \
+            --no-cpu-baseline $args ${BENCH_ARGS:-} > $out 2> ${out%.json}.err || exit 1
+        done
+      done ;;
+    abpmc)
+      for run in $RUNS; do
+        name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}
+        pmc $(libpath $lib) $CFG ${name}_fetch FETCH_SIZE && pmc $(libpath $lib) $CFG ${name}_write WRITE_SIZE || exit 1
+      done ;;
+    *) echo "unknown step $s" >> $P; exit 2 ;;
+  esac
+done
+step done
