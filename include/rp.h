@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 6
+#define RP_ABI_VERSION 7
 
 /* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -223,6 +223,11 @@ enum { RP_QUEUES_AUTO = 0, RP_QUEUES_SINGLE = 1, RP_QUEUES_XCD_TILES = 2, RP_QUE
  * of largest surface area until a node has 4 children; SAH takes the cut through the binary subtree that minimises
  * the 4-wide tree's SAH cost (dynamic program).  Never changes an image beyond exact-t ties. */
 enum { RP_COLLAPSE_AUTO = 0, RP_COLLAPSE_GREEDY = 1, RP_COLLAPSE_SAH = 2 };
+/* rp_scene_options.node_layout (ABI v7): the memory order of a device-built (PLOC) tree's wide nodes.  DFS: depth-first,
+ * a node's inner children as one consecutive family; DFS_LINE: the same with every family starting on a 128-B cache
+ * line (64-B quantized nodes: a pad slot after odd families; f32 nodes are one line each, so the same as DFS).  Speed
+ * only: the image never depends on it. */
+enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles); PLOC */
@@ -247,6 +252,7 @@ typedef struct rp_scene_options {
                                depth the tree needs.  Too small a stack drops entries -- wrong frames -- and the
                                render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */
   uint32_t collapse;        /* RP_COLLAPSE_*: the 4-wide collapse of the host-built tree (ABI v6) */
+  uint32_t node_layout;     /* RP_LAYOUT_*: node order of a device-built (PLOC) tree (ABI v7) */
 } rp_scene_options;
 
 typedef struct rp_stats {

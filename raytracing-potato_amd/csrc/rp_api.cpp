@@ -362,6 +362,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.debug_stack_depth != 0 && (o.debug_stack_depth < 8 || o.debug_stack_depth > 4096))
     return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
   if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
+  if (o.node_layout > RP_LAYOUT_DFS_LINE) return fail(RP_EINVAL, "options.node_layout must be RP_LAYOUT_*");
   return RP_OK;
 }
 
@@ -491,7 +492,10 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
                                                    : (uint32_t)rpl::NODES_F32;
     rpg::GpuTree gt;
     const uint32_t algo = opt.builder == RP_BUILDER_PLOC ? rpg::GPU_PLOC : rpg::GPU_LBVH;
-    if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, algo, opt.cost_traverse, gt, err))) return bail(fail(rc, err));
+    // node families on 128-B lines (RP_LAYOUT_DFS_LINE) for 64-B quantized nodes; f32 nodes are a line each
+    const uint32_t align = opt.node_layout == RP_LAYOUT_DFS_LINE && node_format == rpl::NODES_Q8 ? 2u : 1u;
+    if ((rc = rpg::build_gpu(pin, opt.max_leaf, node_format, algo, opt.cost_traverse, align, gt, err)))
+      return bail(fail(rc, err));
     s->d_nodes = gt.d_nodes;
     s->d_prims = gt.d_prims;
     s->d_prim_refs = gt.d_prim_refs;

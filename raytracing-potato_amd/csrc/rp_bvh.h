@@ -122,7 +122,8 @@ struct GpuTree {
 // bits split), GPU_PLOC = Meister & Bittner 2018 (agglomerative, SAH quality).
 enum { GPU_LBVH = 0, GPU_PLOC = 1 };
 // cost_traverse: the SAH node cost relative to a primitive test (PLOC's leaf decisions; rp_scene_options).
+// align: PLOC's depth-first node families start at multiples of this many nodes (pad slots zero; RP_LAYOUT_DFS_LINE).
 int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, uint32_t algo, double cost_traverse,
-              GpuTree& out, std::string& err);
+              uint32_t align, GpuTree& out, std::string& err);
 
 }  // namespace rpg

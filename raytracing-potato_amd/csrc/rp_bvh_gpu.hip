@@ -306,7 +306,9 @@ unsigned grid(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / 
 // its family first -- right behind the family, in child order), so a descent walks forward through memory.  The
 // relayout: per level (the collapse's frontiers, recorded), bottom-up the number of wide nodes below each node, then
 // top-down each node's new index and the start of its family, then every record copied to its new index with its
-// inner child indices renamed.  Leaf entries and the primitive order are unchanged.
+// inner child indices renamed.  Leaf entries and the primitive order are unchanged.  `align` (nodes): every family
+// starts at a multiple of it -- 2 puts a 64-B quantized node's family on 128-B cache lines (RP_LAYOUT_DFS_LINE; the
+// pad slots are zero and never referenced), 1 packs the families.
 template <uint32_t NF>
 __device__ __forceinline__ const uint32_t* node_children(const void* nodes, uint32_t i) {
   typedef typename std::conditional<NF == rpl::NODES_Q8, rpl::Node4Q, rpl::Node4>::type NodeT;
@@ -321,20 +323,23 @@ __global__ void record_level_kernel(const uint32_t* __restrict__ wide_of, uint32
 
 template <uint32_t NF>
 __global__ void subtree_count_kernel(const uint32_t* __restrict__ ids, uint32_t n, const void* __restrict__ nodes,
-                                     uint32_t* __restrict__ below) {
+                                     uint32_t align, uint32_t* __restrict__ below) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t u = ids[i];
   const uint32_t* ch = node_children<NF>(nodes, u);
-  uint32_t f = 0;
+  uint32_t f = 0, m = 0;
   for (int k = 0; k < 4; k++)
-    if (!(ch[k] & rpl::ENTRY_LEAF)) f += 1u + below[ch[k]];
-  below[u] = f;
+    if (!(ch[k] & rpl::ENTRY_LEAF)) {
+      m++;
+      f += below[ch[k]];
+    }
+  below[u] = f + (m + align - 1) / align * align;  // the family (padded) and the children's own subtrees
 }
 
 template <uint32_t NF>
 __global__ void dfs_index_kernel(const uint32_t* __restrict__ ids, uint32_t n, const void* __restrict__ nodes,
-                                 const uint32_t* __restrict__ below, uint32_t* __restrict__ newid,
+                                 const uint32_t* __restrict__ below, uint32_t align, uint32_t* __restrict__ newid,
                                  uint32_t* __restrict__ fam) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -342,7 +347,7 @@ __global__ void dfs_index_kernel(const uint32_t* __restrict__ ids, uint32_t n, c
   const uint32_t* ch = node_children<NF>(nodes, u);
   uint32_t m = 0;
   for (int k = 0; k < 4; k++) m += !(ch[k] & rpl::ENTRY_LEAF);
-  uint32_t slot = fam[u], next = fam[u] + m;
+  uint32_t slot = fam[u], next = fam[u] + (m + align - 1) / align * align;
   for (int k = 0; k < 4; k++) {
     const uint32_t c = ch[k];
     if (c & rpl::ENTRY_LEAF) continue;
@@ -366,40 +371,44 @@ __global__ void relayout_kernel(uint32_t n, const void* __restrict__ nodes, cons
 
 // Renumber the n_nodes wide nodes of `nodes` depth-first (see above); `level_ids` holds each collapse level's wide
 // node ids (level k at level_off[k] .. level_off[k + 1]).  Replaces *nodes (the old buffer is freed).
-int dfs_relayout(void** nodes, uint32_t node_format, uint64_t n_nodes, const uint32_t* level_ids,
-                 const std::vector<uint32_t>& level_off, std::string& err) {
+int dfs_relayout(void** nodes, uint32_t node_format, uint64_t* n_nodes_io, const uint32_t* level_ids,
+                 const std::vector<uint32_t>& level_off, uint32_t align, std::string& err) {
+  const uint64_t n_nodes = *n_nodes_io;
   const size_t nb = node_format == rpl::NODES_Q8 ? sizeof(rpl::Node4Q) : sizeof(rpl::Node4);
   uint32_t *below = nullptr, *newid = nullptr, *fam = nullptr;
   void* out = nullptr;
   hipError_t e = hipMalloc((void**)&below, sizeof(uint32_t) * n_nodes);
   if (e == hipSuccess) e = hipMalloc((void**)&newid, sizeof(uint32_t) * n_nodes);
   if (e == hipSuccess) e = hipMalloc((void**)&fam, sizeof(uint32_t) * n_nodes);
-  if (e == hipSuccess) e = hipMalloc(&out, nb * n_nodes);
   const unsigned B = 256;
   const uint32_t L = (uint32_t)level_off.size() - 1;
   for (uint32_t k = L; k-- > 0 && e == hipSuccess;) {
     const uint32_t n = level_off[k + 1] - level_off[k];
     if (node_format == rpl::NODES_Q8)
       hipLaunchKernelGGL(subtree_count_kernel<rpl::NODES_Q8>, dim3(grid(n, B)), dim3(B), 0, nullptr, level_ids + level_off[k],
-                         n, *nodes, below);
+                         n, *nodes, align, below);
     else
       hipLaunchKernelGGL(subtree_count_kernel<rpl::NODES_F32>, dim3(grid(n, B)), dim3(B), 0, nullptr, level_ids + level_off[k],
-                         n, *nodes, below);
+                         n, *nodes, align, below);
     e = hipGetLastError();
   }
-  const uint32_t root_new = 0, root_fam = 1;
-  uint32_t root = 0;
+  const uint32_t root_new = 0, root_fam = align;  // the root, padded to the alignment, then its family
+  uint32_t root = 0, below_root = 0;
   if (e == hipSuccess) e = hipMemcpy(&root, level_ids, sizeof root, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(&below_root, below + root, sizeof below_root, hipMemcpyDeviceToHost);
+  const uint64_t total = (uint64_t)root_fam + below_root;  // == n_nodes when align == 1
+  if (e == hipSuccess) e = hipMalloc(&out, nb * total);
+  if (e == hipSuccess && total != n_nodes) e = hipMemset(out, 0, nb * total);
   if (e == hipSuccess) e = hipMemcpy(newid + root, &root_new, sizeof root_new, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(fam + root, &root_fam, sizeof root_fam, hipMemcpyHostToDevice);
   for (uint32_t k = 0; k < L && e == hipSuccess; k++) {
     const uint32_t n = level_off[k + 1] - level_off[k];
     if (node_format == rpl::NODES_Q8)
       hipLaunchKernelGGL(dfs_index_kernel<rpl::NODES_Q8>, dim3(grid(n, B)), dim3(B), 0, nullptr, level_ids + level_off[k], n,
-                         *nodes, below, newid, fam);
+                         *nodes, below, align, newid, fam);
     else
       hipLaunchKernelGGL(dfs_index_kernel<rpl::NODES_F32>, dim3(grid(n, B)), dim3(B), 0, nullptr, level_ids + level_off[k], n,
-                         *nodes, below, newid, fam);
+                         *nodes, below, align, newid, fam);
     e = hipGetLastError();
   }
   if (e == hipSuccess) {
@@ -420,6 +429,7 @@ int dfs_relayout(void** nodes, uint32_t node_format, uint64_t n_nodes, const uin
   }
   (void)hipFree(*nodes);
   *nodes = out;
+  *n_nodes_io = total;
   return RP_OK;
 }
 
@@ -651,8 +661,8 @@ namespace {
 // PLOC build (see the kernels above) from the Morton-sorted keys, then the depth-first collapse; fills out.d_nodes
 // and out.d_prims / d_prim_refs (permuted).  Device buffers: boxes / prims_in / refs_in in hittable order.
 int build_ploc(uint32_t n, const uint32_t* d_order, const Box6* d_boxes, const rpl::Prim* d_prims_in,
-               const rpl::PrimRef* d_refs_in, uint32_t max_leaf, double cost_traverse, uint32_t node_format, GpuTree& out,
-               std::string& err) {
+               const rpl::PrimRef* d_refs_in, uint32_t max_leaf, double cost_traverse, uint32_t node_format, uint32_t align,
+               GpuTree& out, std::string& err) {
   std::vector<void*> tmp;
   hipError_t e = hipSuccess;
   auto alloc = [&](void** p, size_t bytes) {
@@ -770,7 +780,7 @@ int build_ploc(uint32_t n, const uint32_t* d_order, const Box6* d_boxes, const r
   out.max_depth = depth;
   {
     std::string rerr;
-    const int rc = dfs_relayout(&out.d_nodes, node_format, out.n_nodes, d_levels, level_off, rerr);
+    const int rc = dfs_relayout(&out.d_nodes, node_format, &out.n_nodes, d_levels, level_off, align, rerr);
     if (rc) return done(rc, rerr);
   }
   hipLaunchKernelGGL(permute_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_perm, d_prims_in, d_refs_in, out.d_prims,
@@ -786,7 +796,7 @@ int build_ploc(uint32_t n, const uint32_t* d_order, const Box6* d_boxes, const r
 
 // Temporaries are freed on every path; on success the caller owns out.d_nodes / d_prims / d_prim_refs.
 int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format, uint32_t algo, double cost_traverse,
-              GpuTree& out, std::string& err) {
+              uint32_t align, GpuTree& out, std::string& err) {
   out = GpuTree{};
   const uint32_t n = (uint32_t)in.prims.size();
   if (n < 2) {
@@ -889,7 +899,8 @@ int build_gpu(const rpb::PrimInput& in, uint32_t max_leaf, uint32_t node_format,
     out.node_format = node_format;
     out.qbound = rpl::qbound(in.amax);
     std::string perr;
-    const int rc = build_ploc(n, d_order, d_boxes, d_prims_in, d_refs_in, max_leaf, cost_traverse, node_format, out, perr);
+    const int rc = build_ploc(n, d_order, d_boxes, d_prims_in, d_refs_in, max_leaf, cost_traverse, node_format,
+                                std::max(1u, align), out, perr);
     return cleanup(rc, perr);
   }
   hipLaunchKernelGGL(morton_kernel, dim3(grid(n, B)), dim3(B), 0, nullptr, n, d_boxes, cmin,

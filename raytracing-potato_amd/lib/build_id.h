@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "8ea710addda81833"
+#define RP_BUILD_ID "d5e8b9da5e0643ae"

@@ -32,9 +32,10 @@ RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
 RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 0, 1, 2, 3, 4
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 RP_COLLAPSE_AUTO, RP_COLLAPSE_GREEDY, RP_COLLAPSE_SAH = 0, 1, 2
+RP_LAYOUT_AUTO, RP_LAYOUT_DFS, RP_LAYOUT_DFS_LINE = 0, 1, 2
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
-RP_ABI_VERSION = 6
+RP_ABI_VERSION = 7
 
 
 class rp_hittable(Structure):
@@ -94,7 +95,7 @@ class rp_scene_options(Structure):
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
                 ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
                 ("unit_queues", c_uint32), ("queue_chunk", c_uint32), ("debug_stack_depth", c_uint32),
-                ("collapse", c_uint32)]
+                ("collapse", c_uint32), ("node_layout", c_uint32)]
 
 
 class rp_stats(Structure):

@@ -317,6 +317,24 @@ def test_device_bvh_builder(gpu, name, arg, fmt, builder):
     _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED), options=opt)
 
 
+def test_ploc_line_aligned_node_families(gpu):
+    """rp_scene_options.node_layout = RP_LAYOUT_DFS_LINE (ABI v7): the PLOC tree's 64-B quantized nodes laid out depth
+    first with every family of inner children starting on a 128-B line (zero pad slots after odd families, never
+    referenced).  More node slots than the packed layout, the structural self-check passes (it walks from the root),
+    and the image and ray counts are the oracle's."""
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.random_mesh(200_000), 64, 40)
+    nodes = {}
+    for layout in ("dfs", "dfs_line"):
+        opt = {"builder": "ploc", "node_format": "q8", "node_layout": layout, "self_check": 1}
+        with gpu.DeviceScene(sc, options=opt) as ds:
+            nodes[layout] = ds.info()["nodes"]
+    assert nodes["dfs"] < nodes["dfs_line"] < 1.5 * nodes["dfs"], nodes
+    _check(gpu, sc, RenderParams(64, 40, 4, 8, scenes.DEFAULT_SEED),
+           options={"builder": "ploc", "node_format": "q8", "node_layout": "dfs_line"})
+
+
 @pytest.mark.parametrize("builder", ["ploc", "gpu", "host"])
 def test_nan_vertex_triangles_build_and_render(gpu, builder):
     """NaN geometry: a mesh with a run of adjacent triangles whose vertices are all NaN.  Their boxes sort

@@ -10,6 +10,7 @@
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
+#   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
 #   ab                 interleaved A/B timing: RUNS = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
 #                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
 #   abpmc              per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
@@ -90,6 +91,11 @@ for s in ${STEPS:-tests}; do
         gpurun_out/${TAG}_${cfg}_pmc_sq gpurun_out/${TAG}_${cfg}_pmc_mix64 gpurun_out/${TAG}_${cfg}_pmc_mix32 \
         gpurun_out/${TAG}_${cfg}_pmc_fetch gpurun_out/${TAG}_${cfg}_pmc_write gpurun_out/${TAG}_${cfg}_pmc_l2 \
         > gpurun_out/${TAG}_${cfg}_roofline.log 2>&1 || exit 1 ;;
+    lat_*)  # memory-latency picture: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of fills
+      cfg=${s#lat_}
+      pmc $LIB $cfg lat_tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum \
+        TCP_TCC_READ_REQ_sum &&
+      pmc $LIB $cfg lat_tcc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_REQ_sum || exit 1 ;;
     ab)
       read st wu <<< "$(frames $CFG)"
       for rep in $(seq 1 ${REPS:-2}); do
