@@ -11,9 +11,9 @@
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
-#   ab                 interleaved A/B timing: RUNS = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
+#   ab[_<CFG>]         interleaved A/B timing: RUNS (or RUNS_<CFG>) = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
 #                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
-#   abpmc              per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
+#   abpmc[_<CFG>]      per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
 # Outputs: gpurun_out/${TAG}_*; gpurun_out/${TAG}_manifest.txt lists every output file with the command that made it.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -96,22 +96,26 @@ for s in ${STEPS:-tests}; do
       pmc $LIB $cfg lat_tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum \
         TCP_TCC_READ_REQ_sum &&
       pmc $LIB $cfg lat_tcc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_REQ_sum || exit 1 ;;
-    ab)
+    ab|ab_*)
+      [ "$s" != ab ] && CFG=${s#ab_}
       read st wu <<< "$(frames $CFG)"
+      runs_var=RUNS_$CFG; runs=${!runs_var:-$RUNS}  # RUNS_<CFG> overrides RUNS for that config
       for rep in $(seq 1 ${REPS:-2}); do
-        for run in $RUNS; do
+        for run in $runs; do
           name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}; opts=${rest#*:}
           args=""
           for o in $(echo $opts | tr ',' ' '); do args="$args --opt $o"; done
-          out=gpurun_out/${TAG}_${name}_$rep.json
+          out=gpurun_out/${TAG}_${CFG}_${name}_$rep.json
           step "ab $rep $name"
           made $out "RP_LIB=$(libpath $lib) python3 bench.py --config $CFG --steps ${STEPS_AB:-$st} --warmup $wu --no-cpu-baseline $args ${BENCH_ARGS:-}"
           RP_LIB=$(libpath $lib) timeout -k 10 300 python3 bench.py --config $CFG --steps ${STEPS_AB:-$st} --warmup $wu \
             --no-cpu-baseline $args ${BENCH_ARGS:-} > $out 2> ${out%.json}.err || exit 1
         done
       done ;;
-    abpmc)
-      for run in $RUNS; do
+    abpmc|abpmc_*)
+      [ "$s" != abpmc ] && CFG=${s#abpmc_}
+      runs_var=RUNS_$CFG; runs=${!runs_var:-$RUNS}
+      for run in $runs; do
         name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}
         pmc $(libpath $lib) $CFG ${name}_fetch FETCH_SIZE && pmc $(libpath $lib) $CFG ${name}_write WRITE_SIZE || exit 1
       done ;;
