@@ -85,6 +85,14 @@ void dfree(void* p) {
 constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
 constexpr uint32_t DEF_UNIT_QUEUES = RP_QUEUES_XCD_TILES;
 constexpr double DEF_COST_TRAVERSE = 0.7;
+// Balanced plans of scenes past the Infinity Cache deal square blocks of tiles (rpk::launch_tile_plan): 4 x 4, or 2 x 2,
+// as long as every rank still gets >= PLAN_UNITS_MIN of them (balance needs many units per rank), else single tiles.
+constexpr uint32_t PLAN_UNITS_MIN = 32;
+uint32_t plan_block(uint32_t n_tiles, uint32_t nranks) {
+  for (uint32_t b : {4u, 2u})
+    if (n_tiles >= PLAN_UNITS_MIN * nranks * b * b) return b;
+  return 1u;
+}
 
 }  // namespace
 
@@ -757,7 +765,11 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
       if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
       frame_cost = w->d_tile_cost;
     }
-    int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, w->d_plan, w->d_sort, stream);
+    // scenes past the Infinity Cache (Z-order tiles) deal square blocks of tiles: a rank's tiles stay in compact
+    // squares of the frame, so its working set does too (C5 8-way shards: DESIGN.md 6); cache-resident scenes deal
+    // tile by tile
+    const uint32_t block = order_mode == RP_TILES_MORTON ? plan_block(t.n_tiles, t.shards) : 1u;
+    int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, t.tiles_x, block, w->d_plan, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile plan launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_map = w->d_plan;
     tg.map = w->d_plan;

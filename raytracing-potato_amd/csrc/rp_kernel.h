@@ -142,8 +142,9 @@ struct TileGeom {
   uint32_t map_tiles;
   uint32_t cost_by_tile;  // 1: cost[] is indexed by frame tile (a whole-frame probe), 0: by shard tile
 };
-// scratch: SORT_SCRATCH words of device memory (the sort's keys; not LDS, see rp_kernel.hip SORT_BLOCK).
-enum { SORT_SCRATCH = TILE_SORT_MAX + 1 };
+// scratch: SORT_SCRATCH words of device memory (the sort's keys, the plan's hash word and its per-block costs; not
+// LDS, see rp_kernel.hip SORT_BLOCK).
+enum { SORT_SCRATCH = 2 * TILE_SORT_MAX + 1 };
 int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const TileGeom& g, uint32_t* order,
                      uint64_t* scratch, void* stream);
 
@@ -168,13 +169,16 @@ struct FrameGeom {
                              // pos / nranks); NULL = interleave (pos = the tile index)
 };
 
-// Balanced tile plan (rp.h RP_SHARD_BALANCED): from a whole-frame cost probe (cost[t] = summed probed work of frame
-// tile t, deterministic: the probe traverses without the speculative and early-exit steps), the n frame tiles are
-// sorted by cost (descending, ties by tile index) and dealt longest-processing-time first to the least-loaded of
-// `nranks` ranks that still has room for a tile, every rank receiving exactly the interleave's tile count.  Writes
-// plan[0, n) = the deal order (tile of shard s, shard tile k at plan[s + k * nranks]), plan[n, 2n) = its inverse
-// and plan[2n, 2n+2) = a 64-bit hash of the order (compared across ranks in the frame gather).  One block.
-int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, uint64_t* scratch, void* stream);
+// Balanced tile plan (rp.h RP_SHARD_BALANCED): from per-frame-tile costs (cost[t]: a learned table, or a whole-frame
+// probe, deterministic: the probe traverses without the speculative and early-exit steps), the n frame tiles are
+// grouped into blocks of block x block tiles (block = 1: single tiles), the blocks sorted by summed cost (descending,
+// ties by block index) and dealt in rounds of nranks blocks alternating direction ("snake"), the tiles past the last
+// whole round one at a time -- every rank receiving exactly the interleave's tile count.  Blocks keep a rank's tiles
+// in compact squares of the frame, so a scene past the Infinity Cache keeps its working set small on every rank.
+// Writes plan[0, n) = the deal order (tile of shard s, shard tile k at plan[s + k * nranks]), plan[n, 2n) = its
+// inverse and plan[2n, 2n+2) = a 64-bit hash of the order (compared across ranks in the frame gather).  One block.
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t tiles_x, uint32_t block, uint32_t* plan,
+                     uint64_t* scratch, void* stream);
 // Counters of a frame gather: stage this rank's block (ctr may be NULL = zeros; hash may be NULL = 0) for the
 // all-gather, and reduce the gathered blocks of nranks ranks into out (sums; status bits OR-ed, plus
 // STATUS_PLAN_MISMATCH when two ranks' plan hashes differ).

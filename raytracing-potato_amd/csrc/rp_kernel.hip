@@ -593,13 +593,15 @@ int launch_tile_sort(const uint32_t* cost, uint32_t n, uint32_t probe_px, const 
 }
 
 // Balanced tile plan (rp_kernel.h launch_tile_plan).  One block: the n frame tiles sorted by 64-bit key
-// (~cost << 32 | tile: descending cost, ties by tile index; 16384 tiles = 128 KB of global scratch), then dealt in rounds of nranks tiles, alternating direction ("snake": round k gives its tiles to ranks
-// 0..N-1 when k is even, N-1..0 when odd, so each pair of rounds gives every rank one tile from the costly end and
-// one from the cheap end of the pair's 2N-tile range), the last partial round forward -- every rank gets exactly
-// the interleave's tile count, so shard sizes and gather strides do not change.  The deal is parallel (position p
-// of the sorted order -> deal slot k * N + rank), its imbalance is second order in the cost curve (a greedy LPT
-// step per tile would be a serial loop of n wave reductions).  Deterministic: integer keys, no atomics but the
-// order-free hash sum.
+// (~block cost << 32 | block << 14 | tile: descending block cost, a block's tiles together; 16384 tiles = 128 KB of
+// global scratch), then dealt in units of block x block sorted positions, rounds of nranks units alternating direction
+// ("snake": round k gives its units to ranks 0..N-1 when k is even, N-1..0 when odd, so each pair of rounds gives
+// every rank one unit from the costly and one from the cheap end of the pair's 2N-unit range), and the positions past
+// the last whole round tile by tile the same way, the last partial round forward -- every rank gets exactly the
+// interleave's tile count, so shard sizes and gather strides do not change.  With block = 1 this is the per-tile deal
+// (block index = tile index).  The deal is parallel (position p of the sorted order -> rank and shard tile), its
+// imbalance is second order in the cost curve (a greedy LPT step per tile would be a serial loop of n wave
+// reductions).  Deterministic: integer keys and sums, no atomics but order-free integer adds.
 static constexpr int PLAN_BLOCK = SORT_BLOCK;
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -607,21 +609,47 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   return z ^ (z >> 31);
 }
 __global__ void __launch_bounds__(PLAN_BLOCK) tile_plan_kernel(const uint32_t* __restrict__ cost, uint32_t n,
-                                                               uint32_t np2, uint32_t N, uint32_t* __restrict__ plan,
+                                                               uint32_t np2, uint32_t N, uint32_t tiles_x, uint32_t bs,
+                                                               uint32_t* __restrict__ plan,
                                                                unsigned long long* __restrict__ key) {
-  // key[TILE_SORT_MAX]: the plan hash's accumulator (global, like the keys: no LDS, see SORT_BLOCK)
+  // scratch: key[0, np2) the sort keys, key[TILE_SORT_MAX] the plan hash's accumulator, key[TILE_SORT_MAX + 1 + b] block
+  // b's summed cost (global, like the keys: no LDS, see SORT_BLOCK)
   unsigned long long* hash = key + TILE_SORT_MAX;
+  unsigned long long* bcost = key + TILE_SORT_MAX + 1;
+  const uint32_t bx_n = (tiles_x + bs - 1) / bs;
+  auto block_of = [&](uint32_t t) { return (t / tiles_x / bs) * bx_n + (t % tiles_x) / bs; };
   if (threadIdx.x == 0) *hash = 0;
-  for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK)
-    key[i] = i < n ? ((uint64_t)(0xFFFFFFFFu - cost[i]) << 32) | i : ~0ull;
+  for (uint32_t i = threadIdx.x; i < n; i += PLAN_BLOCK) bcost[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += PLAN_BLOCK) atomicAdd(&bcost[block_of(i)], (unsigned long long)cost[i]);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < np2; i += PLAN_BLOCK) {
+    if (i < n) {
+      const uint32_t b = block_of(i);
+      const uint64_t c = min(bcost[b], 0xFFFFFFFFull);
+      key[i] = ((0xFFFFFFFFull - c) << 32) | ((uint64_t)b << 14) | i;
+    } else {
+      key[i] = ~0ull;
+    }
+  }
   __syncthreads();
   bitonic_global(key, np2);
-  const uint32_t full = n / N;  // complete rounds
+  const uint32_t U = bs * bs, R = n / (U * N), head = R * U * N;  // whole rounds of N units
+  const uint32_t tail_full = (n - head) / N;                        // whole tile rounds past them
   uint64_t h = 0;
   for (uint32_t p = threadIdx.x; p < n; p += PLAN_BLOCK) {
-    const uint32_t t = (uint32_t)key[p], k = p / N, i = p - k * N;
-    const uint32_t rank = (k < full && (k & 1u)) ? N - 1u - i : i;
-    const uint32_t pos = k * N + rank;
+    const uint32_t t = (uint32_t)key[p] & 0x3FFFu;
+    uint32_t rank, j;
+    if (p < head) {
+      const uint32_t u = p / U, k = u / N, i = u - k * N;
+      rank = (k & 1u) ? N - 1u - i : i;
+      j = k * U + (p - u * U);
+    } else {
+      const uint32_t q = p - head, k = q / N, i = q - k * N;
+      rank = (k < tail_full && (k & 1u)) ? N - 1u - i : i;
+      j = R * U + k;
+    }
+    const uint32_t pos = j * N + rank;
     plan[pos] = t;
     plan[n + t] = pos;
     h += mix64(((uint64_t)pos << 32) | t);
@@ -635,12 +663,13 @@ __global__ void __launch_bounds__(PLAN_BLOCK) tile_plan_kernel(const uint32_t* _
   }
 }
 
-int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t* plan, uint64_t* scratch, void* stream) {
-  if (n == 0 || n > TILE_SORT_MAX || nranks == 0) return (int)hipErrorInvalidValue;
+int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t tiles_x, uint32_t block, uint32_t* plan,
+                     uint64_t* scratch, void* stream) {
+  if (n == 0 || n > TILE_SORT_MAX || nranks == 0 || tiles_x == 0 || block == 0) return (int)hipErrorInvalidValue;
   uint32_t np2 = 1;
   while (np2 < n) np2 <<= 1;
-  hipLaunchKernelGGL(tile_plan_kernel, dim3(1), dim3(PLAN_BLOCK), 0, (hipStream_t)stream, cost, n, np2, nranks, plan,
-                     reinterpret_cast<unsigned long long*>(scratch));
+  hipLaunchKernelGGL(tile_plan_kernel, dim3(1), dim3(PLAN_BLOCK), 0, (hipStream_t)stream, cost, n, np2, nranks, tiles_x,
+                     block, plan, reinterpret_cast<unsigned long long*>(scratch));
   return (int)hipGetLastError();
 }
 

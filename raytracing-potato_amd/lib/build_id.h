@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "d5e8b9da5e0643ae"
+#define RP_BUILD_ID "96aa69cf214ccf75"

@@ -47,20 +47,40 @@ def assemble_frame(gathered: np.ndarray, params: RenderParams, world: int, tile_
     return gathered[slot]
 
 
-def deal_tiles(cost, world: int) -> np.ndarray:
-    """NumPy restatement of the balanced tile plan's deal (rp_kernel.hip tile_plan_kernel, RP_SHARD_BALANCED):
-    tiles sorted by cost descending (ties by tile index), dealt in rounds of `world` alternating direction (round k
-    to ranks 0..world-1 when k is even, world-1..0 when odd; the last partial round forward).  Returns the deal
-    order: shard s's k-th tile is order[s + k * world]."""
+def deal_tiles(cost, world: int, tiles_x: int = 0, block: int = 1) -> np.ndarray:
+    """NumPy restatement of the balanced tile plan's deal (rp_kernel.hip tile_plan_kernel, RP_SHARD_BALANCED): the frame
+    tiles (row-major, `tiles_x` a row) grouped into blocks of block x block tiles, the tiles sorted by their block's
+    summed cost descending (ties by block index, then tile index), then dealt in units of block**2 sorted positions,
+    rounds of `world` units alternating direction (round k to ranks 0..world-1 when k is even, world-1..0 when odd),
+    the positions past the last whole round one at a time the same way (the last partial round forward).  block = 1:
+    tile by tile.  Returns the deal order: shard s's k-th tile is order[s + k * world]."""
     cost = np.asarray(cost, dtype=np.int64)
     n = len(cost)
-    srt = np.lexsort((np.arange(n), -cost))  # cost descending, then tile index
+    t = np.arange(n)
+    if block > 1:
+        bx_n = -(-tiles_x // block)
+        b = (t // tiles_x // block) * bx_n + (t % tiles_x) // block
+    else:
+        b = t
+    bcost = np.zeros(n, dtype=np.int64)
+    np.add.at(bcost, b, cost)
+    bc = np.minimum(bcost[b], 0xFFFFFFFF)
+    srt = np.lexsort((t, b, -bc))  # block cost descending, then block, then tile
+    U = block * block
+    R = n // (U * world)
+    head = R * U * world
+    tail_full = (n - head) // world
     p = np.arange(n)
-    k, i = p // world, p % world
-    full = n // world
-    rank = np.where((k < full) & (k % 2 == 1), world - 1 - i, i)
+    u = p // U
+    k, i = u // world, u % world
+    rank = np.where(k % 2 == 1, world - 1 - i, i)
+    j = k * U + (p - u * U)
+    q = p - head
+    k2, i2 = q // world, q % world
+    rank = np.where(p < head, rank, np.where((k2 < tail_full) & (k2 % 2 == 1), world - 1 - i2, i2))
+    j = np.where(p < head, j, R * U + k2)
     order = np.empty(n, dtype=np.int64)
-    order[k * world + rank] = srt
+    order[j * world + rank] = srt
     return order
 
 

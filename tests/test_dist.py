@@ -123,6 +123,39 @@ def test_deal_tiles_balances_and_keeps_counts():
             assert inter.max() / inter.mean() > 1.05  # the interleave is not balanced on this field
 
 
+def test_block_deal_keeps_counts_and_compact_squares():
+    """The block deal of large scenes (tile_plan_kernel with block = 4; rtpotato.dist.deal_tiles(..., block=4)): still a
+    permutation with the interleave's tile count per rank (C5's 128 x 128 tiles; a ragged 1080p grid with a partial last
+    round), a rank's tiles come in whole 4 x 4 squares of the frame (C5's grid divides evenly), and the per-rank cost
+    totals stay balanced.  block = 1 is the per-tile deal."""
+    from rtpotato.dist import deal_tiles, shard_params
+    from rtpotato.scene import RenderParams, shard_slot_count
+    rng = np.random.default_rng(7)
+    for (W, H, tx, ty) in ((4096, 4096, 128, 128), (1920, 1080, 60, 34)):
+        p = RenderParams(W, H, 1, 8, 0)
+        n = tx * ty
+        xs, ys = np.meshgrid(np.arange(tx), np.arange(ty))
+        r2 = ((xs - tx / 2) ** 2 + (ys - ty / 2) ** 2) / (tx * tx / 4)
+        cost = ((100 + 900 * (r2 < 0.5)) * rng.uniform(0.8, 1.2, (ty, tx))).astype(np.int64).reshape(-1)
+        assert np.array_equal(deal_tiles(cost, 8, tx, 1), deal_tiles(cost, 8))
+        for world in (2, 3, 8):
+            # rp_api.cpp plan_block: 4 x 4 or 2 x 2 blocks while every rank gets >= 32 of them
+            block = next((b for b in (4, 2) if n >= 32 * world * b * b), 1)
+            order = deal_tiles(cost, world, tx, block)
+            assert np.array_equal(np.sort(order), np.arange(n))
+            loads = np.zeros(world)
+            for r in range(world):
+                mine = order[r::world]
+                assert len(mine) * 32 * 32 == shard_slot_count(shard_params(p, r, world))
+                loads[r] = cost[mine].sum()
+                if block > 1 and tx % block == 0 and ty % block == 0 and n % (block * block * world) == 0:
+                    blocks = (mine // tx // block) * (tx // block) + (mine % tx) // block
+                    _, counts = np.unique(blocks, return_counts=True)
+                    assert (counts == block * block).all()  # whole squares only
+            assert loads.max() / loads.mean() < 1.03, (W, world, block, loads)
+            assert (W, block) != (4096, 1)  # C5's grid always deals blocks
+
+
 def _worker_balanced(rank, world, port, result_dir):
     """Ranks deal the tiles by the balanced plan (costs: the frame's per-tile ray counts, the same on every rank),
     render their shards (pixels of the oracle frame: per-pixel seeding), all-gather and assemble with the plan."""

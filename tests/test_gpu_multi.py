@@ -75,6 +75,50 @@ def test_balanced_plan_rebuilds_frame(gpu, world):
     assert rays == st["rays"]
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_block_deal_matches_restatement(gpu, world):
+    """Scenes dealt in Z-order (large scenes: tile_order morton) make balanced plans of square tile blocks
+    (rp_api.cpp plan_block: 4 x 4 here, 4,096 tiles) from the installed cost table: the device plan equals the NumPy
+    restatement (rtpotato.dist.deal_tiles with block = 4), and the shards rebuild the interleave frame bit for bit."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.dist import deal_tiles, max_slots, shard_params
+    from rtpotato.scene import RenderParams, shard_slot_count
+    W = H = 512
+    sc = scenes.configure(scenes.bunny_full(), W, H)
+    p = RenderParams(W, H, 1, 8, scenes.DEFAULT_SEED, 8, 8, shard_map=F.RP_SHARD_BALANCED)
+    tx = W // 8
+    n = tx * (H // 8)
+    rng = np.random.default_rng(3)
+    xs, ys = np.meshgrid(np.arange(tx), np.arange(H // 8))
+    cost = ((50 + 500 * (((xs - 32) ** 2 + (ys - 32) ** 2) < 400)) * rng.uniform(0.8, 1.2, xs.shape)).astype(np.uint32)
+    table = np.stack([cost.reshape(-1), cost.reshape(-1) // 4])
+    want = deal_tiles(table[0], world, tx, 4)
+    S = max_slots(p, world)
+    gathered = torch.zeros(world * S * 3, dtype=torch.float64, device="cuda")
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+    with gpu.DeviceScene(sc, options={"tile_order": "morton"}) as ds:
+        ref, _, st = ds.render(replace(p, shard_map=0))
+        wss = [ds.workspace() for _ in range(world)]
+        for r in range(world):
+            sp = shard_params(p, r, world)
+            ds.reserve(sp, wss[r])
+            ds.set_tile_costs(p, table, world, wss[r])
+            ds.render_device(sp, gathered[r * S * 3:(r * S + shard_slot_count(sp)) * 3], ctr, workspace=wss[r])
+            torch.cuda.synchronize()
+            assert int(ctr[3]) == 0
+            assert np.array_equal(ds.tile_map(sp, wss[r]), want), r
+        frame = torch.zeros(W * H * 3, dtype=torch.float64, device="cuda")
+        pc = shard_params(p, 0, world).to_c()
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        F.check(F.rp().rp_frame_assemble_ws(ds.handle, wss[0].handle, ctypes.byref(pc), gathered.data_ptr(), 6,
+                                            frame.data_ptr(), s))
+        torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().reshape(H, W, 3), ref)
+    assert n == 4096
+
+
 def test_balanced_host_render_and_unpack(gpu):
     """rp_render of a balanced shard writes exactly the pixels of its planned tiles, equal to the full frame's; the
     interleave-only rp_shard_unpack refuses a balanced frame, rp_shard_unpack_map takes its plan."""
