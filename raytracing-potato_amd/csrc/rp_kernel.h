@@ -37,7 +37,9 @@ enum { RENDER_BLOCK = 64 };
 // Diagnostic counters (RPK_DIAG builds): wave-cycles per phase {fetch, new sample, traverse, shade,
 // tail}, wave loop iterations, active lanes at traverse, traversal wave-trips, lane node visits,
 // lane primitive tests.
-enum { DIAG_N = 352 };
+// [352 + b] units whose duration (100 MHz ticks) has floor(log2) = b + DIAG_DUR_LOG0 (clamped to 0..23), [376 + b]
+// their rays summed.
+enum { DIAG_N = 400, DIAG_DUR = 352, DIAG_DUR_N = 24, DIAG_DUR_LOG0 = 10 };
 // Cycle regions (RPK_DIAG builds), from DIAG_N index DIAG_CYC: wave-cycles spent executing each code region
 enum { DIAG_CYC = 320 };
 enum {

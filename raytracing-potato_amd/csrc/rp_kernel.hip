@@ -263,6 +263,10 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
               const uint64_t now = __builtin_amdgcn_s_memrealtime();
               atomicMax(&A->diag[13], ((now - t_pix) << 32) | ((uint64_t)batch << 28) | (uint64_t)(pipj & 0x0FFFFFFFu));
               atomicMax(&A->diag[14], ((now - t_pix) << 32) | (uint64_t)(lane_rays - rays_pix));
+              // the distribution of unit durations (log2 bins) and the rays those units traced
+              const int lb = min(max(63 - __builtin_clzll((now - t_pix) | 1ull) - (int)DIAG_DUR_LOG0, 0), (int)DIAG_DUR_N - 1);
+              atomicAdd(&A->diag[DIAG_DUR + lb], 1ull);
+              atomicAdd(&A->diag[DIAG_DUR + DIAG_DUR_N + lb], (unsigned long long)(lane_rays - rays_pix));
             }
             t_pix = __builtin_amdgcn_s_memrealtime();
             rays_pix = lane_rays;

@@ -31,10 +31,11 @@ def main():
         opts[k] = float(v) if k == "cost_traverse" else (v if not v.lstrip("-").isdigit() else int(v))
     ds = DeviceScene(scene, options=opts)
     ds.render(replace(params, spp=1))  # warm
-    buf = (ctypes.c_uint64 * 352)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 352, 1))
+    NDIAG = 400  # rp_kernel.h DIAG_N
+    buf = (ctypes.c_uint64 * NDIAG)()
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
     _, _, st = ds.render(params)
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, 352, 1))
+    F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
     d = list(buf)
     ph = d[:5]
     tot = sum(ph)
@@ -71,6 +72,10 @@ def main():
     out["timeline_10ms"] = [{"t_ms": 10 * b, "retired_lanes": d[64 + b], "pixels": d[192 + b],
                              "rays_per_pixel": round(d[128 + b] / max(1, d[192 + b]), 1),
                              "max_rays_unit": d[256 + b]} for b in range(last + 1)]
+    # unit durations (rp_kernel.h DIAG_DUR): log2 bins of 100 MHz ticks from 2^10 (10.24 us)
+    out["unit_durations"] = [{"ms_from": round(2 ** (10 + b) / 1e5, 3), "ms_to": round(2 ** (11 + b) / 1e5, 3),
+                              "units": d[352 + b], "rays_per_unit": round(d[376 + b] / max(1, d[352 + b]), 1)}
+                             for b in range(24) if d[352 + b]]
     print(json.dumps(out, indent=1))
 
 

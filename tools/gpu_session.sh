@@ -6,7 +6,8 @@
 # STEPS, run in order, each under its own time limit; the first failure (a crash, abort or time limit) ends the session:
 #   tests              pytest -m gpu (PYTEST_ARGS, e.g. "-k c3 -m 'gpu and not slow'")
 #   bench_<CFG>        bench.py --config CFG (BENCH_ARGS appended; the CPU baseline only for C3 unless NO_CPU=1)
-#   shards_<CFG>       tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps
+#   shards_<CFG>[.<L>] tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps,
+#                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run)
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
@@ -53,12 +54,14 @@ for s in ${STEPS:-tests}; do
       made gpurun_out/${TAG}_${cfg}_bench.json "python3 bench.py --config $cfg --steps $st --warmup $wu $cpu ${BENCH_ARGS:-}"
       timeout -k 10 600 python3 bench.py --config $cfg --steps $st --warmup $wu $cpu ${BENCH_ARGS:-} \
         > gpurun_out/${TAG}_${cfg}_bench.json 2> gpurun_out/${TAG}_${cfg}_bench.err || exit 1 ;;
-    shards_*)
-      cfg=${s#shards_}
-      step "shards $cfg"
-      made gpurun_out/${TAG}_${cfg}_shards.json "python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} ${SHARD_ARGS:-}"
-      timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} ${SHARD_ARGS:-} \
-        > gpurun_out/${TAG}_${cfg}_shards.json 2> gpurun_out/${TAG}_${cfg}_shards.err || exit 1 ;;
+    shards_*)  # shards_<CFG>[.<label>]: SHARD_ARGS, or SHARD_ARGS_<label> for a labelled run
+      cfg=${s#shards_}; label=""; [[ $cfg == *.* ]] && label=${cfg#*.} && cfg=${cfg%%.*}
+      sa=SHARD_ARGS${label:+_$label}; sargs=${!sa:-}
+      out=gpurun_out/${TAG}_${cfg}${label:+_$label}_shards
+      step "shards $cfg $label"
+      made $out.json "python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs"
+      timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs \
+        > $out.json 2> $out.err || exit 1 ;;
     diag_*)
       cfg=${s#diag_}
       step "diag $cfg"

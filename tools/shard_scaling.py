@@ -93,15 +93,22 @@ def main():
                     help="1: schedule balanced N > 1 shards from a learned cost table (what every rank holds after "
                          "its first gathered frame: the measured costs of all shards, combined through the deal order "
                          "and installed with rp_workspace_set_tile_costs); 0: the whole-frame probe every frame")
+    ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value (as bench.py --opt)")
     a = ap.parse_args()
+    options = {}
+    for kv in a.opt:
+        k, v = kv.split("=", 1)
+        options[k] = float(v) if k == "cost_traverse" else (
+            v if k in ("builder", "engine", "node_format", "tile_order", "unit_queues", "collapse", "node_layout") else int(v))
     from rtpotato import scenes
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
     if a.tile:
         params = replace(params, tile_w=a.tile, tile_h=a.tile)
-    ds = DeviceScene(scene)
+    ds = DeviceScene(scene, options=options)
     ds.render(replace(params, spp=4))  # warm
-    out = {"config": a.config, "tile": [params.tile_w, params.tile_h], "reps": a.reps, "per_map": {}}
+    out = {"config": a.config, "tile": [params.tile_w, params.tile_h], "reps": a.reps, "inflight": a.inflight,
+           "scene_options": options or "defaults", "per_map": {}}
     import statistics
     for mp in a.maps.split(","):
         smap = {"interleave": 0, "balanced": 1}[mp]
