@@ -211,8 +211,8 @@ enum { RP_NODES_AUTO = 0, RP_NODES_F32 = 1, RP_NODES_Q8 = 2, RP_NODES_W8 = 3 };
 /* Tile orders: PLAIN = shard order (row-major); COST = the costliest tiles go first (short frame tail), by the
  * workspace's learned costs of the previous frame (see rp_workspace_tile_costs) or, without them, by a probe
  * launch that traces sample 0 of a lattice of pixels per tile; PROBE = COST always from the probe; MORTON = Z-order
- * of the tiles (neighbouring tiles run together: a small cache working set).  AUTO = COST while the scene fits
- * the 256 MB Infinity Cache, MORTON above. */
+ * of the tiles (neighbouring tiles run together: a small cache working set; a balanced multi-GPU plan then deals
+ * square blocks of tiles).  AUTO = COST (round 4; rounds 2-3: MORTON for scenes past the 256 MB Infinity Cache). */
 enum { RP_TILES_AUTO = 0, RP_TILES_PLAIN = 1, RP_TILES_COST = 2, RP_TILES_MORTON = 3, RP_TILES_PROBE = 4 };
 /* Unit queues: SINGLE = one device-wide queue over the tile order; XCD_TILES = eight queues, one per group of
  * render blocks sharing an XCD (and its L2), tile k of the order served by queue k mod 8 (a tile's pixels

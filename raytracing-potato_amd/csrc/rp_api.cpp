@@ -593,10 +593,12 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->device_bytes = rp_node_bytes(node_format) * n_tree_nodes + (sizeof(rpl::Prim) + sizeof(rpl::PrimRef)) * n_tree_prims +
                     sizeof(double) * 5 * n_vert + sizeof(rpl::Material) * ps.materials.size() +
                     sizeof(rpl::Texture) * ps.textures.size() + sizeof(uint32_t) * ps.texels.size();
-  // Cache-resident scenes (C3: 11 MB) gain ~15 % from cost-ordered tiles (short frame tail); a scene past the
-  // 256 MB Infinity Cache (C5: 2.5 GB) loses 5-7 % to any reordering that scatters the concurrently rendered
-  // tiles over the frame, and the Z-order keeps them together.
-  s->tiles_auto = s->device_bytes > (256ull << 20) ? RP_TILES_MORTON : RP_TILES_COST;
+  // Cost-ordered tiles for every scene: cache-resident scenes (C3: 11 MB) gain ~15 % from them (short frame tail);
+  // past the 256 MB Infinity Cache (C5: 2.5 GB) the Z-order once won (one device-wide queue: cost order scattered the
+  // tiles in flight, +7 %), but with per-XCD queues and costs learned from the previous frame the cost order is even
+  // or better there too (round 4: C5 -0.8 % on one box, -7.5 % on another, where the Z-order ran 11 % slower than
+  // usual).  MORTON stays an option, and with it the balanced plan's square tile blocks.
+  s->tiles_auto = RP_TILES_COST;
   // the speculative-traversal exit: C3 246.3 ms at 8 (3: 248.2, 12: 248.5); C5 at 16 (per-XCD queues, ab34: 12 +0.4 %,
   // 20 +0.1 %, 24 +0.7 %)
   s->ks.leaf_break = opt.leaf_break ? opt.leaf_break : (s->device_bytes > (256ull << 20) ? 16u : 8u);

@@ -11,6 +11,7 @@
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
+#   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
 #   ab[_<CFG>]         interleaved A/B timing: RUNS (or RUNS_<CFG>) = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
 #                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
@@ -94,6 +95,12 @@ for s in ${STEPS:-tests}; do
         gpurun_out/${TAG}_${cfg}_pmc_sq gpurun_out/${TAG}_${cfg}_pmc_mix64 gpurun_out/${TAG}_${cfg}_pmc_mix32 \
         gpurun_out/${TAG}_${cfg}_pmc_fetch gpurun_out/${TAG}_${cfg}_pmc_write gpurun_out/${TAG}_${cfg}_pmc_l2 \
         > gpurun_out/${TAG}_${cfg}_roofline.log 2>&1 || exit 1 ;;
+    units_*)  # the longest measured unit per tile (product build): tools/unit_times.py
+      cfg=${s#units_}
+      step "units $cfg"
+      made gpurun_out/${TAG}_${cfg}_units.json "python3 tools/unit_times.py --config $cfg ${UNITS_ARGS:-}"
+      timeout -k 10 300 python3 tools/unit_times.py --config $cfg ${UNITS_ARGS:-} \
+        > gpurun_out/${TAG}_${cfg}_units.json 2> gpurun_out/${TAG}_${cfg}_units.err || exit 1 ;;
     lat_*)  # memory-latency picture: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of fills
       cfg=${s#lat_}
       pmc $LIB $cfg lat_tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum \
