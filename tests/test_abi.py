@@ -82,6 +82,12 @@ def test_integration_rust_mirror_matches_c():
     for rust, c in (("RpRenderParams", F.rp_render_params), ("RpSceneOptions", F.rp_scene_options)):
         body = re.search(r"pub struct " + rust + r" \{(.*?)\}", text, re.S).group(1)
         assert re.findall(r"pub (\w+):", body) == [f[0] for f in c._fields_], rust
+        # the worked examples' struct literals name only real fields (a stale name would not compile)
+        for lit in re.findall(r"\b" + rust + r" \{([^}]*)\}", text):
+            if "pub " in lit:
+                continue
+            names = re.findall(r"(\w+)\s*:", lit)
+            assert set(names) <= {f[0] for f in c._fields_}, (rust, names)
 
 
 def test_no_oracle_in_product():
