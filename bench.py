@@ -58,6 +58,8 @@ VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
 # MI355X_MICROARCH.md "Indexed rows": rows shared by every workgroup, gathered from the XCD's L2: 16.8-18.8 TB/s
 L2_GATHER_GBS = 18800.0
+# FP64 vector peak: half the FP32 vector rate (157.3 TFLOP/s, MI355X_MICROARCH.md); the guide lists no FP64 figure
+FP64_VALU_PEAK_TFLOPS = 157.3 / 2
 # (workers, spp) of the CPU baseline runs, ~13 s each: 1 worker; main.rs:27 num_workers = 4; 8; 16 = the GPU box's CPU
 # share (the line through all four is the full-host extrapolation)
 CPU_RUNS = ((1, 2), (4, 8), (8, 16), (16, 32))
@@ -350,6 +352,17 @@ def main():
                     "traffic_over_algorithmic": round(rec["traffic_bytes_per_ray"] / alg, 4),
                     "note": "the kernel's own algorithmic bytes (what its loads touch), served by L2 / Infinity Cache; "
                             "peak = MI355X_MICROARCH.md's L2-shared row gather, 16.8-18.8 TB/s (upper end used)"}
+            c = rec.get("counters", {})
+            if all(k in c for k in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")):
+                # % FP64-VALU roofline beside % HBM -- wave-instructions x 64 lanes, i.e. an upper bound
+                # (inactive lanes counted), per ray of the record x this launch's rays
+                f64_per_ray = 64.0 * (2.0 * c["SQ_INSTS_VALU_FMA_F64"] + c["SQ_INSTS_VALU_MUL_F64"] +
+                                      c["SQ_INSTS_VALU_ADD_F64"] + c.get("SQ_INSTS_VALU_TRANS_F64", 0.0)) / rec["rays"]
+                tf = f64_per_ray * local_rays / kernel_s / 1e12
+                roof["fp64_valu"] = {"achieved": round(tf, 2), "peak": FP64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                     "frac": round(tf / FP64_VALU_PEAK_TFLOPS, 4),
+                                     "note": "upper bound: f64 FMA (2 flops), MUL, ADD, transcendental wave-instructions "
+                                             "x 64 lanes; peak = half the FP32 vector rate (spec)"}
             binding = ("valu_issue", valu_frac) if valu_frac >= tr_frac else ("hbm_traffic", tr_frac)
             roof["binding"] = {"resource": binding[0], "frac": round(binding[1], 4),
                                "note": "the kernel is latency-bound (cycle_budget: waves wait on memory ~45 % of their "
@@ -372,6 +385,7 @@ def main():
                        "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
+                       "msamples_per_s": round(samples_step * args.steps / elapsed_max / 1e6, 1),
                        "scene_options": options or "defaults", "shard_map": smap,
                        **({"simulated_shard": f"shard {args.shard} of {args.shard_of}, no gather (diagnostic)"}
                           if args.shard_of else {})},

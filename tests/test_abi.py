@@ -182,3 +182,22 @@ def test_bench_cpu_fit_is_a_least_squares_line():
     assert abs(lin["intercept"] - 0.5) < 1e-9 and abs(lin["per_worker"] - 0.9) < 1e-9 and lin["r2"] == 1.0
     bent = b.fit_workers([{"workers": w, "value": v} for w, v in ((1, 1.0), (4, 4.0), (8, 7.0), (16, 11.0))])
     assert bent["per_worker"] < 0.75 and bent["r2"] < 1.0 and bent["points"] == 4
+
+
+def test_profile_records_price_fractions_below_one():
+    """the bench line's fractions are of a roof -- priced at the record's own frame time, the memory-side
+    traffic is <= 8 TB/s (roofline.frac), the algorithmic bytes <= the L2 gather rate (roofline.l2_level) and the VALU
+    issue <= 1 (binding_frac)."""
+    import importlib.util
+    import json
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    cur = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"]
+    for cfg, rel in cur.items():
+        rec = json.load(open(os.path.join(REPO, rel)))
+        secs = rec["bench_ms_per_step"] / 1e3
+        rate = rec["rays"] / secs
+        assert 0 < rec["traffic_bytes_per_ray"] * rate / 1e9 / b.HBM_PEAK_GBS <= 1.0, cfg
+        assert 0 < rec["algorithmic_bytes_per_ray"] * rate / 1e9 / b.L2_GATHER_GBS <= 1.0, cfg
+        assert 0 < rec["valu_per_ray"] * rate / b.VALU_ISSUE_PEAK <= 1.0, cfg
