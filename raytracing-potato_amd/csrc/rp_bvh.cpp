@@ -410,18 +410,10 @@ struct CollapsePlan {
     const size_t n = bin.size();
     std::vector<double> F(4 * n);
     choice.assign(4 * n, 0);
-    // post-order without recursion: children before parents
-    std::vector<int32_t> stack, post;
-    post.reserve(n);
-    stack.push_back(0);
-    while (!stack.empty()) {
-      const int32_t v = stack.back();
-      stack.pop_back();
-      post.push_back(v);
-      if (!bin[v].leaf()) { stack.push_back(bin[v].left); stack.push_back(bin[v].right); }
-    }
-    for (size_t q = post.size(); q-- > 0;) {
-      const int32_t v = post[q];
+    // both binary builders number a node before its children (Builder::build, ParallelBuild::splice: pre-order),
+    // so descending ids visit children before parents -- no post-order list (8 B per node) is needed
+    for (size_t q = n; q-- > 0;) {
+      const int32_t v = (int32_t)q;
       const BinNode& b = bin[v];
       double* f = &F[4 * (size_t)v];
       uint8_t* c = &choice[4 * (size_t)v];

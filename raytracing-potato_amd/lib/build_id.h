@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "96aa69cf214ccf75"
+#define RP_BUILD_ID "f3d668241d2aac0a"
