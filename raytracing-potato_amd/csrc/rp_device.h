@@ -155,6 +155,9 @@ static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING;
 static constexpr uint32_t SLAB_N = SLAB_JIT + 8;
 // A refill pass runs when some lane is at or below RNG_CRIT blocks ahead, or RNG_BATCH lanes have room.
 static constexpr uint32_t RNG_CRIT = 2, RNG_BATCH = 48;
+// The lanes a refill pass leaves without a block of their own make blocks for the others (rng_refill): first for the
+// lanes at or below RNG_CRIT, then (COOP_FILL) one each for any lane whose ring has room.
+static constexpr bool COOP_FILL = false;
 // Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
 // the wave still look for a leaf (rp_scene_options.leaf_break; C3: 0 -> 3 was -2.7 % frame time, 8 is -0.8 %
 // more; C5 wants 12-16), and the leaf loop once at most PRIM_BREAK lanes still test primitives (their
@@ -206,6 +209,16 @@ RPK_INLINE uint4* jit_slot(const RngT<RN>& r, uint32_t b) { return r.slab + RngT
 // samples s+1.. need jitter blocks (s+1)/4 and the one after.  A lane with a `fresh` unit (fetched last
 // round, not started) gets its key from the unit's seed and keystream block 0 here, batched with the other
 // lanes' ChaCha work -- at the fetch site the whole wave paid a ChaCha block for each fetching lane.
+// Position of the n-th (0-based) set bit of m (n < popcount(m)).
+RPK_INLINE uint32_t nth_set(uint64_t m, uint32_t n) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+    if (n >= c) { n -= c; m >>= w; pos += (uint32_t)w; }
+  }
+  return pos;
+}
 template <uint32_t RN>
 RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
   const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
@@ -215,33 +228,68 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
   const bool crit = alive && (fresh || have <= RNG_CRIT);
   const bool room = alive && (fresh || have < RN || j1 || j2);
   if (__ballot(crit) == 0 && (uint32_t)__popcll(__ballot(room)) < RNG_BATCH) return;
-  if (room) {
+  // This lane's own block (room): a fresh unit's block 0, else the next ring block or a missing jitter block.
+  const bool main = fresh || crit || !(j1 || j2);  // crit: have <= RNG_CRIT < RN, so the ring has room
+  const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
+  const uint32_t end1 = !room ? end : (fresh ? 1u : (main ? end + 1u : end));  // ring end after it
+  const uint32_t have1 = end1 - (fresh ? 0u : cur);
+  // The lanes without a block of their own this pass (full rings, retired lanes) make ring blocks for the lanes still
+  // at or below the critical level after it -- up to two each, the next blocks of their streams -- in the same ChaCha
+  // pass: a fresh unit leaves the pass 3 blocks ahead instead of 1, so it does not force the next two passes, and the
+  // in-place fallback (gen_block: one lane, a whole wave's ChaCha time) is rarer.  Requests are numbered lane by lane,
+  // first blocks before second ones; executor x (the x-th lane without a block) takes request x.
+  // (COOP_FILL: then one more block for every other lane whose ring has room, while executors are left)
+  const uint32_t want = alive && have1 <= RNG_CRIT ? min(RNG_CRIT + 1u - have1, RN - have1) : 0u;
+  const bool fill = COOP_FILL && alive && want == 0u && have1 < RN;
+  const uint64_t m1 = __ballot(want >= 1u), m2 = __ballot(want >= 2u), m3 = COOP_FILL ? __ballot(fill) : 0ull;
+  const uint64_t ex = __ballot(!room);
+  const uint32_t lane = __lane_id();
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t n1 = (uint32_t)__popcll(m1), n12 = n1 + (uint32_t)__popcll(m2), nex = (uint32_t)__popcll(ex);
+  const uint32_t nreq = n12 + (uint32_t)__popcll(m3);
+  const uint32_t xr = (uint32_t)__popcll(ex & below);
+  const bool sec = !room && xr < nreq;
+  uint32_t owner = lane, j = 0u;
+  if (sec) {
+    if (xr < n1) owner = nth_set(m1, xr);
+    else if (xr < n12) { owner = nth_set(m2, xr - n1); j = 1u; }
+    else owner = nth_set(m3, xr - n12);
+  }
+  const uint32_t slo = __shfl((uint32_t)seed, (int)owner), shi = __shfl((uint32_t)(seed >> 32), (int)owner);
+  const uint32_t oend = __shfl(end1, (int)owner);
+  // this lane's requests that an executor took
+  const uint32_t served = (uint32_t)(want >= 1u && (uint32_t)__popcll(m1 & below) < nex) +
+                          (uint32_t)(want >= 2u && n1 + (uint32_t)__popcll(m2 & below) < nex) +
+                          (uint32_t)(fill && n12 + (uint32_t)__popcll(m3 & below) < nex);
+  if (room || sec) {
     DREG(DREG_REFILL)
-    const bool main = fresh || crit || !(j1 || j2);  // crit: have <= RNG_CRIT < RN, so the ring has room
-    const uint32_t b = fresh ? 0u : (main ? end : (j1 ? b1 : b2));
     uint32_t k[8], w[16];
     // The key is recomputed from the unit's seed (PCG32 seed_from_u64, ~100 VALU) rather than loaded from the
     // slab: a slab load that misses L2 stalls the whole pass before its ChaCha work (C3 -0.7 %, C5 -0.1 %,
     // ab48).  A fresh unit still stores it for the in-place fallback (gen_block).
-    seed_key(seed, k);
+    seed_key(room ? seed : ((uint64_t)shi << 32 | slo), k);
     if (fresh) {
       DREG(DREG_BEGIN_PIXEL)
       store_key(r, k);
     }
-    chacha12(k, b, w);
-    store_block(main ? ring_slot(r, b) : jit_slot(r, b), w);
-    if (fresh) {  // block 0 is also the jitter block of samples 0-3 (render.rs:74-82)
-      store_block(jit_slot(r, 0), w);
+    const uint32_t bb = room ? b : oend + j;
+    chacha12(k, bb, w);
+    // an executor's block goes into its owner's ring (lane slabs are consecutive within the block)
+    uint4* dst = room ? (main ? ring_slot(r, b) : jit_slot(r, b))
+                      : r.slab + ((int)owner - (int)lane) * (int)RngT<RN>::lane_n + SLAB_RING + 4u * (bb & (RN - 1u));
+    store_block(dst, w);
+    if (fresh) store_block(jit_slot(r, 0), w);  // block 0 is also the jitter block of samples 0-3 (render.rs:74-82)
+  }
+  if (room) {
+    if (fresh) {
       r.pos = 0;
-      *r.end = 1;
       r.jtag[0] = 0;
       r.jtag[BLOCK] = 0xFFFFFFFFu;
-    } else if (main) {
-      *r.end = end + 1;
-    } else {
+    } else if (!main) {
       r.jtag[(b & 1u) * BLOCK] = b;
     }
   }
+  if (room || served) *r.end = end1 + served;
 }
 
 // Jitter words 4s..4s+3 of the pixel-start stream (block s/4).

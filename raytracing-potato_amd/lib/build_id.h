@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "f3d668241d2aac0a"
+#define RP_BUILD_ID "67fcd69d1b2a6ff4"

@@ -13,6 +13,7 @@
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
+#   pmcx_<CFG>         one --pmc pass of the counters in PMCX (output name PMCX_NAME)
 #   ab[_<CFG>]         interleaved A/B timing: RUNS (or RUNS_<CFG>) = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
 #                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
 #   abpmc[_<CFG>]      per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
@@ -106,6 +107,9 @@ for s in ${STEPS:-tests}; do
       pmc $LIB $cfg lat_tcp TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum \
         TCP_TCC_READ_REQ_sum &&
       pmc $LIB $cfg lat_tcc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_REQ_sum || exit 1 ;;
+    pmcx_*)  # one extra --pmc pass: PMCX="<counters>" (within one pass's per-block limits), named PMCX_NAME
+      cfg=${s#pmcx_}
+      pmc $LIB $cfg ${PMCX_NAME:-x} $PMCX || exit 1 ;;
     ab|ab_*)
       [ "$s" != ab ] && CFG=${s#ab_}
       read st wu <<< "$(frames $CFG)"
