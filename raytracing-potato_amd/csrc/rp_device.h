@@ -219,6 +219,7 @@ RPK_INLINE uint32_t nth_set(uint64_t m, uint32_t n) {
   }
   return pos;
 }
+static_assert(BLOCK == 64, "rng_refill: a block is one wave, so a lane's slab is the wave's lane index past the first");
 template <uint32_t RN>
 RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, uint32_t s, uint32_t spp) {
   const uint32_t cur = r.pos >> 4, end = *r.end, have = end - cur;
