@@ -688,6 +688,13 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // queue) or one per fetch that passes a drained queue on the way to another (per-XCD queues)
   if ((kp.queue_groups > 1 ? 2 * kp.n_queue : kp.n_queue) + s->lanes() >= 0xffffffffull)
     return fail(RP_EINVAL, "shard too large (>= 2^32 pixel-batch units with the resident lanes)");
+  // the unit decode divides by launch constants with 31-bit numerators (rpk::make_div32)
+  if (kp.n_queue >= (1ull << 31)) return fail(RP_EINVAL, "shard too large (>= 2^31 pixel-batch units)");
+  kp.dv_units = rpk::make_div32(t.tw * t.th * kp.nbatch);
+  kp.dv_nbatch = rpk::make_div32(kp.nbatch ? kp.nbatch : 1u);
+  kp.dv_tiles_x = rpk::make_div32(t.tiles_x);
+  kp.dv_tw = rpk::make_div32(t.tw);
+  kp.dv_chunk = rpk::make_div32(kp.queue_chunk);
   if (kp.nbatch > 1) {
     if (kp.n_queue > w->partial_units)
       return fail(RP_EINVAL, "workspace not reserved for this frame's sample batches: call rp_workspace_reserve");

@@ -1431,6 +1431,9 @@ RPK_INLINE KArgsPtr kargs() {
 // Pull the next unit (pixel, sample batch) of the shard from the unit queues.  Queue order: shard tiles
 // (in cost or Z-order when tile_order is set), inside a tile the pixels row-major, each pixel's batches
 // consecutive; slots of edge tiles outside the frame are skipped.  Returns false when every queue is drained.
+RPK_INLINE uint32_t udiv(uint32_t n, uint32_t m, uint32_t s) { return (uint32_t)(((uint64_t)n * m) >> s); }  // rp_kernel.h make_div32
+#define RPK_UDIV(n, dv) udiv((n), A->P.dv.m, A->P.dv.s)
+
 template <bool PROBE>
 RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t& batch) {
   KArgsPtr A = kargs();
@@ -1474,20 +1477,23 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
         continue;
       }
     }
-    const uint32_t i = q / tile_units;
+    // (PROBE launches decode with plain divisions: one small launch)
+    const uint32_t i = PROBE ? q / tile_units : RPK_UDIV(q, dv_units);
     const uint32_t rem = q - i * tile_units;
-    uint32_t k = (i / C) * GC + g * C + i % C;
+    const uint32_t ic = PROBE ? i / C : RPK_UDIV(i, dv_chunk);
+    uint32_t k = ic * GC + g * C + (i - ic * C);
     // a tile's units pixel-major, a pixel's batches consecutive: a wave fetches 64 / nbatch pixels with all
     // their batches, whose camera rays traverse nearly the same nodes (C3 -0.9 %, C5 -0.9 % against
     // batch-major, ab32)
-    const uint32_t local = rem / A->P.nbatch;
+    const uint32_t local = PROBE ? rem / A->P.nbatch : RPK_UDIV(rem, dv_nbatch);
     batch = rem - local * A->P.nbatch;
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
     slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
     const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
-    const uint32_t tx = t % A->P.tiles_x, ty = t / A->P.tiles_x;
-    pi = tx * tw + local % tw;
-    pj = ty * th + local / tw;
+    const uint32_t ty = PROBE ? t / A->P.tiles_x : RPK_UDIV(t, dv_tiles_x), tx = t - ty * A->P.tiles_x;
+    const uint32_t lj = PROBE ? local / tw : RPK_UDIV(local, dv_tw), li = local - lj * tw;
+    pi = tx * tw + li;
+    pj = ty * th + lj;
     if (pi < A->P.W && pj < A->P.H) return true;
   }
 }

@@ -62,6 +62,20 @@ enum {
   DREG_N
 };
 
+// Division by a launch constant d >= 1 of numerators n < 2^31 (Granlund & Montgomery 1994, Thm 4.2 with N = 31):
+// l = ceil(log2 d), s = 31 + l, m = ceil(2^s / d) < 2^32 (m d - 2^s < d <= 2^l), and floor(n / d) = (n m) >> s.
+// The unit decode of every fetch (rp_device.h fetch_pixel) divides by five per-launch values; the compiler's
+// division by a run-time divisor is ~25 VALU each.
+struct Div32 {
+  uint32_t m, s;
+};
+inline Div32 make_div32(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < (uint64_t)d) l++;
+  const uint32_t s = 31 + l;
+  return Div32{(uint32_t)(((1ull << s) + d - 1) / d), s};
+}
+
 struct KParams {
   double orient[9];
   double pos[3];
@@ -80,6 +94,8 @@ struct KParams {
   uint64_t n_queue;         // queue entries: n_slots * nbatch units (render), probed pixels (probe)
   uint32_t queue_groups;    // render: unit queues (1, or QUEUE_GROUPS: one per group blockIdx mod 8 = one XCD)
   uint32_t queue_chunk;     // render: queue g serves the chunks g, g + G, ... of queue_chunk consecutive tiles (>= 1)
+  // render: make_div32 of tw * th * nbatch (a tile's units), nbatch, tiles_x, tw, queue_chunk (n_queue < 2^31)
+  Div32 dv_units, dv_nbatch, dv_tiles_x, dv_tw, dv_chunk;
   double* partial;          // nbatch > 1: per unit (slot * nbatch + batch) the batch's sample sum, 3 f64
   uint32_t* partial_hits;   // nbatch > 1: per unit, samples whose first ray hit (foreground)
   const uint32_t* tile_order;  // render: queue position k -> shard tile index (NULL = identity)
