@@ -186,6 +186,9 @@ def main():
     ap.add_argument("--samples-per-stream", type=int, default=0,
                     help="rp_render_params.samples_per_stream, the RNG contract (0 = RP_SAMPLES_PER_STREAM = 32; "
                          ">= spp: one stream per pixel, SURVEY.md 8c)")
+    ap.add_argument("--tile", type=int, default=0,
+                    help="tile side in pixels (rp_render_params.tile_w/tile_h; 0 = the config's 32): scheduling only, "
+                         "the image does not depend on it")
     ap.add_argument("--cpu-spp", type=int, default=0, help="override the CPU baseline runs' spp (0 = per run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=0,
@@ -226,6 +229,8 @@ def main():
         params = replace(params, spp=args.spp)
     if args.samples_per_stream:
         params = replace(params, samples_per_stream=args.samples_per_stream)
+    if args.tile:
+        params = replace(params, tile_w=args.tile, tile_h=args.tile)
     t = time.time()
     ds = DeviceScene(scene, device=local, options=options)
     info = ds.info()
@@ -316,7 +321,7 @@ def main():
     if rank == 0:
         local_rays = rays_step / world  # this rank's launch (shards carry near-equal work under the balanced plan)
         # the per-ray record is of the default workload (its spp and RNG batches)
-        rec = kernel_record(args.config) if args.spp == 0 and args.samples_per_stream == 0 else None
+        rec = kernel_record(args.config) if args.spp == 0 and args.samples_per_stream == 0 and args.tile == 0 else None
         build = F.rp().rp_build_id().decode()
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
                 "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3), "build_id": build}
@@ -380,7 +385,7 @@ def main():
             "config": {"workload": f"{args.config}: {scenes.CONFIGS[args.config].description}",
                        "width": params.width, "height": params.height, "spp": params.spp,
                        "max_bounce": params.max_bounce, "seed": params.seed,
-                       "samples_per_stream": params.samples_per_stream or 32,
+                       "samples_per_stream": params.samples_per_stream or 32, "tile": [params.tile_w, params.tile_h],
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
                        "frames_in_flight": F_,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",

@@ -538,7 +538,10 @@ __device__ __forceinline__ void bitonic_global(T* __restrict__ key, uint32_t np2
 }
 
 static_assert(TILE_SORT_MAX <= (1 << 14), "tile index field is 14 bits");
-static constexpr float SORT_Q = 4.0f;  // buckets per octave of cost
+// Buckets per octave of cost.  Inside a bucket the tiles keep their Z-order, so coarser buckets trade cost order for
+// locality: octave buckets C5 -1.7 % against quarter-octave ones (C3 -0.1 %); two octaves per bucket C5 -2.0 % but C3
+// +0.5 % (profiles/r4/c3_c5_sort_buckets*_ab.json, learned costs and per-XCD queues; the probe-era C3 sweep preferred 4)
+static constexpr float SORT_Q = 1.0f;
 __device__ __forceinline__ uint32_t spread8(uint32_t v) {  // 8 bits -> every other bit of 16
   v = (v | (v << 4)) & 0x0F0Fu;
   v = (v | (v << 2)) & 0x3333u;
@@ -564,8 +567,7 @@ __global__ void __launch_bounds__(SORT_BLOCK) tile_sort_kernel(const uint32_t* _
       const uint32_t dk = g.shard + i * g.nshards, t = g.map ? g.map[dk] : dk, tx = t % g.tiles_x, ty = t / g.tiles_x;
       uint32_t ql = 0, qm = 0;
       if (cost) {
-        // quarter-octave buckets of the costliest probed sample's cost and of the mean cost (C3: 2^(1/4)
-        // steps 248.1 ms, 2^(1/32) steps 250.1 ms, the round-1 ray-count cost 254.7 ms per frame)
+        // SORT_Q buckets per octave of the costliest probed (or measured) sample's cost and of the mean cost
         const uint32_t c = g.cost_by_tile ? t : i;
         const float mean = (float)cost[c] / (float)probe_px;
         ql = min((uint32_t)(log2f((float)cost[TILE_SORT_MAX + c] + 1.0f) * SORT_Q), 63u);

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "72d692625c7b753a"
+#define RP_BUILD_ID "ff7fd58c2e5269af"

@@ -15,7 +15,7 @@
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
 #   pmcx_<CFG>         one --pmc pass of the counters in PMCX (output name PMCX_NAME)
 #   ab[_<CFG>]         interleaved A/B timing: RUNS (or RUNS_<CFG>) = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
-#                      opts = bench.py --opt field=value,...), REPS rounds, config CFG, STEPS_AB frames each
+#                      opts = bench.py --opt field=value,... or --flag=value), REPS rounds, config CFG, STEPS_AB frames each
 #   abpmc[_<CFG>]      per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
 # Outputs: gpurun_out/${TAG}_*; gpurun_out/${TAG}_manifest.txt lists every output file with the command that made it.
 set -o pipefail
@@ -118,7 +118,9 @@ for s in ${STEPS:-tests}; do
         for run in $runs; do
           name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}; opts=${rest#*:}
           args=""
-          for o in $(echo $opts | tr ',' ' '); do args="$args --opt $o"; done
+          for o in $(echo $opts | tr ',' ' '); do  # field=value: --opt; --flag=value: a bench.py flag
+            if [[ $o == --* ]]; then args="$args ${o%%=*} ${o#*=}"; else args="$args --opt $o"; fi
+          done
           out=gpurun_out/${TAG}_${CFG}_${name}_$rep.json
           step "ab $rep $name"
           made $out "RP_LIB=$(libpath $lib) python3 bench.py --config $CFG --steps ${STEPS_AB:-$st} --warmup $wu --no-cpu-baseline $args ${BENCH_ARGS:-}"
