@@ -7,7 +7,7 @@
 #   tests              pytest -m gpu (PYTEST_ARGS, e.g. "-k c3 -m 'gpu and not slow'")
 #   bench_<CFG>        bench.py --config CFG (BENCH_ARGS appended; the CPU baseline only for C3 unless NO_CPU=1)
 #   shards_<CFG>[.<L>] tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps,
-#                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run)
+#                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run), library SHARD_LIB_<L> (default main)
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
@@ -58,11 +58,12 @@ for s in ${STEPS:-tests}; do
         > gpurun_out/${TAG}_${cfg}_bench.json 2> gpurun_out/${TAG}_${cfg}_bench.err || exit 1 ;;
     shards_*)  # shards_<CFG>[.<label>]: SHARD_ARGS, or SHARD_ARGS_<label> for a labelled run
       cfg=${s#shards_}; label=""; [[ $cfg == *.* ]] && label=${cfg#*.} && cfg=${cfg%%.*}
-      sa=SHARD_ARGS${label:+_$label}; sargs=${!sa:-}
+      sa=SHARD_ARGS${label:+_$label}; sargs=${!sa:-${SHARD_ARGS:-}}
+      sl=SHARD_LIB${label:+_$label}; slib=$(libpath ${!sl:-main})  # SHARD_LIB_<label>: a lib/librp_<name>.so variant
       out=gpurun_out/${TAG}_${cfg}${label:+_$label}_shards
       step "shards $cfg $label"
-      made $out.json "python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs"
-      timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs \
+      made $out.json "RP_LIB=$slib python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs"
+      RP_LIB=$slib timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs \
         > $out.json 2> $out.err || exit 1 ;;
     diag_*)
       cfg=${s#diag_}
