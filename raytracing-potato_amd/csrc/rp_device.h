@@ -155,9 +155,6 @@ static constexpr uint32_t SLAB_KEY = 0, SLAB_RING = 2, SLAB_JIT = 2 + 4 * RING;
 static constexpr uint32_t SLAB_N = SLAB_JIT + 8;
 // A refill pass runs when some lane is at or below RNG_CRIT blocks ahead, or RNG_BATCH lanes have room.
 static constexpr uint32_t RNG_CRIT = 2, RNG_BATCH = 48;
-// The lanes a refill pass leaves without a block of their own make blocks for the others (rng_refill): first for the
-// lanes at or below RNG_CRIT, then (COOP_FILL) one each for any lane whose ring has room.
-static constexpr bool COOP_FILL = false;
 // Traversal wave-level exits (trav_step): leave the inner-node loop once at most KScene::leaf_break lanes of
 // the wave still look for a leaf (rp_scene_options.leaf_break; C3: 0 -> 3 was -2.7 % frame time, 8 is -0.8 %
 // more; C5 wants 12-16), and the leaf loop once at most PRIM_BREAK lanes still test primitives (their
@@ -239,29 +236,24 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
   // pass: a fresh unit leaves the pass 3 blocks ahead instead of 1, so it does not force the next two passes, and the
   // in-place fallback (gen_block: one lane, a whole wave's ChaCha time) is rarer.  Requests are numbered lane by lane,
   // first blocks before second ones; executor x (the x-th lane without a block) takes request x.
-  // (COOP_FILL: then one more block for every other lane whose ring has room, while executors are left)
+  // (Topping up every other ring with room as well cost C3 +1.0 %, C5 +2.6 %: profiles/r4/c3_c5_refill_variants_ab.json.)
   const uint32_t want = alive && have1 <= RNG_CRIT ? min(RNG_CRIT + 1u - have1, RN - have1) : 0u;
-  const bool fill = COOP_FILL && alive && want == 0u && have1 < RN;
-  const uint64_t m1 = __ballot(want >= 1u), m2 = __ballot(want >= 2u), m3 = COOP_FILL ? __ballot(fill) : 0ull;
-  const uint64_t ex = __ballot(!room);
+  const uint64_t m1 = __ballot(want >= 1u), m2 = __ballot(want >= 2u), ex = __ballot(!room);
   const uint32_t lane = __lane_id();
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t n1 = (uint32_t)__popcll(m1), n12 = n1 + (uint32_t)__popcll(m2), nex = (uint32_t)__popcll(ex);
-  const uint32_t nreq = n12 + (uint32_t)__popcll(m3);
+  const uint32_t n1 = (uint32_t)__popcll(m1), nreq = n1 + (uint32_t)__popcll(m2), nex = (uint32_t)__popcll(ex);
   const uint32_t xr = (uint32_t)__popcll(ex & below);
   const bool sec = !room && xr < nreq;
   uint32_t owner = lane, j = 0u;
   if (sec) {
     if (xr < n1) owner = nth_set(m1, xr);
-    else if (xr < n12) { owner = nth_set(m2, xr - n1); j = 1u; }
-    else owner = nth_set(m3, xr - n12);
+    else { owner = nth_set(m2, xr - n1); j = 1u; }
   }
   const uint32_t slo = __shfl((uint32_t)seed, (int)owner), shi = __shfl((uint32_t)(seed >> 32), (int)owner);
   const uint32_t oend = __shfl(end1, (int)owner);
   // this lane's requests that an executor took
   const uint32_t served = (uint32_t)(want >= 1u && (uint32_t)__popcll(m1 & below) < nex) +
-                          (uint32_t)(want >= 2u && n1 + (uint32_t)__popcll(m2 & below) < nex) +
-                          (uint32_t)(fill && n12 + (uint32_t)__popcll(m3 & below) < nex);
+                          (uint32_t)(want >= 2u && n1 + (uint32_t)__popcll(m2 & below) < nex);
   if (room || sec) {
     DREG(DREG_REFILL)
     uint32_t k[8], w[16];
