@@ -171,6 +171,26 @@ def test_c4_balanced_shard_against_oracle(gpu):
     assert (sst["rays"], sst["samples"]) == (ctr["rays"], ctr["samples"]), (sst, ctr)
 
 
+def test_shards_of_2_31_units_are_refused(gpu):
+    """The unit decode divides by launch constants with 31-bit multiply-shift magic numbers (rp_kernel.h make_div32,
+    rp_device.h fetch_pixel), so rp_api.cpp refuses a shard of 2^31 or more (pixel, sample batch) units with RP_EINVAL
+    before anything is launched: here 8192 x 8192 pixels x 32 batches of 32 samples on one unit queue (per-XCD queues
+    hit the 2^32 queue-word limit first)."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams, shard_slot_count
+    sc = scenes.configure(scenes.bunny_full(), 8192, 8192)
+    p = RenderParams(8192, 8192, 1024, 8, 3)
+    out = torch.zeros(3 * shard_slot_count(p), dtype=torch.float64, device="cuda")
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+    with gpu.DeviceScene(sc, options={"unit_queues": "single"}) as ds:
+        with pytest.raises(F.RPError) as e:
+            ds.render_device(p, out, ctr)
+        assert e.value.code == F.RP_EINVAL and "2^31" in str(e.value)
+    del out
+
+
 def test_async_render_needs_reservation(gpu):
     """rp_render_device never allocates: a multi-batch frame without rp_workspace_reserve is refused with
     RP_EINVAL (nothing launched); after the reservation it renders the rp_render image bit for bit."""
