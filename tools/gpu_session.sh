@@ -8,6 +8,7 @@
 #   bench_<CFG>        bench.py --config CFG (BENCH_ARGS appended; the CPU baseline only for C3 unless NO_CPU=1)
 #   shards_<CFG>[.<L>] tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps,
 #                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run), library SHARD_LIB_<L> (default main)
+#   shardtrace_<CFG>   rocprofv3 --kernel-trace around one tools/shard_scaling.py run (SHARD_NS, SHARD_ARGS)
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
@@ -65,6 +66,13 @@ for s in ${STEPS:-tests}; do
       made $out.json "RP_LIB=$slib python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs"
       RP_LIB=$slib timeout -k 10 900 python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-1,8} --reps ${SHARD_REPS:-3} $sargs \
         > $out.json 2> $out.err || exit 1 ;;
+    shardtrace_*)  # rocprofv3 kernel trace of one shards run (SHARD_ARGS, SHARD_NS): overlap of in-flight frames
+      cfg=${s#shardtrace_}
+      out=gpurun_out/${TAG}_${cfg}_shardtrace
+      step "shardtrace $cfg"
+      made $out "rocprofv3 --kernel-trace -- python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-8} --reps 1 ${SHARD_ARGS:-}"
+      timeout -k 10 600 rocprofv3 --kernel-trace -d $out -o run --output-format csv -- \
+        python3 tools/shard_scaling.py --config $cfg --ns ${SHARD_NS:-8} --reps 1 ${SHARD_ARGS:-} > $out.json 2> $out.err || exit 1 ;;
     diag_*)
       cfg=${s#diag_}
       step "diag $cfg"
