@@ -193,6 +193,9 @@ typedef struct rp_render_params {
                                   stream per pixel */
   uint32_t shard_map;       /* RP_SHARD_INTERLEAVE (0) or RP_SHARD_BALANCED */
 } rp_render_params;
+/* A shard holds at most 2^31 - 1 (pixel, sample stream) units -- its pixels x ceil(spp / samples_per_stream) -- and
+ * with the default per-XCD unit queues half the 32-bit queue word less the resident lanes; larger shards are refused
+ * with RP_EINVAL (e.g. 8192 x 8192 pixels at 1024 spp: split the frame into shards). */
 
 /* Scene build and kernel tuning options (rp_scene_create_ex).  None of them changes an image beyond
  * exact-t ties between primitives (the closest hit does not depend on the tree).
