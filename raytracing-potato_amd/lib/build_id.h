@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "ff7fd58c2e5269af"
+#define RP_BUILD_ID "e9be37cfc887f1e8"

@@ -3,6 +3,7 @@
 import ctypes
 import os
 import re
+import subprocess
 
 from conftest import PKG, REPO
 
@@ -169,6 +170,30 @@ def test_profile_records_are_of_this_build():
         rec = json.load(open(os.path.join(REPO, rel)))
         assert rec["build_id"] == build, (cfg, rel, rec["build_id"], build)
         assert rec["config"] == cfg and rec["rays"] > 0 and rec["traffic_bytes_per_ray"] > 0
+
+
+def test_build_id_is_path_independent(tmp_path):
+    """rp_build_id must not depend on the directory the library is built in (a clean checkout elsewhere
+    must keep the committed records valid).  The same HIP source compiled at two paths gives objects whose whole
+    .hip_fatbin differs (a path-derived __hip_cuid symbol) but whose build_id.sh hash -- the one the Makefile stamps --
+    is the same."""
+    import hashlib
+    src = ("#include <hip/hip_runtime.h>\n__global__ void k(float* x) { x[threadIdx.x] *= 2.0f; }\n"
+           "void run(float* x, hipStream_t s) { hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, s, x); }\n")
+    ids, fats = [], []
+    for sub in ("a", "bb/longer_path"):
+        d = tmp_path / sub
+        d.mkdir(parents=True)
+        (d / "t.hip").write_text(src)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-fPIC", "-c", str(d / "t.hip"), "-o", "t.o"],
+                       cwd=d, check=True, capture_output=True)
+        subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", "t.o", "fat.bin"], cwd=d, check=True)
+        fats.append(hashlib.sha256((d / "fat.bin").read_bytes()).hexdigest())
+        r = subprocess.run(["bash", os.path.join(PKG, "build_id.sh"), "gfx950", str(d / "t.o"), "--", str(d / "t.o")],
+                           capture_output=True, text=True, check=True)
+        ids.append(r.stdout.strip())
+    assert len(ids[0]) == 16 and ids[0] == ids[1], ids
+    assert fats[0] != fats[1]  # what the round-4 id hashed
 
 
 def test_bench_cpu_fit_is_a_least_squares_line():
