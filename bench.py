@@ -54,6 +54,22 @@ SIMDS = 1024                 # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9             # MI355X_MICROARCH.md max clock
 # a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md "Wave scheduling")
 VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
+# Weighted VALU pipe occupancy: SIMD cycles per wave64 instruction by class.  f32 / integer / conversion:
+# 2 (the row above); f64 add, mul and FMA issue at half the f32 rate (spec): 4; f32 transcendentals take 8 cycles of
+# one wave's issue against 4 for v_fma_f32 (MI355X_MICROARCH.md "vector-instruction ISSUE cost"): 4; f64
+# transcendentals (v_rcp/v_sqrt/v_rsq_f64) are priced at twice that, 8 -- an assumption, the guide lists no f64 row.
+VALU_CYCLES = {"SQ_INSTS_VALU_ADD_F64": 4.0, "SQ_INSTS_VALU_MUL_F64": 4.0, "SQ_INSTS_VALU_FMA_F64": 4.0,
+               "SQ_INSTS_VALU_TRANS_F32": 4.0, "SQ_INSTS_VALU_TRANS_F64": 8.0}
+
+
+def valu_cycles_per_ray(rec):
+    """SIMD cycles per ray the record's VALU instructions occupy, weighted by class (VALU_CYCLES, else 2), or None when
+    the record lacks the instruction mix."""
+    c = rec.get("counters", {})
+    if "SQ_INSTS_VALU" not in c or not all(k in c for k in VALU_CYCLES):
+        return None
+    other = c["SQ_INSTS_VALU"] - sum(c[k] for k in VALU_CYCLES)
+    return (2.0 * other + sum(w * c[k] for k, w in VALU_CYCLES.items())) / rec["rays"]
 # SURVEY.md 8d algorithmic bytes per event of the REFERENCE traversal (reference tree, f64 layout)
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
 # MI355X_MICROARCH.md "Indexed rows": rows shared by every workgroup, gathered from the XCD's L2: 16.8-18.8 TB/s
@@ -200,6 +216,10 @@ def main():
     ap.add_argument("--shard", type=int, default=0, help="with --shard-of: which shard")
     ap.add_argument("--shard-map", default="auto", choices=("auto", "interleave", "balanced"),
                     help="tile deal across ranks (rp_render_params.shard_map); auto = balanced for N > 1 or --shard-of")
+    ap.add_argument("--contract-steps", type=int, default=-1,
+                    help="frames timed after the headline under SURVEY.md 8c's RNG contract itself (one stream per "
+                         "pixel, samples_per_stream = spp), reported as contract_one_stream (-1 = 3 for the default "
+                         "workload, 0 = off)")
     ap.add_argument("--opt", action="append", default=[],
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
@@ -262,7 +282,8 @@ def main():
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
-    def step(k_start=None, k_end=None):
+    def step(k_start=None, k_end=None, spx=None):
+        spx = spx if spx is not None else sp
         i = state["k"] % F_
         state["k"] += 1
         st = streams[i]
@@ -270,7 +291,7 @@ def main():
             st.wait_event(freed[i])
         if k_start is not None:
             k_start.record(st)
-        ds.render_device(sp, bufs[i], ctrs[i], stream=st, workspace=wss[i])
+        ds.render_device(spx, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         if k_end is not None:
             k_end.record(st)
         if st is not main_stream:
@@ -281,7 +302,7 @@ def main():
             freed[i] = done if st is not main_stream else None
             return
         # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks), on the main stream
-        ds.frame_gather(comm, sp, bufs[i], frame_bgra=frame, counters=ctrs[i], stream=main_stream,
+        ds.frame_gather(comm, spx, bufs[i], frame_bgra=frame, counters=ctrs[i], stream=main_stream,
                         workspace=wss[i])
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
@@ -317,6 +338,42 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     elapsed_max = float(tmax.item())
     value = rays_step * args.steps / elapsed_max / 1e6
+
+    # SURVEY.md 8c's RNG contract itself: one StdRng stream per pixel running the unchanged body of
+    # main.rs:70-86 over all spp (samples_per_stream = spp), timed the same way after the headline frames
+    contract = None
+    csteps = args.contract_steps if args.contract_steps >= 0 else (
+        3 if not (args.samples_per_stream or args.shard_of or args.spp or args.tile) else 0)
+    if csteps > 0 and params.spp > (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM):
+        pc = replace(params, samples_per_stream=params.spp)
+        spc = shard_params(pc, rank, world)
+        for w in wss:
+            ds.reserve(spc, w)
+        for _ in range(F_):  # one frame per in-flight workspace: each learns this contract's tile costs
+            step(spx=spc)
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(csteps):
+            step(spx=spc)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tc = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        cc = [c.cpu().tolist() for c in ctrs]
+        if any(c[3] != 0 for c in cc):
+            raise RuntimeError(f"render kernel reported status {[c[3] for c in cc]} under the one-stream contract")
+        crays = cc[0][0]
+        contract = {"samples_per_stream": params.spp, "steps": csteps, "warmup": F_,
+                    "ms_per_step": round(float(tc.item()) / csteps * 1e3, 3),
+                    "value": round(crays * csteps / float(tc.item()) / 1e6, 3), "unit": "Mrays/s",
+                    "rays_per_frame": int(crays),
+                    "note": "SURVEY.md 8c: one StdRng::seed_from_u64(seed + j*W + i) stream per pixel over all spp "
+                            "(main.rs:70-86 unchanged); the headline uses streams of samples_per_stream samples"}
 
     if rank == 0:
         local_rays = rays_step / world  # this rank's launch (shards carry near-equal work under the balanced plan)
@@ -368,10 +425,25 @@ def main():
                                      "frac": round(tf / FP64_VALU_PEAK_TFLOPS, 4),
                                      "note": "upper bound: f64 FMA (2 flops), MUL, ADD, transcendental wave-instructions "
                                              "x 64 lanes; peak = half the FP32 vector rate (spec)"}
-            binding = ("valu_issue", valu_frac) if valu_frac >= tr_frac else ("hbm_traffic", tr_frac)
+            wcyc = valu_cycles_per_ray(rec)
+            pipe = None
+            if wcyc is not None:
+                # the VALU pipes' busy fraction: weighted SIMD cycles of this launch's rays over the SIMD-cycles of the launch
+                pipe = wcyc * local_rays / kernel_s / (SIMDS * CLOCK_HZ)
+                roof["valu_issue"]["weighted"] = {
+                    "frac": round(pipe, 4), "simd_cycles_per_ray": round(wcyc, 2),
+                    "weights": {**{k.replace("SQ_INSTS_VALU_", "").lower(): v for k, v in VALU_CYCLES.items()},
+                                "other": 2.0},
+                    "note": "SIMD cycles per wave64 instruction by class (bench.py VALU_CYCLES): f64 add/mul/fma at half "
+                            "the f32 rate, transcendentals at the guide's 8-cycle single-wave issue (f64 assumed twice "
+                            "that); unweighted frac counts every instruction at 2 cycles"}
+            valu_bind = pipe if pipe is not None else valu_frac
+            binding = (("valu_pipe_weighted" if pipe is not None else "valu_issue"), valu_bind) \
+                if valu_bind >= tr_frac else ("hbm_traffic", tr_frac)
             roof["binding"] = {"resource": binding[0], "frac": round(binding[1], 4),
+                               "unweighted_valu_issue": round(valu_frac, 4),
                                "note": "the kernel is latency-bound (cycle_budget: waves wait on memory ~45 % of their "
-                                       "cycles at 4 waves/SIMD); neither VALU issue nor memory traffic is near its roof"}
+                                       "cycles at 4 waves/SIMD); the weighted VALU pipe occupancy is the larger share"}
         ref_bpr = reference_equivalent(args.config)
         roof["reference_equivalent"] = {
             "bytes_per_ray": round(ref_bpr, 1), "GBps": round(ref_bpr * local_rays / kernel_s / 1e9, 1),
@@ -398,6 +470,7 @@ def main():
             "binding_frac": round(binding[1], 4) if binding else None,
             "binding_resource": binding[0] if binding else None,
             "cpu_baseline": None,
+            "contract_one_stream": contract,
         }
         if world == 1 and not args.no_cpu_baseline and not args.shard_of:
             log("[rank 0] cpu baseline ...")
