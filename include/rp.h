@@ -412,9 +412,10 @@ int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
  * pass counters does not learn the status.  Tile costs (the collectives also all-gather every rank's measured
  * tile costs for frames of <= 16384 tiles) and the balanced plan live in the workspace: the gather reads the
  * workspace's plan and measured costs and writes its learned cost table on `stream`, and the next render with the
- * same workspace rewrites the first two and reads the third on ITS stream -- so that render must be stream-ordered
- * after this gather (same stream, or an event; bench.py waits on the gather's event before reusing a workspace).
- * Frames in flight use one workspace per frame. */
+ * same workspace rewrites the first two and reads the third on ITS stream.  The library orders the two itself: the
+ * gather records an event in the workspace at its end, and the next render with that workspace makes its stream wait
+ * on it (a caller with separate render and gather streams cannot race them).  Frames in flight use one workspace
+ * per frame. */
 int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                     const double* d_shard_rgb, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, void* stream);

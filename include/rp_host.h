@@ -73,6 +73,11 @@ int rph_bvh_tree_hash(const rp_scene_desc* desc, uint32_t node_format, uint32_t 
  * generation (the synthetic C5 mesh: 120 M draws); multi-threaded. */
 int rph_stdrng_u64(const uint8_t seed[32], uint64_t first, uint64_t n, uint64_t* out);
 
+/* Test hook: the magic numbers of the render kernel's unit decode (raytracing-potato_amd/csrc/rp_kernel.h
+ * rpk::make_div32, the same header the library's launches use): for a divisor d >= 1, m and s such that
+ * floor(n / d) == (n * m) >> s (64-bit product) for every n < 2^31.  RP_EINVAL for d == 0. */
+int rph_make_div32(uint32_t d, uint32_t* m, uint32_t* s);
+
 const char* rph_last_error(void);
 
 #ifdef __cplusplus

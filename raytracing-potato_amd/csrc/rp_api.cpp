@@ -85,8 +85,13 @@ void dfree(void* p) {
 constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
 constexpr uint32_t DEF_UNIT_QUEUES = RP_QUEUES_XCD_TILES;
 constexpr double DEF_COST_TRAVERSE = 0.7;
-// Balanced plans of scenes past the Infinity Cache deal square blocks of tiles (rpk::launch_tile_plan): 4 x 4, or 2 x 2,
+// Balanced plans under tile_order = RP_TILES_MORTON deal square blocks of tiles (rpk::launch_tile_plan): 4 x 4, or 2 x 2,
 // as long as every rank still gets >= PLAN_UNITS_MIN of them (balance needs many units per rank), else single tiles.
+// (AUTO is the cost order for every scene since v49, which deals tile by tile; the block deal runs only when a caller
+// asks for Z-order tiles.)  The deal hands out U = block^2 consecutive positions of the block-sorted order: on a grid
+// whose tiles_x or tiles_y is not a multiple of block, the edge blocks hold fewer than U tiles, so a unit after the
+// first partial block straddles two blocks -- counts and balance are unchanged, only the squares are no longer whole
+// (tests/test_dist.py test_block_deal_ragged_grid).
 constexpr uint32_t PLAN_UNITS_MIN = 32;
 uint32_t plan_block(uint32_t n_tiles, uint32_t nranks) {
   for (uint32_t b : {4u, 2u})
@@ -139,6 +144,12 @@ struct rp_workspace {
   uint32_t fcost_geom[4] = {0, 0, 0, 0};  // width, height, tile_w, tile_h of the learned table
   uint32_t fcost_ranks = 0;               // ranks whose gather made it (1: a whole-frame render on one device)
   rpk::WfBuffers wf{};               // the stage-split engine's path-slot pool (engine = wavefront only)
+  // A frame gather reads this workspace's measured costs (d_meas) and writes its learned table (d_fcost) on the gather
+  // stream; the next render on the workspace reads the table and clears d_meas on ITS stream.  The gather records
+  // this event at its end and render_shard waits on it, so a caller with separate render and gather streams cannot
+  // race the two; on one stream the wait is already satisfied.
+  hipEvent_t ev_gathered = nullptr;
+  bool gathered_pending = false;
 };
 
 struct rp_scene {
@@ -194,6 +205,7 @@ void ws_release(rp_workspace* w) {
                   (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
                   (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0})
     dfree(p);
+  if (w->ev_gathered) (void)hipEventDestroy(w->ev_gathered);
   *w = rp_workspace{};
 }
 
@@ -209,7 +221,7 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
       !dalloc(&w->d_fcost, 2 * rpk::TILE_SORT_MAX) || !dalloc(&w->d_sort, rpk::SORT_SCRATCH) ||
       !dalloc(reinterpret_cast<uint8_t**>(&w->d_slab), lanes * rpk::rng_slab_bytes_per_lane()) ||
       !dalloc(&w->d_spill, lanes * std::max<uint64_t>(1, s->ks.stack_depth - s->ks.lds_depth)) ||
-      !dalloc(&w->d_t0, lanes)) {
+      !dalloc(&w->d_t0, lanes) || hipEventCreateWithFlags(&w->ev_gathered, hipEventDisableTiming) != hipSuccess) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
   }
@@ -644,6 +656,11 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   DeviceGuard g(s->device);
   uint64_t* ctr = d_counters ? d_counters : w->d_ctr;
   hipStream_t st = (hipStream_t)stream;
+  // the last frame gather on this workspace (another stream, perhaps) has read d_meas and written d_fcost
+  if (w->gathered_pending) {
+    RP_HIP(hipStreamWaitEvent(st, w->ev_gathered, 0));
+    w->gathered_pending = false;
+  }
   RP_HIP(hipMemsetAsync(ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
   if (t.n_slots == 0) return RP_OK;
   if (p->spp == 0) {
@@ -774,9 +791,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
       if ((rc = probe(0, 1, t.n_tiles, lattice, probe_px))) return rc;
       frame_cost = w->d_tile_cost;
     }
-    // scenes past the Infinity Cache (Z-order tiles) deal square blocks of tiles: a rank's tiles stay in compact
-    // squares of the frame, so its working set does too (C5 8-way shards: DESIGN.md 6); cache-resident scenes deal
-    // tile by tile
+    // Z-order tiles (tile_order = MORTON, on request only) deal square blocks of tiles: a rank's tiles stay in compact
+    // squares of the frame, so its working set does too (C5 8-way shards: DESIGN.md 6); the cost order (AUTO, every
+    // scene) deals tile by tile
     const uint32_t block = order_mode == RP_TILES_MORTON ? plan_block(t.n_tiles, t.shards) : 1u;
     int e = rpk::launch_tile_plan(frame_cost, t.n_tiles, t.shards, t.tiles_x, block, w->d_plan, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile plan launch: ") + hipGetErrorString((hipError_t)e));
@@ -904,13 +921,16 @@ int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_re
   DeviceGuard g(s->device);
   if (!w->meas_on || gp.t.n_tiles > (uint32_t)rpk::TILE_SORT_MAX) {
     w->fcost_valid = false;
-    return RP_OK;
+  } else {
+    const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
+    int e = rpk::launch_learn_costs(w->d_meas_g, w->d_meas_g + n, gp.stride_tiles, gp.geom.nranks, gp.t.n_tiles,
+                                    gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
+    if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
+    set_fcost(w, p, gp.t, gp.geom.nranks);
   }
-  const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
-  int e = rpk::launch_learn_costs(w->d_meas_g, w->d_meas_g + n, gp.stride_tiles, gp.geom.nranks, gp.t.n_tiles,
-                                  gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
-  if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
-  set_fcost(w, p, gp.t, gp.geom.nranks);
+  // the next render on this workspace waits for the collectives (which read d_meas) and the table (ev_gathered)
+  RP_HIP(hipEventRecord(w->ev_gathered, st));
+  w->gathered_pending = true;
   return RP_OK;
 }
 

@@ -283,6 +283,10 @@ RPK_INLINE void rng_refill(RngT<RN>& r, bool alive, bool fresh, uint64_t seed, u
     }
   }
   if (room || served) *r.end = end1 + served;
+  // An executor lane stored blocks into its owner lane's slab above, and the owner reads them through ring_u64 later:
+  // a cross-lane hand-off inside one wave.  One wave's memory operations stay in order, and this wavefront-scope fence
+  // states the ordering for the memory model; it compiles to no instruction (the kernel's ISA is unchanged).
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 
 // Jitter words 4s..4s+3 of the pixel-start stream (block s/4).

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "rp_bvh.h"
+#include "rp_kernel.h"
 
 namespace {
 
@@ -727,6 +728,14 @@ int rph_stdrng_u64(const uint8_t seed[32], uint64_t first, uint64_t n, uint64_t*
   }
   work(0, std::min<uint64_t>(n, per));
   for (auto& t : th) t.join();
+  return RP_OK;
+}
+
+int rph_make_div32(uint32_t d, uint32_t* m, uint32_t* s) {
+  if (d == 0 || !m || !s) return fail("rph_make_div32: d must be >= 1 and m, s non-NULL");
+  const rpk::Div32 v = rpk::make_div32(d);
+  *m = v.m;
+  *s = v.s;
   return RP_OK;
 }
 

@@ -134,7 +134,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_selfcheck_ex", "rph_bvh_traversal_stats_ex", "rph_bvh_tree_hash", "rph_last_error",
-                "rph_stdrng_u64"]
+                "rph_stdrng_u64", "rph_make_div32"]
 
 
 def rp_lib_path() -> str:
@@ -243,6 +243,7 @@ def host() -> ctypes.CDLL:
     lib.rph_bvh_tree_hash.argtypes = [POINTER(rp_scene_desc), c_uint32, c_uint32, POINTER(c_uint64)]
     lib.rph_last_error.restype = c_char_p
     lib.rph_stdrng_u64.argtypes = [c_void_p, c_uint64, c_uint64, c_void_p]
+    lib.rph_make_div32.argtypes = [c_uint32, POINTER(c_uint32), POINTER(c_uint32)]
     _host = lib
     return lib
 

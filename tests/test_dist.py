@@ -208,3 +208,28 @@ def test_balanced_gather_rebuilds_frame(tmp_path, world):
     assert np.array_equal(np.load(tmp_path / "frame.npy"), ref)
     orders = np.load(tmp_path / "orders.npy")
     assert (orders == orders[0]).all() and not np.array_equal(orders[0], np.arange(15))
+
+def test_block_deal_ragged_grid():
+    """on a grid whose tile counts are not multiples of the block, the edge blocks hold fewer than block^2
+    tiles and the deal's units of block^2 consecutive sorted positions then straddle two blocks (rp_api.cpp plan_block's
+    comment).  What still holds: a permutation, the interleave's count per rank, balanced loads, and most of a rank's
+    tiles in whole squares; what does not: every square whole."""
+    from rtpotato.dist import deal_tiles
+    rng = np.random.default_rng(11)
+    tx, ty, world, block = 65, 61, 2, 4
+    n = tx * ty
+    cost = rng.integers(50, 500, n)
+    order = deal_tiles(cost, world, tx, block)
+    assert np.array_equal(np.sort(order), np.arange(n))
+    bx_n = -(-tx // block)
+    split = 0
+    for r in range(world):
+        mine = order[r::world]
+        assert len(mine) == len(range(r, n, world))
+        blocks = (mine // tx // block) * bx_n + (mine % tx) // block
+        size = np.bincount((np.arange(n) // tx // block) * bx_n + (np.arange(n) % tx) // block)
+        b, counts = np.unique(blocks, return_counts=True)
+        split += int((counts != size[b]).sum())
+    loads = [cost[order[r::world]].sum() for r in range(world)]
+    assert max(loads) / np.mean(loads) < 1.03
+    assert 0 < split < 0.5 * len(size)  # some squares split (documented), most whole

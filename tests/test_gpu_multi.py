@@ -76,25 +76,28 @@ def test_balanced_plan_rebuilds_frame(gpu, world):
 
 
 @pytest.mark.parametrize("world", [2, 8])
-def test_block_deal_matches_restatement(gpu, world):
-    """Scenes dealt in Z-order (large scenes: tile_order morton) make balanced plans of square tile blocks
+@pytest.mark.parametrize("W,H", [(512, 512), (520, 488)])
+def test_block_deal_matches_restatement(gpu, world, W, H):
+    """Scenes dealt in Z-order (tile_order morton, on request: AUTO is the cost order) make balanced plans of square tile blocks
     (rp_api.cpp plan_block: 4 x 4 here, 4,096 tiles) from the installed cost table: the device plan equals the NumPy
-    restatement (rtpotato.dist.deal_tiles with block = 4), and the shards rebuild the interleave frame bit for bit."""
+    restatement (rtpotato.dist.deal_tiles with block = 4), and the shards rebuild the interleave frame bit for bit.  The
+    520 x 488 grid (65 x 61 tiles) is ragged: its edge blocks hold fewer than block^2 tiles, so later units
+    straddle two blocks (rp_api.cpp plan_block) -- the device must still equal the restatement and rebuild the frame."""
     import torch
     from rtpotato import _ffi as F
     from rtpotato import scenes
     from rtpotato.dist import deal_tiles, max_slots, shard_params
     from rtpotato.scene import RenderParams, shard_slot_count
-    W = H = 512
     sc = scenes.configure(scenes.bunny_full(), W, H)
     p = RenderParams(W, H, 1, 8, scenes.DEFAULT_SEED, 8, 8, shard_map=F.RP_SHARD_BALANCED)
-    tx = W // 8
-    n = tx * (H // 8)
+    tx, ty = -(-W // 8), -(-H // 8)
+    n = tx * ty
     rng = np.random.default_rng(3)
-    xs, ys = np.meshgrid(np.arange(tx), np.arange(H // 8))
+    xs, ys = np.meshgrid(np.arange(tx), np.arange(ty))
     cost = ((50 + 500 * (((xs - 32) ** 2 + (ys - 32) ** 2) < 400)) * rng.uniform(0.8, 1.2, xs.shape)).astype(np.uint32)
     table = np.stack([cost.reshape(-1), cost.reshape(-1) // 4])
-    want = deal_tiles(table[0], world, tx, 4)
+    block = next((b for b in (4, 2) if n >= 32 * world * b * b), 1)  # rp_api.cpp plan_block
+    want = deal_tiles(table[0], world, tx, block)
     S = max_slots(p, world)
     gathered = torch.zeros(world * S * 3, dtype=torch.float64, device="cuda")
     ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
@@ -116,7 +119,7 @@ def test_block_deal_matches_restatement(gpu, world):
                                             frame.data_ptr(), s))
         torch.cuda.synchronize()
     assert np.array_equal(frame.cpu().numpy().reshape(H, W, 3), ref)
-    assert n == 4096
+    assert (n, block) == (4096, 4) if W == 512 else (block > 1 and tx % block != 0)
 
 
 def test_balanced_host_render_and_unpack(gpu):
