@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 7
+#define RP_ABI_VERSION 8
 
 /* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -231,6 +231,13 @@ enum { RP_COLLAPSE_AUTO = 0, RP_COLLAPSE_GREEDY = 1, RP_COLLAPSE_SAH = 2 };
  * line (64-B quantized nodes: a pad slot after odd families; f32 nodes are one line each, so the same as DFS).  Speed
  * only: the image never depends on it. */
 enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
+/* rp_scene_options.primary (ABI v8): the coherent primary pass.  AUTO: when the camera's lens_radius is 0 (a camera
+ * ray's direction then depends only on its jitter, render.rs:36-44,74-82) and the workspace is reserved for it
+ * (rp_workspace_reserve: 4 bytes per pixel and sample of the shard), every camera ray of the frame is traced first in
+ * waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 samples), and the path loop starts each sample from that
+ * closest hit instead of traversing: the same image (the closest hit does not depend on the order rays are traced,
+ * up to exact-t ties).  OFF: camera rays traverse in the path loop. */
+enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles); PLOC */
@@ -256,6 +263,8 @@ typedef struct rp_scene_options {
                                render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */
   uint32_t collapse;        /* RP_COLLAPSE_*: the 4-wide collapse of the host-built tree (ABI v6) */
   uint32_t node_layout;     /* RP_LAYOUT_*: node order of a device-built (PLOC) tree (ABI v7) */
+  uint32_t primary;         /* RP_PRIMARY_*: the coherent primary pass (ABI v8) */
+  uint32_t reserved;        /* 0 */
 } rp_scene_options;
 
 typedef struct rp_stats {
@@ -351,6 +360,14 @@ int rp_workspace_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_r
                             uint32_t* costs, uint32_t n);
 int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                                 const uint32_t* costs, uint32_t ranks);
+/* How the last render enqueued with `workspace` (NULL = the scene's) was scheduled (ABI v8): RP_FRAME_* bits.
+ * Host state only (no device synchronisation); results never depend on any of it. */
+enum {
+  RP_FRAME_PRIMARY_PASS = 1,  /* the coherent primary pass traced the camera rays (rp_scene_options.primary) */
+  RP_FRAME_LEARNED_ORDER = 2, /* tiles ordered / dealt from the workspace's learned cost table */
+  RP_FRAME_PROBED = 4         /* a cost probe launch ran */
+};
+int rp_workspace_frame_info(const rp_scene* scene, const rp_workspace* workspace, uint32_t* flags);
 /* The deal order of params' frame (one entry per frame tile; shard s's k-th tile is tile_map[s + k*num_shards]):
  * for RP_SHARD_BALANCED the plan the last render of this frame in `workspace` (NULL = the scene's) made, for the
  * interleave 0, 1, 2, ...  n >= the frame's tile count.  Synchronises the device. */

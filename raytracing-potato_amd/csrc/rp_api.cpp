@@ -85,6 +85,8 @@ void dfree(void* p) {
 constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4;
 constexpr uint32_t DEF_UNIT_QUEUES = RP_QUEUES_XCD_TILES;
 constexpr double DEF_COST_TRAVERSE = 0.7;
+// Largest hint buffer a workspace reserves for the coherent primary pass (4 B per pixel and sample of a shard).
+constexpr uint64_t PRIM_HINT_MAX_BYTES = 64ull << 30;
 // Balanced plans under tile_order = RP_TILES_MORTON deal square blocks of tiles (rpk::launch_tile_plan): 4 x 4, or 2 x 2,
 // as long as every rank still gets >= PLAN_UNITS_MIN of them (balance needs many units per rank), else single tiles.
 // (AUTO is the cost order for every scene since v49, which deals tile by tile; the block deal runs only when a caller
@@ -117,6 +119,8 @@ struct rp_workspace {
   double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames
   uint32_t* d_partial_hits = nullptr;
   uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
+  int32_t* d_hint = nullptr;         // the coherent primary pass's closest primitive per shard slot and sample
+  uint64_t hint_cap = 0;             // capacity of d_hint in entries
   double* d_gs_rgb = nullptr;        // gather staging: this rank's shard, padded to the stride (3 f64 / slot)
   uint32_t* d_gs_bgra = nullptr;     //   ... its to_srgb_u8 bytes (1 word / slot)
   double* d_gather_rgb = nullptr;    //   all ranks' shards (nranks x stride x 3 f64)
@@ -150,6 +154,7 @@ struct rp_workspace {
   // race the two; on one stream the wait is already satisfied.
   hipEvent_t ev_gathered = nullptr;
   bool gathered_pending = false;
+  uint32_t frame_flags = 0;  // RP_FRAME_* of the last render (rp_workspace_frame_info)
 };
 
 struct rp_scene {
@@ -203,7 +208,8 @@ void ws_release(rp_workspace* w) {
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
                   (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
-                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0})
+                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0,
+                  (void*)w->d_hint})
     dfree(p);
   if (w->ev_gathered) (void)hipEventDestroy(w->ev_gathered);
   *w = rp_workspace{};
@@ -383,6 +389,8 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
     return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
   if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
   if (o.node_layout > RP_LAYOUT_DFS_LINE) return fail(RP_EINVAL, "options.node_layout must be RP_LAYOUT_*");
+  if (o.primary > RP_PRIMARY_OFF) return fail(RP_EINVAL, "options.primary must be RP_PRIMARY_*");
+  if (o.reserved != 0) return fail(RP_EINVAL, "options.reserved must be 0");
   return RP_OK;
 }
 
@@ -415,6 +423,17 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
   DeviceGuard g(s->device);
   const uint64_t units = t.nbatch > 1 ? t.n_slots * t.nbatch : 0;
   if ((rc = grow(w->d_partial, w->d_partial_hits, w->partial_units, units, 3, 1, "sample-batch workspace"))) return rc;
+  // the coherent primary pass's hints: 4 bytes per shard slot and sample (C3 2.1 GB, C5 17 GB of the 288 GB HBM); a
+  // frame past PRIM_HINT_MAX_BYTES renders without the pass
+  const uint64_t hints = t.n_slots * p->spp;
+  if (s->opt.primary != RP_PRIMARY_OFF && s->opt.engine == RP_ENGINE_MEGAKERNEL && hints > w->hint_cap &&
+      hints * sizeof(int32_t) <= PRIM_HINT_MAX_BYTES) {
+    dfree(w->d_hint);
+    w->d_hint = nullptr;
+    w->hint_cap = 0;
+    if (!dalloc(&w->d_hint, hints)) return fail(RP_ENOMEM, "hipMalloc primary-pass hints");
+    w->hint_cap = hints;
+  }
   if (gather) {
     const uint64_t stride = stage_slots(t);
     if ((rc = grow(w->d_gs_rgb, w->d_gs_bgra, w->gs_slots, stride, 3, 1, "gather staging"))) return rc;
@@ -754,6 +773,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     pk.tile_map = nullptr;
     probe_px = pk.probe_px;
     RP_HIP(hipMemsetAsync(w->d_probe_ctr, 0, sizeof(uint64_t) * rpk::CTR_N, st));
+    w->frame_flags |= RP_FRAME_PROBED;
     RP_HIP(hipMemsetAsync(w->d_tile_cost, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
     int e = rpk::launch_render(ks, pk, d_rgb, nullptr, w->d_probe_ctr, w->d_queue + rpk::QUEUE_PROBE, grid_for(pk.n_slots), stream);
     if (e != 0) return fail(RP_EHIP, std::string("probe launch: ") + hipGetErrorString((hipError_t)e));
@@ -767,6 +787,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   uint32_t probe_px = 0;
   const uint32_t* frame_cost = nullptr;  // per-frame-tile costs (sum, max) the plan and the shard order use
   w->plan_on = false;
+  w->frame_flags = 0;
   // Scheduling costs.  The megakernel measures every unit's duration into its tile's cost (kp.tile_meas); once a
   // frame of this geometry has been rendered whole on one device, or gathered from all ranks, the workspace holds a
   // learned per-tile table and the next frame schedules from it -- no probe launch.  For a balanced plan over
@@ -779,6 +800,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   if (probe_order) order_mode = RP_TILES_COST;
   const bool learned = measure && !probe_order && fcost_matches(w, p, t);
   const uint32_t learned_px = t.tw * t.th * std::max(1u, t.nbatch);  // units per tile: sum / units = mean unit
+  if (learned) w->frame_flags |= RP_FRAME_LEARNED_ORDER;
   if (t.balanced) {
     // RP_SHARD_BALANCED: deal the frame's tiles to the ranks by cost (rpk::launch_tile_plan).  Without a learned
     // table, probe the whole frame (deterministic costs, rp_device.h trav_step COUNT); scenes past the Infinity
@@ -820,6 +842,27 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
                                   w->d_tile_order, w->d_sort, stream);
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
+  }
+  // The coherent primary pass (rp.h RP_PRIMARY_AUTO): camera rays of a lens-less camera traced in neighbouring waves of
+  // 64 before the path loop, which then starts every sample at its closest hit.  Needs the workspace's hint buffer
+  // (rp_workspace_reserve); without it, or with a lens, camera rays traverse in the path loop.
+  const uint64_t n_hints = t.n_slots * p->spp;
+  if (s->opt.primary != RP_PRIMARY_OFF && s->opt.engine == RP_ENGINE_MEGAKERNEL && cam->lens_radius == 0.0 &&
+      w->d_hint && n_hints <= w->hint_cap) {
+    kp.prim_quads_x = (t.tw + 1) / 2;
+    kp.prim_sgroups = (p->spp + rpk::PRIM_SAMPLES - 1) / rpk::PRIM_SAMPLES;
+    const uint64_t per_tile = (uint64_t)kp.prim_quads_x * ((t.th + 1) / 2) * kp.prim_sgroups;
+    // queue g's words count its tiles' items, plus one failed fetch per wave and per queue it passes
+    const uint64_t per_queue = ((t.n_shard_tiles + rpk::QUEUE_GROUPS - 1) / rpk::QUEUE_GROUPS) * per_tile;
+    if (per_tile < (1ull << 31) && per_queue + resident * rpk::QUEUE_GROUPS < 0xffffffffull) {
+      kp.prim_items_tile = (uint32_t)per_tile;
+      kp.prim_hint = w->d_hint;
+      kp.dv_sps = rpk::make_div32(t.sps);
+      const uint64_t items = per_tile * t.n_shard_tiles;
+      int e = rpk::launch_primary(ks, kp, ctr, w->d_queue + rpk::QUEUE_PRIM, grid_for(items * rpk::RENDER_BLOCK), stream);
+      if (e != 0) return fail(RP_EHIP, std::string("primary pass launch: ") + hipGetErrorString((hipError_t)e));
+      w->frame_flags |= RP_FRAME_PRIMARY_PASS;
+    }
   }
   RP_HIP(hipMemsetAsync(w->d_meas, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
   kp.tile_meas = measure ? w->d_meas : nullptr;
@@ -1089,6 +1132,14 @@ int rp_workspace_tile_map(rp_scene* s, rp_workspace* w, const rp_render_params* 
   DeviceGuard g(s->device);
   RP_HIP(hipDeviceSynchronize());
   RP_HIP(hipMemcpy(tile_map, w->d_plan, sizeof(uint32_t) * t.n_tiles, hipMemcpyDeviceToHost));
+  return RP_OK;
+}
+
+int rp_workspace_frame_info(const rp_scene* s, const rp_workspace* w, uint32_t* flags) {
+  if (!s || !flags) return fail(RP_EINVAL, "scene and flags must be non-NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  *flags = w->frame_flags;
   return RP_OK;
 }
 

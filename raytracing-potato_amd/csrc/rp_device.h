@@ -119,6 +119,57 @@ RPK_INLINE void chacha12(const uint32_t k[8], uint32_t ctr, uint32_t o[16]) {
   o[12] = x12 + ctr; o[13] = x13; o[14] = x14; o[15] = x15;
 }
 
+// The same block computed by the four lanes of a DPP quad together (the coherent primary pass: four neighbouring
+// samples of a pixel share a jitter block).  Lane c of the quad holds column c of the state -- words c, 4 + c, 8 + c,
+// 12 + c -- so a column round is one quarter round per lane, and a diagonal round is one quarter round per lane after
+// rotating rows 1, 2, 3 of the state by 1, 2, 3 lanes (quad_perm DPP moves), rotated back after it.  A quarter of a
+// block's VALU per lane.  Every lane of the quad must be active and pass the same key and counter; returns the
+// lane's column of the output block (words c, 4 + c, 8 + c, 12 + c).
+RPK_INLINE uint32_t quad_rot(uint32_t v, int by) {  // lane c of a quad reads lane (c + by) & 3
+  return by == 1 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x39, 0xF, 0xF, false)
+       : by == 2 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false)
+                 : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x93, 0xF, 0xF, false);
+}
+RPK_INLINE uint4 chacha12_quad(const uint32_t k[8], uint32_t ctr) {
+  const uint32_t c = __lane_id() & 3u;
+  const uint32_t a0 = c == 0 ? 0x61707865u : c == 1 ? 0x3320646eu : c == 2 ? 0x79622d32u : 0x6b206574u;
+  const uint32_t b0 = c == 0 ? k[0] : c == 1 ? k[1] : c == 2 ? k[2] : k[3];
+  const uint32_t c0 = c == 0 ? k[4] : c == 1 ? k[5] : c == 2 ? k[6] : k[7];
+  const uint32_t d0 = c == 0 ? ctr : 0u;
+  uint32_t a = a0, b = b0, x = c0, d = d0;
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    RPK_QR(a, b, x, d);  // column c
+    b = quad_rot(b, 1);
+    x = quad_rot(x, 2);
+    d = quad_rot(d, 3);
+    RPK_QR(a, b, x, d);  // diagonal starting at word c
+    b = quad_rot(b, 3);
+    x = quad_rot(x, 2);
+    d = quad_rot(d, 1);
+  }
+  return make_uint4(a + a0, b + b0, x + c0, d + d0);
+}
+// Row `row` of a block held column-wise by a quad (chacha12_quad): words 4 row .. 4 row + 3.  Lane m of the quad holds
+// word 4 row + m in component `row` of its column; each of the four components is read from every lane (DPP
+// broadcasts within the quad) and the lane keeps its own row.
+RPK_INLINE uint32_t quad_bcast(uint32_t v, int from) {  // every lane of a quad reads lane `from`
+  return from == 0 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false)
+       : from == 1 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, false)
+       : from == 2 ? (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xAA, 0xF, 0xF, false)
+                   : (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xFF, 0xF, 0xF, false);
+}
+RPK_INLINE uint4 quad_row(uint4 col, uint32_t row) {
+  uint32_t o[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const uint32_t r0 = quad_bcast(col.x, m), r1 = quad_bcast(col.y, m), r2 = quad_bcast(col.z, m),
+                   r3 = quad_bcast(col.w, m);
+    o[m] = row == 0 ? r0 : row == 1 ? r1 : row == 2 ? r2 : r3;
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // rand_core 0.6 seed_from_u64: PCG32 expansion of the u64 into the 8 key words.
 RPK_INLINE void seed_key(uint64_t state, uint32_t key[8]) {
 #pragma unroll
@@ -1504,6 +1555,22 @@ RPK_INLINE uint32_t unit_spp(KArgsPtr A, uint32_t batch) {
   return min(A->P.spp_batch, A->P.spp - batch * A->P.spp_batch);
 }
 
+// Camera::shoot (render.rs:32-52) from the jittered frame coordinates (ju, jv) and the UnitDisk sample (dx, dy): one
+// definition for the path loop (start_sample) and the coherent primary pass, which passes (0, 0) -- with lens_radius 0
+// the disk is multiplied by 0 and only the signs of zeros could differ (the direction never: -focal - 0 and
+// x - (+-0) for x != 0 are exact, and x = (2 ju - 1) ... is +0 when 2 ju - 1 = 0).
+RPK_INLINE void camera_dir(KArgsPtr A, double ju, double jv, double dx, double dy, V3& o, V3& d) {
+  // tan(fov/2) is computed on the host (render.rs:33 is a per-camera constant; same libm as the reference)
+  const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
+  const V3 lo = v3(lens * dx, lens * dy, 0.0);
+  const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
+  double m[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
+  d = matvec(m, dl);
+  o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
+}
+
 // One camera sample (main.rs:75-76): make_uv_jitter draws 2s, 2s+1 of a CLONE of the pixel-start
 // stream (render.rs:74-82) = keystream words 4s..4s+3 = block s/4 at offset 4(s%4); Camera::shoot
 // (render.rs:32-52) then draws its UnitDisk from the main stream (even when lens_radius == 0).
@@ -1533,16 +1600,7 @@ RPK_INLINE void start_sample(R& rng, uint32_t s, uint32_t pi, uint32_t pj, V3& o
     }
     if (done) break;
   }
-  A = kargs();
-  // tan(fov/2) is computed on the host (render.rs:33 is a per-camera constant; same libm as the reference)
-  const double lens = A->P.lens, tanf = A->P.tan_fov, focal = A->P.focal, aspect = A->P.aspect;
-  const V3 lo = v3(lens * dx, lens * dy, 0.0);
-  const V3 dl = normalize(sub(v3((2.0 * ju - 1.0) * tanf * focal * aspect, (2.0 * jv - 1.0) * tanf * focal, -focal), lo));
-  double m[9];
-#pragma unroll
-  for (int q = 0; q < 9; q++) m[q] = A->P.orient[q];
-  d = matvec(m, dl);
-  o = add(matvec(m, lo), v3(A->P.pos[0], A->P.pos[1], A->P.pos[2]));
+  camera_dir(kargs(), ju, jv, dx, dy, o, d);
 }
 
 }  // namespace rpk

@@ -59,7 +59,7 @@ enum {
   DREG_NODE, DREG_PRIM, DREG_STEP, DREG_SHADE, DREG_SURF, DREG_SPHUV, DREG_TEX, DREG_LAMBERT, DREG_METAL,
   DREG_DIELEC, DREG_LOOP_LAMBERT, DREG_LOOP_METAL, DREG_END_SAMPLE, DREG_END_PIXEL, DREG_START_SAMPLE,
   DREG_REFILL, DREG_RNG_FALLBACK, DREG_JIT_FALLBACK, DREG_BEGIN_PIXEL, DREG_RING_LOAD, DREG_ROUND, DREG_MISS,
-  DREG_N
+  DREG_HINT_FALLBACK, DREG_N
 };
 
 // Division by a launch constant d >= 1 of numerators n < 2^31 (Granlund & Montgomery 1994, Thm 4.2 with N = 31):
@@ -106,6 +106,14 @@ struct KParams {
   uint32_t* tile_cost;         // probe: [k] cost (rp_device.h WORK_*: node visits, primitive tests, rays)
                                // summed over the tile's probed samples, [TILE_SORT_MAX + k] the costliest
                                // probed sample (zeroed by the caller)
+  // Coherent primary pass (launch_primary; camera lens_radius == 0 only): per shard slot and sample (slot * spp + the
+  // sample's index in the pixel) the camera ray's closest primitive, -1 = none.  The render kernel reads it at every
+  // camera sample instead of traversing (NULL = off: camera rays traverse in the path loop).
+  int32_t* prim_hint;
+  uint32_t prim_quads_x;       // primary pass: 2 x 2 pixel quads per tile row, ceil(tw / 2)
+  uint32_t prim_items_tile;    // primary pass: work items (64 camera rays: a quad x 16 samples) per tile
+  uint32_t prim_sgroups;       // primary pass: 16-sample groups per pixel, ceil(spp / 16)
+  Div32 dv_sps;                // primary pass: make_div32(spp_batch)
 };
 
 // Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last
@@ -135,8 +143,14 @@ int launch_learn_costs(const uint32_t* sum, const uint32_t* max, uint32_t rank_s
 enum { SPP_BATCH = 32 };
 
 // Unit-queue words of a workspace: group g's counter at g * QUEUE_STRIDE (own 128 B line), the probe's at
-// QUEUE_PROBE.
-enum { QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_STRIDE, QUEUE_WORDS = QUEUE_PROBE + 1 };
+// QUEUE_PROBE, the primary pass's group g at QUEUE_PRIM + g * QUEUE_STRIDE.
+enum {
+  QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_STRIDE, QUEUE_PRIM = QUEUE_PROBE + QUEUE_STRIDE,
+  QUEUE_WORDS = QUEUE_PRIM + QUEUE_GROUPS * QUEUE_STRIDE
+};
+// Coherent primary pass: a work item is 64 camera rays -- a 2 x 2 pixel quad of one shard tile x PRIM_SAMPLES
+// consecutive samples of each pixel (lane = 16 x quad pixel + sample); items of shard tile k go to queue k mod 8.
+enum { PRIM_SAMPLES = 16 };
 
 // Counter block layout (RP_COUNTERS_LEN x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_N = 4 };
@@ -149,6 +163,11 @@ enum { GATHER_CTR = 8, GATHER_CTR_HASH = 4 };
 // `queue` (workspace-owned) must have been zeroed on the same stream.  Returns a hipError_t as int.
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
                   uint32_t* queue, int grid, void* stream);
+
+// Coherent primary pass over the shard (KParams::prim_hint, lens_radius == 0): every camera ray of the frame traced in
+// waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 jittered samples), its closest primitive written to prim_hint.
+// `queue` = the workspace's QUEUE_PRIM counters, zeroed on the same stream; grid <= the render grid (the spill runs).
+int launch_primary(const KScene& s, const KParams& p, uint64_t* counters, uint32_t* queue, int grid, void* stream);
 
 // Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (costliest sample, mean cost per probed
 // pixel), log-quantized, ties by tile index, into order[] (shard tile indices).  One block.

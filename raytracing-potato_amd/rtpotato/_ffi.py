@@ -33,9 +33,11 @@ RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 RP_COLLAPSE_AUTO, RP_COLLAPSE_GREEDY, RP_COLLAPSE_SAH = 0, 1, 2
 RP_LAYOUT_AUTO, RP_LAYOUT_DFS, RP_LAYOUT_DFS_LINE = 0, 1, 2
+RP_PRIMARY_AUTO, RP_PRIMARY_OFF = 0, 1
+RP_FRAME_PRIMARY_PASS, RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED = 1, 2, 4
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
-RP_ABI_VERSION = 7
+RP_ABI_VERSION = 8
 
 
 class rp_hittable(Structure):
@@ -95,7 +97,7 @@ class rp_scene_options(Structure):
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
                 ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
                 ("unit_queues", c_uint32), ("queue_chunk", c_uint32), ("debug_stack_depth", c_uint32),
-                ("collapse", c_uint32), ("node_layout", c_uint32)]
+                ("collapse", c_uint32), ("node_layout", c_uint32), ("primary", c_uint32), ("reserved", c_uint32)]
 
 
 class rp_stats(Structure):
@@ -131,7 +133,8 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_scene_create_ex", "rp_workspace_reserve", "rp_comm_unique_id", "rp_comm_create", "rp_comm_destroy",
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
               "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
-              "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times"]
+              "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times",
+              "rp_workspace_frame_info"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_selfcheck_ex", "rph_bvh_traversal_stats_ex", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64", "rph_make_div32"]
@@ -207,6 +210,7 @@ def rp() -> ctypes.CDLL:
     lib.rp_workspace_tile_map.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_scene_build_times.argtypes = [c_void_p, c_void_p, c_uint32]
     lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
+    lib.rp_workspace_frame_info.argtypes = [c_void_p, c_void_p, POINTER(c_uint32)]
     lib.rp_workspace_set_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_frame_assemble_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32, c_void_p,
                                          c_void_p]

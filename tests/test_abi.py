@@ -42,7 +42,7 @@ def test_librp_host_exports_all_rp_host_h_symbols():
 def test_librp_loads_and_reports_without_gpu():
     from rtpotato import _ffi as F
     L = F.rp()
-    assert L.rp_abi_version() == F.RP_ABI_VERSION == 7
+    assert L.rp_abi_version() == F.RP_ABI_VERSION == 8
     n = ctypes.c_int(-1)
     rc = L.rp_device_count(ctypes.byref(n))
     assert rc in (F.RP_OK, F.RP_ENODEV) and n.value >= 0

@@ -1,0 +1,105 @@
+"""The coherent primary pass (rp_scene_options.primary, rp_kernel.hip primary_kernel).
+
+With lens_radius = 0 a camera ray depends only on its jitter words (render.rs:36-44,74-82), so the library traces every
+camera ray of the frame first, in waves of 64 neighbouring rays, and the path loop starts each sample from that closest
+hit.  The closest hit does not depend on the order rays are traced (up to exact-t ties), so the frame
+must be the path-loop frame: same rays, same samples, pixels equal -- and the oracle's.  Cases: both node formats and
+the 8-wide one, the spilled stack, odd tiles and frame sizes, spp not a multiple of the pass's 16 samples, RNG streams
+whose length is not a multiple of 4 (the pass's per-lane ChaCha path instead of the quad one), multi-batch frames,
+shards of the balanced plan, and lens cameras (no pass).
+"""
+import numpy as np
+import pytest
+from dataclasses import replace
+
+from parity import assert_parity, compare, oracle_render, shard_mask
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(name, w, h, spp, **kw):
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.CATALOGUE[name](**kw), w, h)
+    return sc, RenderParams(w, h, spp, 8, scenes.DEFAULT_SEED)
+
+
+def _render(gpu, sc, p, **opt):
+    with gpu.DeviceScene(sc, options=opt or None) as ds:
+        rgb, fg, st = ds.render(p, foreground=True)
+        flags = ds.frame_info()
+    return rgb, fg, st, flags
+
+
+def _on_off(gpu, sc, p, **opt):
+    """The frame with the pass (AUTO) and without it (OFF): identical counts, pixels to the parity bar (bitwise but for
+    exact-t ties), foreground identical."""
+    from rtpotato import _ffi as F
+    on, fg_on, st_on, f_on = _render(gpu, sc, p, **opt)
+    off, fg_off, st_off, f_off = _render(gpu, sc, p, primary="off", **opt)
+    assert f_on & F.RP_FRAME_PRIMARY_PASS and not f_off & F.RP_FRAME_PRIMARY_PASS, (f_on, f_off)
+    assert (st_on["rays"], st_on["samples"], st_on["pixels"]) == (st_off["rays"], st_off["samples"], st_off["pixels"])
+    m = shard_mask(p)
+    c = compare(on, off, m)
+    assert_parity(c, min_exact=0.9999)
+    assert np.array_equal(fg_on[m], fg_off[m])
+    return on, st_on
+
+
+@pytest.mark.parametrize("name", ["bunny_full", "variants", "variants_sky", "earth", "one_triangle", "glass_bunny",
+                                  "two_balls"])
+def test_primary_pass_equals_path_loop(gpu, name):
+    sc, p = _scene(name, 64, 36, 8)
+    _on_off(gpu, sc, p)
+
+
+@pytest.mark.parametrize("fmt", ["f32", "q8", "w8"])
+def test_primary_pass_node_formats_and_spill(gpu, fmt):
+    """Every node format, with the stack split into LDS + a global spill run (lds_depth 8)."""
+    sc, p = _scene("bunny_full", 80, 48, 12)
+    _on_off(gpu, sc, p, node_format=fmt)
+    _on_off(gpu, sc, p, node_format=fmt, lds_depth=8)
+
+
+def test_primary_pass_against_oracle_odd_shapes(gpu):
+    """Odd frame and tile sizes (quads cut by tile and frame edges), spp 21 (a partial 16-sample group), streams of 7
+    samples (not a multiple of 4: the per-lane ChaCha path) and of 12 (quad path, batches not 16-aligned), a shard of
+    a balanced 3-way frame: against the oracle, exact ray counts."""
+    from rtpotato import _ffi as F
+    sc, p0 = _scene("bunny_full", 53, 37, 21)
+    for sps in (7, 12, 0):
+        for tw, th in ((7, 5), (32, 32)):
+            p = replace(p0, samples_per_stream=sps, tile_w=tw, tile_h=th)
+            rgb, fg, st, flags = _render(gpu, sc, p)
+            assert flags & F.RP_FRAME_PRIMARY_PASS
+            ref, ref_fg, ctr = oracle_render(sc, p, threads=8, foreground=True)
+            m = shard_mask(p)
+            assert_parity(compare(rgb, ref, m))
+            assert (st["rays"], st["samples"]) == (ctr["rays"], ctr["samples"]), (sps, tw, st, ctr)
+            assert np.array_equal(fg[m], ref_fg[m])
+    p = replace(p0, shard=1, num_shards=3, tile_w=8, tile_h=8)
+    rgb, _, st, flags = _render(gpu, sc, p)
+    assert flags & F.RP_FRAME_PRIMARY_PASS
+    ref, _, ctr = oracle_render(sc, p, threads=8)
+    assert_parity(compare(rgb, ref, shard_mask(p)))
+    assert st["rays"] == ctr["rays"]
+
+
+def test_primary_pass_skipped_for_lens_cameras(gpu):
+    """three_balls has lens_radius 0.1: camera rays depend on the main stream's UnitDisk draw, so no pass runs; the frame
+    equals the oracle's."""
+    from rtpotato import _ffi as F
+    sc, p = _scene("three_balls", 48, 32, 4)
+    assert sc.camera.lens_radius > 0
+    rgb, _, st, flags = _render(gpu, sc, p)
+    assert not flags & F.RP_FRAME_PRIMARY_PASS
+    ref, _, ctr = oracle_render(sc, p, threads=8)
+    assert_parity(compare(rgb, ref))
+    assert st["rays"] == ctr["rays"]
+
+
+def test_primary_pass_c3_tile_full_spp(gpu):
+    """C3's scene at its full 256 spp on a 96 x 64 crop, default streams and one stream per pixel: pass on = off."""
+    sc, p = _scene("bunny_full", 96, 64, 256)
+    _on_off(gpu, sc, p)
+    _on_off(gpu, sc, replace(p, samples_per_stream=256))
