@@ -231,13 +231,14 @@ enum { RP_COLLAPSE_AUTO = 0, RP_COLLAPSE_GREEDY = 1, RP_COLLAPSE_SAH = 2 };
  * line (64-B quantized nodes: a pad slot after odd families; f32 nodes are one line each, so the same as DFS).  Speed
  * only: the image never depends on it. */
 enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
-/* rp_scene_options.primary (ABI v8): the coherent primary pass.  AUTO: when the camera's lens_radius is 0 (a camera
+/* rp_scene_options.primary (ABI v8): the coherent primary pass.  ON: when the camera's lens_radius is 0 (a camera
  * ray's direction then depends only on its jitter, render.rs:36-44,74-82) and the workspace is reserved for it
  * (rp_workspace_reserve: 4 bytes per pixel and sample of the shard), every camera ray of the frame is traced first in
  * waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 samples), and the path loop starts each sample from that
  * closest hit instead of traversing: the same image (the closest hit does not depend on the order rays are traced,
- * up to exact-t ties).  OFF: camera rays traverse in the path loop. */
-enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1 };
+ * up to exact-t ties).  OFF: camera rays traverse in the path loop.  AUTO: the library's choice --
+ * ON where it measured faster, else OFF. */
+enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1, RP_PRIMARY_ON = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles); PLOC */

@@ -389,7 +389,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
     return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
   if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
   if (o.node_layout > RP_LAYOUT_DFS_LINE) return fail(RP_EINVAL, "options.node_layout must be RP_LAYOUT_*");
-  if (o.primary > RP_PRIMARY_OFF) return fail(RP_EINVAL, "options.primary must be RP_PRIMARY_*");
+  if (o.primary > RP_PRIMARY_ON) return fail(RP_EINVAL, "options.primary must be RP_PRIMARY_*");
   if (o.reserved != 0) return fail(RP_EINVAL, "options.reserved must be 0");
   return RP_OK;
 }
@@ -398,6 +398,14 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
 uint64_t stage_slots(const Tiling& t) {
   const uint32_t n0 = t.n_tiles ? (t.n_tiles + t.shards - 1) / t.shards : 0;
   return (uint64_t)n0 * t.tw * t.th;
+}
+
+// The coherent primary pass runs for this scene (rp.h RP_PRIMARY_*): ON, megakernel engine.  AUTO is OFF: measured
+// against the path loop's own camera-ray traversal it lost on both configs (C3 226.9 vs 205.7 ms: the render kernel's
+// time did not move without its camera rays; C5 1,987 vs 1,528 ms: the render kernel -27 %, the pass +57 %), DESIGN.md
+// 4.8, profiles/r5/c3_c5_primary_pass_ab.json.
+bool primary_on(const rp_scene* s) {
+  return s->opt.primary == RP_PRIMARY_ON && s->opt.engine == RP_ENGINE_MEGAKERNEL;
 }
 
 // Grow a pair of device buffers (a, b) of na, nb elements per unit to `units` units (synchronous).
@@ -426,7 +434,7 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
   // the coherent primary pass's hints: 4 bytes per shard slot and sample (C3 2.1 GB, C5 17 GB of the 288 GB HBM); a
   // frame past PRIM_HINT_MAX_BYTES renders without the pass
   const uint64_t hints = t.n_slots * p->spp;
-  if (s->opt.primary != RP_PRIMARY_OFF && s->opt.engine == RP_ENGINE_MEGAKERNEL && hints > w->hint_cap &&
+  if (primary_on(s) && hints > w->hint_cap &&
       hints * sizeof(int32_t) <= PRIM_HINT_MAX_BYTES) {
     dfree(w->d_hint);
     w->d_hint = nullptr;
@@ -847,8 +855,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // 64 before the path loop, which then starts every sample at its closest hit.  Needs the workspace's hint buffer
   // (rp_workspace_reserve); without it, or with a lens, camera rays traverse in the path loop.
   const uint64_t n_hints = t.n_slots * p->spp;
-  if (s->opt.primary != RP_PRIMARY_OFF && s->opt.engine == RP_ENGINE_MEGAKERNEL && cam->lens_radius == 0.0 &&
-      w->d_hint && n_hints <= w->hint_cap) {
+  if (primary_on(s) && cam->lens_radius == 0.0 && w->d_hint && n_hints <= w->hint_cap) {
     kp.prim_quads_x = (t.tw + 1) / 2;
     kp.prim_sgroups = (p->spp + rpk::PRIM_SAMPLES - 1) / rpk::PRIM_SAMPLES;
     const uint64_t per_tile = (uint64_t)kp.prim_quads_x * ((t.th + 1) / 2) * kp.prim_sgroups;

@@ -39,7 +39,10 @@ enum { RENDER_BLOCK = 64 };
 // lane primitive tests.
 // [352 + b] units whose duration (100 MHz ticks) has floor(log2) = b + DIAG_DUR_LOG0 (clamped to 0..23), [376 + b]
 // their rays summed.
-enum { DIAG_N = 400, DIAG_DUR = 352, DIAG_DUR_N = 24, DIAG_DUR_LOG0 = 10 };
+// [400 + i] the coherent primary pass (primary_kernel): items, rays, lane node visits, lane primitive tests, wave
+// trav_step calls, wave-cycles in ray setup (key, ChaCha, camera), in traversal and in fetch + store, and the summed
+// per-item maximum of a lane's node visits.
+enum { DIAG_N = 416, DIAG_DUR = 352, DIAG_DUR_N = 24, DIAG_DUR_LOG0 = 10, DIAG_PRIM = 400 };
 // Cycle regions (RPK_DIAG builds), from DIAG_N index DIAG_CYC: wave-cycles spent executing each code region
 enum { DIAG_CYC = 320 };
 enum {

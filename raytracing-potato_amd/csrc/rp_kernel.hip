@@ -396,6 +396,8 @@ __global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
   bool overflow = false;
   const uint32_t G = QUEUE_GROUPS, home = blockIdx.x % G;
   uint32_t tries = 0;
+  DIAG(uint64_t d_items = 0, d_rays = 0, d_steps = 0, d_maxv = 0, c_setup = 0, c_trav = 0, c_rest = 0;
+       TravDiag td; uint64_t t_prev = stamp();)
   for (;;) {
     KArgsPtr A = kargs();
     uint32_t g = home + tries;
@@ -441,6 +443,8 @@ __global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
     const double jv = ((double)pj + words_f64(jw.z, jw.w)) / (double)A->P.H;
     V3 o, d;
     camera_dir(A, ju, jv, 0.0, 0.0, o, d);
+    DIAG(const uint32_t v0 = td.visits;)
+    DIAG({ const uint64_t t = stamp(); c_setup += t - t_prev; t_prev = t; })
     const KScene S = load_scene(A);
     const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + lane) * (S.stack_depth - S.lds_depth) : 0u;
     TravState ts;
@@ -450,16 +454,44 @@ __global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
     bool done = !valid || trav_done(ts);
     while (__ballot(!done) != 0) {
       if (!done) {
+        DIAG(d_steps += lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()) ? 1u : 0u;)
+#ifdef RPK_DIAG
+        trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
+#else
         trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+#endif
         done = trav_done(ts);
       }
     }
+    DIAG({ const uint64_t t = stamp(); c_trav += t - t_prev; t_prev = t; })
+    DIAG(d_items++; d_rays += valid ? 1u : 0u;
+         uint32_t mv = td.visits - v0;
+         for (int off = 32; off >= 1; off >>= 1) mv = max(mv, (uint32_t)__shfl_xor(mv, off));
+         d_maxv += mv;)
     if (valid) {
       const uint64_t slot = (uint64_t)k * tw * th + (uint64_t)lj * tw + li;
       A->P.prim_hint[slot * A->P.spp + s] = ts.bestp;
     }
   }
   if (overflow) atomicOr(&kargs()->ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
+#ifdef RPK_DIAG
+  {
+    const uint64_t t = stamp();
+    c_rest += t - t_prev;
+    unsigned long long* dg = kargs()->diag + DIAG_PRIM;
+    atomicAdd(&dg[1], (unsigned long long)d_rays);
+    atomicAdd(&dg[2], (unsigned long long)td.visits);
+    atomicAdd(&dg[3], (unsigned long long)td.tests);
+    atomicAdd(&dg[4], (unsigned long long)d_steps);
+    if (lane == 0) {
+      atomicAdd(&dg[0], (unsigned long long)d_items);
+      atomicAdd(&dg[5], (unsigned long long)c_setup);
+      atomicAdd(&dg[6], (unsigned long long)c_trav);
+      atomicAdd(&dg[7], (unsigned long long)c_rest);
+      atomicAdd(&dg[8], (unsigned long long)d_maxv);
+    }
+  }
+#endif
 }
 
 int launch_primary(const KScene& s, const KParams& p, uint64_t* counters, uint32_t* queue, int grid, void* stream) {

@@ -33,7 +33,7 @@ RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 RP_COLLAPSE_AUTO, RP_COLLAPSE_GREEDY, RP_COLLAPSE_SAH = 0, 1, 2
 RP_LAYOUT_AUTO, RP_LAYOUT_DFS, RP_LAYOUT_DFS_LINE = 0, 1, 2
-RP_PRIMARY_AUTO, RP_PRIMARY_OFF = 0, 1
+RP_PRIMARY_AUTO, RP_PRIMARY_OFF, RP_PRIMARY_ON = 0, 1, 2
 RP_FRAME_PRIMARY_PASS, RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED = 1, 2, 4
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2

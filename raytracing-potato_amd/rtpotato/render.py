@@ -19,7 +19,7 @@ def scene_options(**kw) -> F.rp_scene_options:
     self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
     node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
     unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*), collapse ("auto" | "greedy" | "sah" or
-    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), primary ("auto" | "off" or RP_PRIMARY_*)."""
+    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), primary ("auto" | "off" | "on" or RP_PRIMARY_*)."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
@@ -41,7 +41,7 @@ def scene_options(**kw) -> F.rp_scene_options:
         if k == "node_layout" and isinstance(v, str):
             v = {"auto": F.RP_LAYOUT_AUTO, "dfs": F.RP_LAYOUT_DFS, "dfs_line": F.RP_LAYOUT_DFS_LINE}[v]
         if k == "primary" and isinstance(v, str):
-            v = {"auto": F.RP_PRIMARY_AUTO, "off": F.RP_PRIMARY_OFF}[v]
+            v = {"auto": F.RP_PRIMARY_AUTO, "off": F.RP_PRIMARY_OFF, "on": F.RP_PRIMARY_ON}[v]
         if not hasattr(o, k):
             raise KeyError(f"unknown scene option {k!r}")
         setattr(o, k, v)

@@ -32,10 +32,10 @@ def _render(gpu, sc, p, **opt):
 
 
 def _on_off(gpu, sc, p, **opt):
-    """The frame with the pass (AUTO) and without it (OFF): identical counts, pixels to the parity bar (bitwise but for
+    """The frame with the pass (ON) and without it (OFF): identical counts, pixels to the parity bar (bitwise but for
     exact-t ties), foreground identical."""
     from rtpotato import _ffi as F
-    on, fg_on, st_on, f_on = _render(gpu, sc, p, **opt)
+    on, fg_on, st_on, f_on = _render(gpu, sc, p, primary="on", **opt)
     off, fg_off, st_off, f_off = _render(gpu, sc, p, primary="off", **opt)
     assert f_on & F.RP_FRAME_PRIMARY_PASS and not f_off & F.RP_FRAME_PRIMARY_PASS, (f_on, f_off)
     assert (st_on["rays"], st_on["samples"], st_on["pixels"]) == (st_off["rays"], st_off["samples"], st_off["pixels"])
@@ -70,7 +70,7 @@ def test_primary_pass_against_oracle_odd_shapes(gpu):
     for sps in (7, 12, 0):
         for tw, th in ((7, 5), (32, 32)):
             p = replace(p0, samples_per_stream=sps, tile_w=tw, tile_h=th)
-            rgb, fg, st, flags = _render(gpu, sc, p)
+            rgb, fg, st, flags = _render(gpu, sc, p, primary="on")
             assert flags & F.RP_FRAME_PRIMARY_PASS
             ref, ref_fg, ctr = oracle_render(sc, p, threads=8, foreground=True)
             m = shard_mask(p)
@@ -78,7 +78,7 @@ def test_primary_pass_against_oracle_odd_shapes(gpu):
             assert (st["rays"], st["samples"]) == (ctr["rays"], ctr["samples"]), (sps, tw, st, ctr)
             assert np.array_equal(fg[m], ref_fg[m])
     p = replace(p0, shard=1, num_shards=3, tile_w=8, tile_h=8)
-    rgb, _, st, flags = _render(gpu, sc, p)
+    rgb, _, st, flags = _render(gpu, sc, p, primary="on")
     assert flags & F.RP_FRAME_PRIMARY_PASS
     ref, _, ctr = oracle_render(sc, p, threads=8)
     assert_parity(compare(rgb, ref, shard_mask(p)))
@@ -91,11 +91,19 @@ def test_primary_pass_skipped_for_lens_cameras(gpu):
     from rtpotato import _ffi as F
     sc, p = _scene("three_balls", 48, 32, 4)
     assert sc.camera.lens_radius > 0
-    rgb, _, st, flags = _render(gpu, sc, p)
+    rgb, _, st, flags = _render(gpu, sc, p, primary="on")
     assert not flags & F.RP_FRAME_PRIMARY_PASS
     ref, _, ctr = oracle_render(sc, p, threads=8)
     assert_parity(compare(rgb, ref))
     assert st["rays"] == ctr["rays"]
+
+
+def test_primary_pass_auto_is_off(gpu):
+    """AUTO resolves to OFF (the pass lost on both configs): no pass, no hint buffer use."""
+    from rtpotato import _ffi as F
+    sc, p = _scene("bunny_full", 32, 32, 4)
+    _, _, _, flags = _render(gpu, sc, p)
+    assert not flags & F.RP_FRAME_PRIMARY_PASS
 
 
 def test_primary_pass_c3_tile_full_spp(gpu):

@@ -31,7 +31,7 @@ def main():
         opts[k] = float(v) if k == "cost_traverse" else (v if not v.lstrip("-").isdigit() else int(v))
     ds = DeviceScene(scene, options=opts)
     ds.render(replace(params, spp=1))  # warm
-    NDIAG = 400  # rp_kernel.h DIAG_N
+    NDIAG = 416  # rp_kernel.h DIAG_N
     buf = (ctypes.c_uint64 * NDIAG)()
     F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
     _, _, st = ds.render(params)
@@ -76,6 +76,18 @@ def main():
     out["unit_durations"] = [{"ms_from": round(2 ** (10 + b) / 1e5, 3), "ms_to": round(2 ** (11 + b) / 1e5, 3),
                               "units": d[352 + b], "rays_per_unit": round(d[376 + b] / max(1, d[352 + b]), 1)}
                              for b in range(24) if d[352 + b]]
+    pd = d[400:409]  # rp_kernel.h DIAG_PRIM: the coherent primary pass
+    if pd[0]:
+        cyc = pd[5] + pd[6] + pd[7]
+        out["primary_pass"] = {
+            "items": pd[0], "rays": pd[1], "visits_per_ray": round(pd[2] / max(1, pd[1]), 3),
+            "prim_tests_per_ray": round(pd[3] / max(1, pd[1]), 3),
+            "trav_steps_per_item": round(pd[4] / pd[0], 2),
+            "max_lane_visits_per_item": round(pd[8] / pd[0], 2),
+            "visit_lane_util": round(pd[2] / max(1, 64 * pd[8]), 4),
+            "wave_cycles_per_item": round(cyc / pd[0], 1),
+            "cycle_share": {"setup": round(pd[5] / cyc, 4), "traverse": round(pd[6] / cyc, 4),
+                            "fetch_store": round(pd[7] / cyc, 4)}}
     print(json.dumps(out, indent=1))
 
 

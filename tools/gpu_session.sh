@@ -4,7 +4,7 @@
 #   TAG=r4a STEPS="tests bench_C3 trace_C3 pmc_C3" tools/gpu_session.sh
 #
 # STEPS, run in order, each under its own time limit; the first failure (a crash, abort or time limit) ends the session:
-#   tests              pytest -m gpu (PYTEST_ARGS, e.g. "-k c3 -m 'gpu and not slow'")
+#   tests              pytest -m gpu (TESTS_K: a -k expression, may hold spaces; PYTEST_ARGS: more words)
 #   bench_<CFG>        bench.py --config CFG (BENCH_ARGS appended; the CPU baseline only for C3 unless NO_CPU=1)
 #   shards_<CFG>[.<L>] tools/shard_scaling.py: every shard of SHARD_NS (default 1,8) on one GPU, SHARD_REPS reps,
 #                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run), library SHARD_LIB_<L> (default main)
@@ -50,7 +50,7 @@ for s in ${STEPS:-tests}; do
       step tests
       made gpurun_out/${TAG}_tests.log "pytest tests -m gpu ${PYTEST_ARGS:-}"
       timeout -k 10 ${TESTS_LIMIT:-1200} python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread \
-        -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/${TAG}_tests.log 2>&1 || { step "tests failed"; exit 1; } ;;
+        -p no:cacheprovider ${TESTS_K:+-k "$TESTS_K"} ${PYTEST_ARGS:-} > gpurun_out/${TAG}_tests.log 2>&1 || { step "tests failed"; exit 1; } ;;
     bench_*)
       cfg=${s#bench_}; read st wu <<< "$(frames $cfg)"
       cpu=""; { [ $cfg != C3 ] || [ -n "${NO_CPU:-}" ]; } && cpu=--no-cpu-baseline
