@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--shards", type=int, default=1, help="render shard 0 of N (per-rank work of an N-GPU run)")
+    ap.add_argument("--sps", type=int, default=0, help="samples_per_stream (the RNG contract; 0 = 32, >= spp: one "
+                                                       "stream per pixel)")
     ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value")
     a = ap.parse_args()
     os.environ.setdefault("RP_LIB", os.path.join(REPO, "raytracing-potato_amd", "lib", "librp_diag.so"))
@@ -24,7 +26,7 @@ def main():
     from rtpotato import _ffi as F, scenes
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
-    params = replace(params, spp=a.spp, shard=0, num_shards=a.shards)
+    params = replace(params, spp=a.spp, shard=0, num_shards=a.shards, samples_per_stream=a.sps)
     opts = {}
     for kv in a.opt:
         k, v = kv.split("=", 1)
@@ -41,7 +43,7 @@ def main():
     tot = sum(ph)
     iters, active, trips, visits, tests = d[5], d[6], d[7], d[8], d[9]
     out = {
-        "config": a.config, "spp": a.spp, "rays": st["rays"], "seconds": st["seconds"],
+        "config": a.config, "spp": a.spp, "samples_per_stream": a.sps or 32, "rays": st["rays"], "seconds": st["seconds"],
         "phase_share": {k: round(v / tot, 4) for k, v in zip(["fetch", "rng_refill", "traverse", "shade", "tail"], ph)},
         "wave_iterations": iters, "lanes_active_at_traverse": round(active / max(1, iters) / 64, 4),
         "visits_per_ray": round(visits / st["rays"], 3), "prim_tests_per_ray": round(tests / st["rays"], 3),

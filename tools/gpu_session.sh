@@ -77,8 +77,8 @@ for s in ${STEPS:-tests}; do
     diag_*)
       cfg=${s#diag_}
       step "diag $cfg"
-      made gpurun_out/${TAG}_${cfg}_diag.json "RP_LIB=raytracing-potato_amd/lib/librp_diag.so python3 tools/diag.py --config $cfg --spp 256"
-      RP_LIB=raytracing-potato_amd/lib/librp_diag.so timeout -k 10 300 python3 tools/diag.py --config $cfg --spp 256 \
+      made gpurun_out/${TAG}_${cfg}_diag.json "RP_LIB=raytracing-potato_amd/lib/librp_diag.so python3 tools/diag.py --config $cfg --spp 256 ${DIAG_ARGS:-}"
+      RP_LIB=raytracing-potato_amd/lib/librp_diag.so timeout -k 10 300 python3 tools/diag.py --config $cfg --spp 256 ${DIAG_ARGS:-} \
         > gpurun_out/${TAG}_${cfg}_diag.json 2> gpurun_out/${TAG}_${cfg}_diag.err || exit 1 ;;
     trace_*)
       cfg=${s#trace_}; read st wu <<< "$(frames $cfg)"
