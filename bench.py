@@ -243,7 +243,7 @@ def main():
     options = {}
     for kv in args.opt:
         k, v = kv.split("=", 1)
-        options[k] = float(v) if k == "cost_traverse" else (v if k in ("builder", "engine", "node_format", "tile_order", "unit_queues", "collapse", "node_layout", "primary") else int(v))
+        options[k] = float(v) if k == "cost_traverse" else (v if k in ("builder", "engine", "node_format", "tile_order", "unit_queues", "collapse", "node_layout", "primary", "unit_order") else int(v))
     scene, params = scenes.config_scene(args.config)
     if args.spp:
         params = replace(params, spp=args.spp)

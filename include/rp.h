@@ -239,6 +239,13 @@ enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
  * up to exact-t ties).  OFF: camera rays traverse in the path loop.  AUTO: the library's choice --
  * ON where it measured faster, else OFF. */
 enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1, RP_PRIMARY_ON = 2 };
+/* rp_scene_options.unit_order (ABI v8): the order the unit queues hand out a shard's (pixel, sample stream) units.
+ * TILES: tile by tile (tile_order), a tile's pixels row-major.  LEARNED: every render stores each unit's duration,
+ * and the next frame of the same shape on the same workspace hands out its units longest first (in log-spaced
+ * buckets that keep shard order inside; a frame ends with its longest unit), on one device or interleaved shards
+ * (a balanced plan's tiles may move between frames: those frames keep TILES).  AUTO = LEARNED where measured faster
+ * (DESIGN.md 4.3).  Results never depend on it. */
+enum { RP_UNITS_AUTO = 0, RP_UNITS_TILES = 1, RP_UNITS_LEARNED = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
                                build, ~24 % slower traversal on 10 M triangles); PLOC */
@@ -265,7 +272,7 @@ typedef struct rp_scene_options {
   uint32_t collapse;        /* RP_COLLAPSE_*: the 4-wide collapse of the host-built tree (ABI v6) */
   uint32_t node_layout;     /* RP_LAYOUT_*: node order of a device-built (PLOC) tree (ABI v7) */
   uint32_t primary;         /* RP_PRIMARY_*: the coherent primary pass (ABI v8) */
-  uint32_t reserved;        /* 0 */
+  uint32_t unit_order;      /* RP_UNITS_*: tile order or the learned per-unit order (ABI v8) */
 } rp_scene_options;
 
 typedef struct rp_stats {
@@ -366,7 +373,8 @@ int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const 
 enum {
   RP_FRAME_PRIMARY_PASS = 1,  /* the coherent primary pass traced the camera rays (rp_scene_options.primary) */
   RP_FRAME_LEARNED_ORDER = 2, /* tiles ordered / dealt from the workspace's learned cost table */
-  RP_FRAME_PROBED = 4         /* a cost probe launch ran */
+  RP_FRAME_PROBED = 4,        /* a cost probe launch ran */
+  RP_FRAME_UNIT_ORDER = 8     /* units handed out in the learned per-unit order (rp_scene_options.unit_order) */
 };
 int rp_workspace_frame_info(const rp_scene* scene, const rp_workspace* workspace, uint32_t* flags);
 /* The deal order of params' frame (one entry per frame tile; shard s's k-th tile is tile_map[s + k*num_shards]):

@@ -121,6 +121,17 @@ struct rp_workspace {
   uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
   int32_t* d_hint = nullptr;         // the coherent primary pass's closest primitive per shard slot and sample
   uint64_t hint_cap = 0;             // capacity of d_hint in entries
+  // the learned per-unit order (rp_sched.hip): each unit's duration in the last render, the sort keys (two buffers),
+  // the radix sort's scratch and the order; ucost_geom = the frame shape the durations belong to
+  uint32_t* d_ucost = nullptr;
+  uint64_t* d_ukey = nullptr;
+  uint64_t* d_ukey2 = nullptr;
+  uint32_t* d_uorder = nullptr;
+  void* d_usort = nullptr;
+  size_t usort_bytes = 0;
+  uint64_t ucost_cap = 0;
+  bool ucost_valid = false;
+  uint32_t ucost_geom[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   double* d_gs_rgb = nullptr;        // gather staging: this rank's shard, padded to the stride (3 f64 / slot)
   uint32_t* d_gs_bgra = nullptr;     //   ... its to_srgb_u8 bytes (1 word / slot)
   double* d_gather_rgb = nullptr;    //   all ranks' shards (nranks x stride x 3 f64)
@@ -209,7 +220,8 @@ void ws_release(rp_workspace* w) {
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
                   (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
                   (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0,
-                  (void*)w->d_hint})
+                  (void*)w->d_hint, (void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder,
+                  w->d_usort})
     dfree(p);
   if (w->ev_gathered) (void)hipEventDestroy(w->ev_gathered);
   *w = rp_workspace{};
@@ -390,7 +402,7 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
   if (o.node_layout > RP_LAYOUT_DFS_LINE) return fail(RP_EINVAL, "options.node_layout must be RP_LAYOUT_*");
   if (o.primary > RP_PRIMARY_ON) return fail(RP_EINVAL, "options.primary must be RP_PRIMARY_*");
-  if (o.reserved != 0) return fail(RP_EINVAL, "options.reserved must be 0");
+  if (o.unit_order > RP_UNITS_LEARNED) return fail(RP_EINVAL, "options.unit_order must be RP_UNITS_*");
   return RP_OK;
 }
 
@@ -398,6 +410,12 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
 uint64_t stage_slots(const Tiling& t) {
   const uint32_t n0 = t.n_tiles ? (t.n_tiles + t.shards - 1) / t.shards : 0;
   return (uint64_t)n0 * t.tw * t.th;
+}
+
+// The learned per-unit order (rp.h RP_UNITS_*) is kept for this scene: LEARNED, or AUTO, megakernel engine.
+bool units_on(const rp_scene* s) {
+  return (s->opt.unit_order == RP_UNITS_LEARNED || s->opt.unit_order == RP_UNITS_AUTO) &&
+         s->opt.engine == RP_ENGINE_MEGAKERNEL;
 }
 
 // The coherent primary pass runs for this scene (rp.h RP_PRIMARY_*): ON, megakernel engine.  AUTO is OFF: measured
@@ -441,6 +459,22 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
     w->hint_cap = 0;
     if (!dalloc(&w->d_hint, hints)) return fail(RP_ENOMEM, "hipMalloc primary-pass hints");
     w->hint_cap = hints;
+  }
+  // the learned per-unit order: 4 + 8 + 8 + 4 bytes per unit and the sort's scratch (C3: 16.6 M units, 400 MB)
+  const uint64_t n_units = t.n_slots * t.nbatch;
+  if (units_on(s) && n_units > w->ucost_cap && n_units < (1ull << 31)) {
+    for (void* q : {(void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder, w->d_usort}) dfree(q);
+    w->d_ucost = w->d_uorder = nullptr;
+    w->d_ukey = w->d_ukey2 = nullptr;
+    w->d_usort = nullptr;
+    w->ucost_cap = 0;
+    w->ucost_valid = false;
+    w->usort_bytes = rpk::unit_order_scratch_bytes(n_units);
+    if (!w->usort_bytes || !dalloc(&w->d_ucost, n_units) || !dalloc(&w->d_ukey, n_units) || !dalloc(&w->d_ukey2, n_units) ||
+        !dalloc(&w->d_uorder, n_units) || !dalloc(reinterpret_cast<uint8_t**>(&w->d_usort), w->usort_bytes))
+      return fail(RP_ENOMEM, "hipMalloc per-unit order");
+    RP_HIP(hipMemset(w->d_ucost, 0, sizeof(uint32_t) * n_units));
+    w->ucost_cap = n_units;
   }
   if (gather) {
     const uint64_t stride = stage_slots(t);
@@ -871,6 +905,25 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
       w->frame_flags |= RP_FRAME_PRIMARY_PASS;
     }
   }
+  // The learned per-unit order (rp.h RP_UNITS_LEARNED): units longest first by the last render's durations on this
+  // workspace -- same frame shape and shard, and not a balanced plan over several ranks (its tiles may move) -- and
+  // every render stores its units' durations for the next one.
+  const uint64_t n_units = t.n_slots * t.nbatch;
+  const uint32_t ugeom[8] = {p->width, p->height, t.tw, t.th, p->spp, t.sps, t.shard, t.shards};
+  const bool ufit = units_on(s) && w->d_ucost && n_units <= w->ucost_cap && (!t.balanced || t.shards == 1);
+  if (ufit && w->ucost_valid && std::memcmp(ugeom, w->ucost_geom, sizeof ugeom) == 0) {
+    int e = rpk::launch_unit_order(w->d_ucost, n_units, w->d_ukey, w->d_ukey2, w->d_usort, w->usort_bytes, w->d_uorder,
+                                   stream);
+    if (e != 0) return fail(RP_EHIP, std::string("unit order launch: ") + hipGetErrorString((hipError_t)e));
+    kp.unit_order = w->d_uorder;
+    kp.order_chunk = rpk::UNIT_ORDER_CHUNK;
+    kp.dv_ochunk = rpk::make_div32(kp.order_chunk);
+    kp.dv_tile_px = rpk::make_div32(t.tw * t.th);
+    w->frame_flags |= RP_FRAME_UNIT_ORDER;
+  }
+  if (ufit) kp.unit_cost = w->d_ucost;
+  w->ucost_valid = ufit;
+  if (ufit) std::memcpy(w->ucost_geom, ugeom, sizeof ugeom);
   RP_HIP(hipMemsetAsync(w->d_meas, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
   kp.tile_meas = measure ? w->d_meas : nullptr;
   w->meas_on = measure;

@@ -1499,6 +1499,40 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     return true;
   }
   const uint32_t tile_px = tw * th, tile_units = tile_px * A->P.nbatch;
+  if (!PROBE && A->P.unit_order) {
+    // the learned per-unit order (rp_sched.hip): queue g serves the chunks g, g + G, ... of C consecutive positions,
+    // position p holds unit unit_order[p] = slot * nbatch + batch; the same drained-queue walk as the tile queues below
+    const uint32_t G = max(A->P.queue_groups, 1u), C = A->P.order_chunk, GC = G * C;
+    const uint32_t home = G > 1 ? blockIdx.x % G : 0u;
+    const uint32_t Q = (uint32_t)A->P.n_queue;
+    for (uint32_t tries = 0;;) {
+      uint32_t g = home + tries;
+      if (g >= G) g -= G;
+      g = __builtin_amdgcn_readfirstlane(g);
+      const uint32_t rest = Q % GC, nq = (Q / GC) * C + min(rest - min(rest, g * C), C);
+      const uint32_t q = atomicAdd(A->queue + g * QUEUE_STRIDE, 1u);
+      const bool drained = q >= nq;
+      if (__ballot(drained) != 0) {
+        ++tries;
+        if (drained) {
+          if (tries >= G) return false;
+          continue;
+        }
+      }
+      const uint32_t i = RPK_UDIV(q, dv_ochunk);
+      const uint32_t u = A->P.unit_order[i * GC + g * C + (q - i * C)];
+      const uint32_t sl = RPK_UDIV(u, dv_nbatch);
+      batch = u - sl * A->P.nbatch;
+      slot = sl;
+      const uint32_t k = RPK_UDIV(sl, dv_tile_px), local = sl - k * tile_px;
+      const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
+      const uint32_t ty = RPK_UDIV(t, dv_tiles_x), tx = t - ty * A->P.tiles_x;
+      const uint32_t lj = RPK_UDIV(local, dv_tw), li = local - lj * tw;
+      pi = tx * tw + li;
+      pj = ty * th + lj;
+      if (pi < A->P.W && pj < A->P.H) return true;
+    }
+  }
   // Per-XCD queues (rp.h RP_QUEUES_*): blocks blockIdx mod G share an XCD; their queue g serves the tiles
   // k = g, g + G, ... of the order (or the g-th run of it), and once it is drained they take units from the
   // next queues in turn.  Every fetch starts at the home queue: a drained queue costs one failed increment.

@@ -117,6 +117,14 @@ struct KParams {
   uint32_t prim_items_tile;    // primary pass: work items (64 camera rays: a quad x 16 samples) per tile
   uint32_t prim_sgroups;       // primary pass: 16-sample groups per pixel, ceil(spp / 16)
   Div32 dv_sps;                // primary pass: make_div32(spp_batch)
+  // Learned per-unit order (launch_unit_order): render -- every unit's duration (100 MHz ticks) is stored at
+  // unit_cost[slot * nbatch + batch] (NULL = off); and when unit_order is set the queues hand out units in its order
+  // (position p -> unit unit_order[p]; queue g serves the chunks g, g + G, ... of order_chunk positions) instead of
+  // tile by tile.
+  uint32_t* unit_cost;
+  const uint32_t* unit_order;
+  uint32_t order_chunk;
+  Div32 dv_ochunk, dv_tile_px;  // make_div32(order_chunk), make_div32(tw * th)
 };
 
 // Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last
@@ -166,6 +174,14 @@ enum { GATHER_CTR = 8, GATHER_CTR_HASH = 4 };
 // `queue` (workspace-owned) must have been zeroed on the same stream.  Returns a hipError_t as int.
 int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
                   uint32_t* queue, int grid, void* stream);
+
+// Learned per-unit order (rp_sched.hip): the n units sorted by the previous frame's durations `cost`, longest first, in
+// log-spaced buckets (UNIT_ORDER_Q per octave) that keep shard order inside -> order[0, n).  keys, keys2: n u64 each;
+// scratch: unit_order_scratch_bytes(n) bytes (hipCUB radix sort).  n < 2^31.
+enum { UNIT_ORDER_Q = 4, UNIT_ORDER_CHUNK = 256 };
+size_t unit_order_scratch_bytes(uint64_t n);
+int launch_unit_order(const uint32_t* cost, uint64_t n, uint64_t* keys, uint64_t* keys2, void* scratch,
+                      size_t scratch_bytes, uint32_t* order, void* stream);
 
 // Coherent primary pass over the shard (KParams::prim_hint, lens_radius == 0): every camera ray of the frame traced in
 // waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 jittered samples), its closest primitive written to prim_hint.

@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       rng_refill(rng, alive, fresh, seed, start ? s - 1 : s, unit_spp(A, batch));
       DCYC_END(DCYC_REFILL, cr)
       // a measured unit's start (100 MHz real-time clock, the same on every XCD): its duration is its tile's cost
-      if (!PROBE && fresh && A->P.tile_meas && meas_unit(pipj, batch))
+      if (!PROBE && fresh && ((A->P.tile_meas && meas_unit(pipj, batch)) || A->P.unit_cost))
         A->S.unit_t0[blockIdx.x * BLOCK + tid] = (uint32_t)__builtin_amdgcn_s_memrealtime();
     }
     if (start) {
@@ -270,10 +270,15 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           }
           // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas), from one unit in eight (pixel and
           // batch hashed: every tile's sample spread over its pixels and batches) -- timing all units cost 0.9 %
-          if (!PROBE && A->P.tile_meas && meas_unit(pipj, batch)) {
-            const uint32_t t0 = A->S.unit_t0[blockIdx.x * BLOCK + tid];
-            meas_dur = ((uint32_t)__builtin_amdgcn_s_memrealtime() - t0) >> MEAS_SHIFT;
-            meas_k = slot / (A->P.tw * A->P.th);
+          // every unit's duration for the next frame's per-unit order (unit_cost, rp_sched.hip)
+          const bool mt = !PROBE && A->P.tile_meas && meas_unit(pipj, batch);
+          if (!PROBE && (mt || A->P.unit_cost)) {
+            const uint32_t dur = (uint32_t)__builtin_amdgcn_s_memrealtime() - A->S.unit_t0[blockIdx.x * BLOCK + tid];
+            if (A->P.unit_cost) A->P.unit_cost[(uint64_t)slot * A->P.nbatch + batch] = dur;
+            if (mt) {
+              meas_dur = dur >> MEAS_SHIFT;
+              meas_k = slot / (A->P.tw * A->P.th);
+            }
           }
           ended_pixel = batch == 0;
           DIAG(if (!PROBE) {

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "9571f344a28ec5a4"
+#define RP_BUILD_ID "14a0538f7cbb422c"

@@ -34,7 +34,8 @@ RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0
 RP_COLLAPSE_AUTO, RP_COLLAPSE_GREEDY, RP_COLLAPSE_SAH = 0, 1, 2
 RP_LAYOUT_AUTO, RP_LAYOUT_DFS, RP_LAYOUT_DFS_LINE = 0, 1, 2
 RP_PRIMARY_AUTO, RP_PRIMARY_OFF, RP_PRIMARY_ON = 0, 1, 2
-RP_FRAME_PRIMARY_PASS, RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED = 1, 2, 4
+RP_UNITS_AUTO, RP_UNITS_TILES, RP_UNITS_LEARNED = 0, 1, 2
+RP_FRAME_PRIMARY_PASS, RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED, RP_FRAME_UNIT_ORDER = 1, 2, 4, 8
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
 RP_ABI_VERSION = 8
@@ -97,7 +98,7 @@ class rp_scene_options(Structure):
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
                 ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
                 ("unit_queues", c_uint32), ("queue_chunk", c_uint32), ("debug_stack_depth", c_uint32),
-                ("collapse", c_uint32), ("node_layout", c_uint32), ("primary", c_uint32), ("reserved", c_uint32)]
+                ("collapse", c_uint32), ("node_layout", c_uint32), ("primary", c_uint32), ("unit_order", c_uint32)]
 
 
 class rp_stats(Structure):

@@ -19,7 +19,8 @@ def scene_options(**kw) -> F.rp_scene_options:
     self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
     node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
     unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*), collapse ("auto" | "greedy" | "sah" or
-    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), primary ("auto" | "off" | "on" or RP_PRIMARY_*)."""
+    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), primary ("auto" | "off" | "on" or RP_PRIMARY_*),
+    unit_order ("auto" | "tiles" | "learned" or RP_UNITS_*)."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
@@ -40,6 +41,8 @@ def scene_options(**kw) -> F.rp_scene_options:
             v = {"auto": F.RP_COLLAPSE_AUTO, "greedy": F.RP_COLLAPSE_GREEDY, "sah": F.RP_COLLAPSE_SAH}[v]
         if k == "node_layout" and isinstance(v, str):
             v = {"auto": F.RP_LAYOUT_AUTO, "dfs": F.RP_LAYOUT_DFS, "dfs_line": F.RP_LAYOUT_DFS_LINE}[v]
+        if k == "unit_order" and isinstance(v, str):
+            v = {"auto": F.RP_UNITS_AUTO, "tiles": F.RP_UNITS_TILES, "learned": F.RP_UNITS_LEARNED}[v]
         if k == "primary" and isinstance(v, str):
             v = {"auto": F.RP_PRIMARY_AUTO, "off": F.RP_PRIMARY_OFF, "on": F.RP_PRIMARY_ON}[v]
         if not hasattr(o, k):

@@ -111,3 +111,28 @@ def test_primary_pass_c3_tile_full_spp(gpu):
     sc, p = _scene("bunny_full", 96, 64, 256)
     _on_off(gpu, sc, p)
     _on_off(gpu, sc, replace(p, samples_per_stream=256))
+
+
+@pytest.mark.parametrize("sps", [0, 256, 7])
+def test_learned_unit_order_same_frame(gpu, sps):
+    """rp_scene_options.unit_order (rp_sched.hip): the second frame on a workspace hands its units out longest first by
+    the first frame's durations -- a different schedule, the same frame bit for bit (per-unit seeding), against the
+    oracle too; with RP_UNITS_TILES no frame does."""
+    from rtpotato import _ffi as F
+    sc, p = _scene("bunny_full", 72, 40, 64)
+    p = replace(p, samples_per_stream=sps, tile_w=16, tile_h=16)
+    with gpu.DeviceScene(sc, options={"unit_order": "learned"}) as ds:
+        a, fa, sa = ds.render(p, foreground=True)
+        f1 = ds.frame_info()
+        b, fb, sb = ds.render(p, foreground=True)
+        f2 = ds.frame_info()
+    assert not f1 & F.RP_FRAME_UNIT_ORDER and f2 & F.RP_FRAME_UNIT_ORDER, (f1, f2)
+    assert np.array_equal(a, b) and np.array_equal(fa, fb) and sa["rays"] == sb["rays"]
+    ref, _, ctr = oracle_render(sc, p, threads=8)
+    assert_parity(compare(b, ref))
+    assert sb["rays"] == ctr["rays"]
+    with gpu.DeviceScene(sc, options={"unit_order": "tiles"}) as ds:
+        ds.render(p)
+        c, _, sc_ = ds.render(p)
+        assert not ds.frame_info() & F.RP_FRAME_UNIT_ORDER
+    assert np.array_equal(c, b) and sc_["rays"] == sb["rays"]
