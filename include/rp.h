@@ -243,8 +243,8 @@ enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1, RP_PRIMARY_ON = 2 };
  * TILES: tile by tile (tile_order), a tile's pixels row-major.  LEARNED: every render stores each unit's duration,
  * and the next frame of the same shape on the same workspace hands out its units longest first (in log-spaced
  * buckets that keep shard order inside; a frame ends with its longest unit), on one device or interleaved shards
- * (a balanced plan's tiles may move between frames: those frames keep TILES).  AUTO = LEARNED where measured faster
- * (DESIGN.md 4.3).  Results never depend on it. */
+ * (a balanced plan's tiles may move between frames: those frames keep TILES).  AUTO = TILES: the learned order lost
+ * 6-28 % on C3 and C5.  Results never depend on it. */
 enum { RP_UNITS_AUTO = 0, RP_UNITS_TILES = 1, RP_UNITS_LEARNED = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster

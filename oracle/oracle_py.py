@@ -34,6 +34,8 @@ def lib(fast: bool = False) -> ctypes.CDLL:
     if fast in _libs:
         return _libs[fast]
     path = LIB_FAST if fast else LIB
+    if os.environ.get("OR_LIB"):  # the sanitizer build of the oracle (tools/sanitize.sh)
+        path = os.environ["OR_LIB"]
     if not os.path.exists(path):
         build()
     L = ctypes.CDLL(path)

@@ -412,10 +412,12 @@ uint64_t stage_slots(const Tiling& t) {
   return (uint64_t)n0 * t.tw * t.th;
 }
 
-// The learned per-unit order (rp.h RP_UNITS_*) is kept for this scene: LEARNED, or AUTO, megakernel engine.
+// The learned per-unit order (rp.h RP_UNITS_*) is kept for this scene: LEARNED, megakernel engine.  AUTO = TILES:
+// longest-first units lost on both configs and both RNG contracts (C3 261.5 vs 206.4 ms, one stream per pixel 337.8 vs
+// 262.8, C5 1,628.6 vs 1,531.4 ms; profiles/r5/c3_c5_unit_order_ab.json) -- a wave's 64 units are then unrelated
+// pixels, and the neighbouring pixels (and a pixel's batches) of the tile order trace coherent paths.
 bool units_on(const rp_scene* s) {
-  return (s->opt.unit_order == RP_UNITS_LEARNED || s->opt.unit_order == RP_UNITS_AUTO) &&
-         s->opt.engine == RP_ENGINE_MEGAKERNEL;
+  return s->opt.unit_order == RP_UNITS_LEARNED && s->opt.engine == RP_ENGINE_MEGAKERNEL;
 }
 
 // The coherent primary pass runs for this scene (rp.h RP_PRIMARY_*): ON, megakernel engine.  AUTO is OFF: measured

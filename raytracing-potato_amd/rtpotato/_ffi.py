@@ -225,7 +225,7 @@ def host() -> ctypes.CDLL:
     global _host
     if _host is not None:
         return _host
-    path = host_lib_path()
+    path = os.environ.get("RP_HOST_LIB") or host_lib_path()  # RP_HOST_LIB: the sanitizer build (tools/sanitize.sh)
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `make -C raytracing-potato_amd`")
     lib = ctypes.CDLL(path)
