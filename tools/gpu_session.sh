@@ -153,6 +153,12 @@ for s in ${STEPS:-tests}; do
       timeout -k 10 600 rocprofv3 --kernel-trace -d $out -o run --output-format csv -- \
         python3 tools/primary_coherence.py --config $cfg --meta $out.meta.json ${COH_ARGS:-} > $out.log 2>&1 &&
       python3 tools/primary_coherence.py --trace $out --meta $out.meta.json > $out.json 2>> $out.log || exit 1 ;;
+    ldswait_*)  # tools/gather_lds_wait.py: a kernel of RCCL's all-gather footprint behind frames in flight (LDSW_ARGS)
+      cfg=${s#ldswait_}
+      out=gpurun_out/${TAG}_${cfg}_ldswait${LDSW_LABEL:+_$LDSW_LABEL}
+      step "ldswait $cfg $LDSW_LABEL"
+      made $out.json "python3 tools/gather_lds_wait.py --config $cfg ${LDSW_ARGS:-}"
+      timeout -k 10 600 python3 tools/gather_lds_wait.py --config $cfg ${LDSW_ARGS:-} > $out.json 2> $out.err || exit 1 ;;
     *) echo "unknown step $s" >> $P; exit 2 ;;
   esac
 done
