@@ -265,7 +265,7 @@ static void check_oracle_render(const MeshScene& s) {
 
 int main(int argc, char** argv) {
   const std::string dir = argc > 1 ? argv[1] : "/tmp";
-  MeshScene a = soup(60000, 11);
+  MeshScene a = soup(200000, 11);  // >= 2^16 primitives: the parallel build form (rp_bvh.cpp ParallelBuild) runs
   check_tree("soup", a.desc);
   MeshScene b = grid_with_degenerates(40, 3);
   check_tree("grid+degenerates", b.desc);
