@@ -430,9 +430,9 @@ int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
  * Outputs (either nullable, on the rank's device, frame order, row 0 = bottom): d_frame_bgra width*height*4
  * bytes = to_srgb_u8 in tga::save byte order (rp_shard_to_bgra8) -- the body of output.tga; d_frame_rgb
  * width*height*3 linear f64.  Every rank must pass the same NULL / non-NULL combination of d_frame_bgra and
- * d_frame_rgb: the collectives issued are, in this order, an all-gather of every rank's counter block (always),
- * two of its measured tile costs (frames of <= 16384 tiles), of the BGRA8 shards (d_frame_bgra) and of the f64
- * shards (d_frame_rgb).  d_counters (nullable): the rank's
+ * d_frame_rgb: the collectives issued are, in this order, ONE all-gather of every rank's packed block -- its counter
+ * block, its measured tile costs (zeros for frames of more than 16384 tiles) and, with d_frame_bgra, its BGRA8
+ * shard -- and, with d_frame_rgb, one of the f64 shards.  d_counters (nullable): the rank's
  * RP_COUNTERS_LEN counters in, the frame's out -- rays, samples and pixels summed over the ranks, status bits
  * OR-ed over them, plus RP_STATUS_PLAN_MISMATCH when the ranks' balanced plans differ.  A caller that does not
  * pass counters does not learn the status.  Tile costs (the collectives also all-gather every rank's measured

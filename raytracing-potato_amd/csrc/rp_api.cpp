@@ -133,14 +133,15 @@ struct rp_workspace {
   bool ucost_valid = false;
   uint32_t ucost_geom[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   double* d_gs_rgb = nullptr;        // gather staging: this rank's shard, padded to the stride (3 f64 / slot)
-  uint32_t* d_gs_bgra = nullptr;     //   ... its to_srgb_u8 bytes (1 word / slot)
   double* d_gather_rgb = nullptr;    //   all ranks' shards (nranks x stride x 3 f64)
-  uint32_t* d_gather_bgra = nullptr; //   all ranks' bytes (nranks x stride words)
-  uint64_t gs_slots = 0;             // capacity of d_gs_* in slots
-  uint64_t gather_slots = 0;         // capacity of d_gather_* in slots (over all ranks)
-  uint64_t* d_ctr_send = nullptr;    // this rank's counter block of a frame gather (rpk::GATHER_CTR words)
-  uint64_t* d_ctr_gather = nullptr;  // every rank's block (ctr_ranks x rpk::GATHER_CTR)
-  uint32_t ctr_ranks = 0;
+  uint64_t gs_slots = 0;             // capacity of d_gs_rgb in slots
+  uint64_t gather_slots = 0;         // capacity of d_gather_rgb in slots (over all ranks)
+  // a frame gather's one collective (rpk::launch_gather_pack): this rank's packed block -- counters, measured tile
+  // costs, to_srgb_u8 bytes -- and every rank's
+  uint32_t* d_pack_send = nullptr;
+  uint32_t* d_pack_recv = nullptr;
+  uint64_t pack_words = 0;           // capacity of d_pack_send in words
+  uint64_t pack_recv_words = 0;      // capacity of d_pack_recv in words
   // the balanced tile plan (RP_SHARD_BALANCED) of the last frame rendered with this workspace: the deal order,
   // its inverse and its hash (rpk::launch_tile_plan), and the frame geometry it was made for
   uint32_t* d_plan = nullptr;
@@ -150,8 +151,6 @@ struct rp_workspace {
   // durations, every rank's of them after a frame gather, and the learned per-frame-tile table the next frame of
   // the same geometry schedules with instead of a cost probe.
   uint32_t* d_meas = nullptr;     // 2 x TILE_SORT_MAX: [k] summed, [TILE_SORT_MAX + k] longest unit of shard tile k
-  uint32_t* d_meas_g = nullptr;   // frame gather: 2 x nranks x stride_tiles (sums, then maxima; rank-major)
-  uint64_t meas_g_words = 0;
   uint32_t* d_fcost = nullptr;    // learned table: 2 x TILE_SORT_MAX, by frame tile
   uint64_t* d_sort = nullptr;     // the tile sorts' keys (rpk::SORT_SCRATCH words: global memory, not LDS)
   bool meas_on = false;           // the last render measured (megakernel)
@@ -217,9 +216,9 @@ void ws_release(rp_workspace* w) {
   if (w->wf.host_count) (void)hipHostFree(w->wf.host_count);
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
-                  (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gs_bgra, (void*)w->d_gather_rgb,
-                  (void*)w->d_gather_bgra, (void*)w->d_ctr_send, (void*)w->d_ctr_gather, (void*)w->d_plan,
-                  (void*)w->d_meas, (void*)w->d_meas_g, (void*)w->d_fcost, (void*)w->d_sort, (void*)w->d_t0,
+                  (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gather_rgb, (void*)w->d_pack_send,
+                  (void*)w->d_pack_recv, (void*)w->d_plan, (void*)w->d_meas, (void*)w->d_fcost, (void*)w->d_sort,
+                  (void*)w->d_t0,
                   (void*)w->d_hint, (void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder,
                   w->d_usort})
     dfree(p);
@@ -428,6 +427,17 @@ bool primary_on(const rp_scene* s) {
   return s->opt.primary == RP_PRIMARY_ON && s->opt.engine == RP_ENGINE_MEGAKERNEL;
 }
 
+// Words of a rank's packed gather block (rpk::launch_gather_pack): the counter block and 2 x tiles per rank of measured
+// costs (rounded up to even), then, when the frame gathers BGRA8, the shard's bytes (rounded up to even: every block
+// starts 8-byte aligned for the u64 counters).
+uint64_t pack_head(const Tiling& t) {
+  const uint64_t st = (t.n_tiles + t.shards - 1) / t.shards;
+  return 2ull * rpk::GATHER_CTR + ((2 * st + 1) & ~1ull);
+}
+uint64_t pack_words(const Tiling& t, bool bgra) {
+  return pack_head(t) + (bgra ? ((stage_slots(t) + 1) & ~1ull) : 0ull);
+}
+
 // Grow a pair of device buffers (a, b) of na, nb elements per unit to `units` units (synchronous).
 template <class A, class B>
 int grow(A*& a, B*& b, uint64_t& cap, uint64_t units, uint64_t na, uint64_t nb, const char* what) {
@@ -480,26 +490,23 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
   }
   if (gather) {
     const uint64_t stride = stage_slots(t);
-    if ((rc = grow(w->d_gs_rgb, w->d_gs_bgra, w->gs_slots, stride, 3, 1, "gather staging"))) return rc;
-    if ((rc = grow(w->d_gather_rgb, w->d_gather_bgra, w->gather_slots, stride * t.shards, 3, 1, "gather buffers")))
-      return rc;
-    if (t.shards > w->ctr_ranks) {
-      dfree(w->d_ctr_send);
-      dfree(w->d_ctr_gather);
-      w->d_ctr_send = w->d_ctr_gather = nullptr;
-      w->ctr_ranks = 0;
-      if (!dalloc(&w->d_ctr_send, rpk::GATHER_CTR) || !dalloc(&w->d_ctr_gather, (uint64_t)rpk::GATHER_CTR * t.shards))
-        return fail(RP_ENOMEM, "hipMalloc gather counters");
-      w->ctr_ranks = t.shards;
-    }
-    const uint64_t mw = 2ull * t.shards * ((t.n_tiles + t.shards - 1) / t.shards);
-    if (mw > w->meas_g_words) {
-      dfree(w->d_meas_g);
-      w->d_meas_g = nullptr;
-      w->meas_g_words = 0;
-      if (!dalloc(&w->d_meas_g, mw)) return fail(RP_ENOMEM, "hipMalloc gather tile costs");
-      w->meas_g_words = mw;
-    }
+    auto grow1 = [&](auto*& b, uint64_t& cap, uint64_t want, const char* what) -> int {
+      if (want <= cap) return RP_OK;
+      dfree(b);
+      b = nullptr;
+      cap = 0;
+      if (!dalloc(&b, want)) return fail(RP_ENOMEM, std::string("hipMalloc ") + what);
+      cap = want;
+      return RP_OK;
+    };
+    uint64_t rgb_cap = w->gs_slots * 3, rgb_g_cap = w->gather_slots * 3;
+    if ((rc = grow1(w->d_gs_rgb, rgb_cap, stride * 3, "gather staging"))) return rc;
+    if ((rc = grow1(w->d_gather_rgb, rgb_g_cap, stride * t.shards * 3, "gather buffers"))) return rc;
+    w->gs_slots = rgb_cap / 3;
+    w->gather_slots = rgb_g_cap / 3;
+    const uint64_t pw = pack_words(t, true);
+    if ((rc = grow1(w->d_pack_send, w->pack_words, pw, "gather block"))) return rc;
+    if ((rc = grow1(w->d_pack_recv, w->pack_recv_words, pw * t.shards, "gathered blocks"))) return rc;
   }
   return RP_OK;
 }
@@ -955,6 +962,7 @@ struct GatherPlan {
   Tiling t;
   uint64_t stride;  // slots per rank buffer
   uint32_t stride_tiles;  // tiles per rank buffer (shard 0's count)
+  uint64_t head;          // words of the packed block before the BGRA8 bytes (pack_head)
   rpk::FrameGeom geom;
   const uint32_t* plan_hash;  // the workspace's plan hash (balanced frames), NULL = interleave
 };
@@ -967,8 +975,9 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
     return fail(RP_EINVAL, "params.shard / num_shards must be the communicator's rank / size");
   gp.stride = stage_slots(gp.t);
   gp.stride_tiles = (gp.t.n_tiles + gp.t.shards - 1) / gp.t.shards;
-  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || (uint32_t)nranks > w->ctr_ranks ||
-      2ull * nranks * gp.stride_tiles > w->meas_g_words)
+  gp.head = pack_head(gp.t);
+  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || pack_words(gp.t, true) > w->pack_words ||
+      pack_words(gp.t, true) * nranks > w->pack_recv_words)
     return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
   gp.geom.W = p->width;
   gp.geom.H = p->height;
@@ -977,6 +986,7 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   gp.geom.tiles_x = gp.t.tiles_x;
   gp.geom.nranks = (uint32_t)nranks;
   gp.geom.stride = gp.stride;
+  gp.geom.rank_words = 0;
   gp.geom.tile_pos = nullptr;
   gp.plan_hash = nullptr;
   if (gp.t.balanced) {
@@ -988,14 +998,18 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   return RP_OK;
 }
 
-// (1) this rank's part: its counter block for the counter all-gather, its to_srgb_u8 bytes and/or a padded f64 copy
+// (1) this rank's packed block for the one collective -- its counters (and plan hash), its measured tile costs, its
+// to_srgb_u8 bytes -- and/or a padded f64 copy of the shard
 int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const double* d_shard_rgb, bool bgra, bool rgb,
                  const uint64_t* d_counters, hipStream_t st) {
   DeviceGuard g(s->device);
-  int e = rpk::launch_counters_stage(d_counters, gp.plan_hash, w->d_ctr_send, st);
-  if (e != 0) return fail(RP_EHIP, std::string("counter stage launch: ") + hipGetErrorString((hipError_t)e));
+  // the measured costs travel only for frames whose tiles fit the table (gather_learn's condition)
+  const uint32_t* meas = gp.t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX ? w->d_meas : nullptr;
+  int e = rpk::launch_gather_pack(d_counters, gp.plan_hash, meas, gp.stride_tiles, w->d_pack_send, st);
+  if (e != 0) return fail(RP_EHIP, std::string("gather pack launch: ") + hipGetErrorString((hipError_t)e));
   if (bgra && gp.t.n_slots) {
-    e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_gs_bgra), st);
+    e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_pack_send + gp.head),
+                              st);
     if (e != 0) return fail(RP_EHIP, std::string("output stage launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (rgb && gp.t.n_slots && d_shard_rgb != w->d_gs_rgb)
@@ -1003,33 +1017,28 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
   return RP_OK;
 }
 
-// (2) the collectives, in a fixed sequence: the counter blocks are always all-gathered (status bits must be OR-ed,
-// not summed: an even number of ranks with the same bit set would clear it -- and the plan hashes compared), then
-// the BGRA8 and/or f64 shards (rp.h: every rank passes the same NULL / non-NULL outputs)
+// (2) the collectives: ONE all-gather of the packed blocks (counters -- status bits are OR-ed, not summed, and the plan
+// hashes compared --, measured tile costs, BGRA8 bytes), then the f64 shards when asked for (rp.h: every rank passes
+// the same NULL / non-NULL outputs, so every rank gathers the same block size).  One collective instead of four: an
+// RCCL all-gather kernel on gfx950 needs 37.7 KB of LDS and 256 VGPRs per lane, so with frames in flight each one
+// waits ~8-24 ms for a CU the render waves leave (profiles/r5/c3_gather_lds_wait.json).
 int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb, hipStream_t st) {
-  RP_NCCL(ncclAllGather(w->d_ctr_send, w->d_ctr_gather, rpk::GATHER_CTR, ncclUint64, comm, st));
-  // every rank's measured tile costs (sums, then maxima): the next frame's learned table, the same on every rank
-  // -- only for frames whose tiles fit the table (gather_learn's condition; a function of the params, so the same on
-  // every rank and the collective sequence stays consistent)
-  if (gp.t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX) {
-    const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
-    RP_NCCL(ncclAllGather(w->d_meas, w->d_meas_g, gp.stride_tiles, ncclUint32, comm, st));
-    RP_NCCL(ncclAllGather(w->d_meas + rpk::TILE_SORT_MAX, w->d_meas_g + n, gp.stride_tiles, ncclUint32, comm, st));
-  }
-  if (bgra) RP_NCCL(ncclAllGather(w->d_gs_bgra, w->d_gather_bgra, gp.stride, ncclUint32, comm, st));
+  RP_NCCL(ncclAllGather(w->d_pack_send, w->d_pack_recv, pack_words(gp.t, bgra), ncclUint32, comm, st));
   if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
   return RP_OK;
 }
 
 // (3a) the gathered tile costs -> the workspace's learned table (on every device of the frame)
-int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_render_params* p, hipStream_t st) {
+int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_render_params* p, bool bgra,
+                 hipStream_t st) {
   DeviceGuard g(s->device);
   if (!w->meas_on || gp.t.n_tiles > (uint32_t)rpk::TILE_SORT_MAX) {
     w->fcost_valid = false;
   } else {
-    const uint64_t n = (uint64_t)gp.geom.nranks * gp.stride_tiles;
-    int e = rpk::launch_learn_costs(w->d_meas_g, w->d_meas_g + n, gp.stride_tiles, gp.geom.nranks, gp.t.n_tiles,
-                                    gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
+    // rank r's sums at r * block + 2 GATHER_CTR, its maxima stride_tiles further
+    const uint32_t* sums = w->d_pack_recv + 2 * rpk::GATHER_CTR;
+    int e = rpk::launch_learn_costs(sums, sums + gp.stride_tiles, (uint32_t)pack_words(gp.t, bgra), gp.geom.nranks,
+                                    gp.t.n_tiles, gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
     if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
     set_fcost(w, p, gp.t, gp.geom.nranks);
   }
@@ -1043,10 +1052,14 @@ int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_re
 int gather_assemble(rp_scene* s, rp_workspace* w, const GatherPlan& gp, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, hipStream_t st) {
   DeviceGuard g(s->device);
-  int e = rpk::launch_counters_reduce(w->d_ctr_gather, gp.geom.nranks, d_counters ? d_counters : w->d_ctr, st);
+  const uint64_t block = pack_words(gp.t, d_frame_bgra != nullptr);
+  int e = rpk::launch_counters_reduce(reinterpret_cast<const uint64_t*>(w->d_pack_recv), gp.geom.nranks, block,
+                                      d_counters ? d_counters : w->d_ctr, st);
   if (e != 0) return fail(RP_EHIP, std::string("counter reduce launch: ") + hipGetErrorString((hipError_t)e));
   if (d_frame_bgra) {
-    e = rpk::launch_frame_assemble(gp.geom, w->d_gather_bgra, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
+    rpk::FrameGeom fg = gp.geom;
+    fg.rank_words = block;
+    e = rpk::launch_frame_assemble(fg, w->d_pack_recv + gp.head, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
     if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (d_frame_rgb) {
@@ -1377,7 +1390,7 @@ int rp_frame_assemble(const rp_render_params* p, const void* d_gathered, uint32_
   if (rc) return rc;
   if (!d_gathered || !d_frame || words == 0) return fail(RP_EINVAL, "NULL buffer or zero words per slot");
   if (t.balanced) return fail(RP_EINVAL, "balanced frame: assemble with rp_frame_assemble_ws (the workspace holds the plan)");
-  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), nullptr};
+  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), 0, nullptr};
   int e = rpk::launch_frame_assemble(g, static_cast<const uint32_t*>(d_gathered), words, static_cast<uint32_t*>(d_frame),
                                      stream);
   if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
@@ -1429,7 +1442,7 @@ int rp_frame_assemble_ws(rp_scene* s, rp_workspace* w, const rp_render_params* p
   int rc = make_tiling(p, t);
   if (rc) return rc;
   if (!d_gathered || !d_frame || words == 0) return fail(RP_EINVAL, "NULL buffer or zero words per slot");
-  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), nullptr};
+  rpk::FrameGeom g{p->width, p->height, t.tw, t.th, t.tiles_x, t.shards, stage_slots(t), 0, nullptr};
   if (t.balanced) {
     if (!plan_matches(w, p, t)) return fail(RP_EINVAL, "no balanced plan for this frame in the workspace: render it first");
     g.tile_pos = w->d_plan + t.n_tiles;
@@ -1501,7 +1514,7 @@ int rp_frame_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_pa
   DeviceGuard g(s->device);
   if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, rgb, d_counters, st))) return rc;
   if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, st))) return rc;
-  if ((rc = gather_learn(s, w, gp, p, st))) return rc;
+  if ((rc = gather_learn(s, w, gp, p, bgra, st))) return rc;
   return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, d_counters, st);
 }
 
@@ -1620,7 +1633,7 @@ int rp_render_multi(rp_multi* m, const rp_camera* cam, const rp_render_params* p
   }
   RP_NCCL(ncclGroupEnd());
   for (int k = 0; k < n; k++) {
-    int rc = gather_learn(m->scenes[k], &m->scenes[k]->ws0, plans[k], &ps[k], m->streams[k]);
+    int rc = gather_learn(m->scenes[k], &m->scenes[k]->ws0, plans[k], &ps[k], bgra, m->streams[k]);
     if (rc) return rc;
   }
   rp_scene* s0 = m->scenes[0];

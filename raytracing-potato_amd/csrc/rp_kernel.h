@@ -220,7 +220,8 @@ int launch_srgb_bgra(const SrgbTable& tab, const double* rgb, uint64_t n, uint8_
 // row-major offset inside the tile, k = t / nranks: rp_shard_unpack's order).  One thread per pixel.
 struct FrameGeom {
   uint32_t W, H, tw, th, tiles_x, nranks;
-  uint64_t stride;
+  uint64_t stride;           // slots per rank buffer
+  uint64_t rank_words;       // 32-bit words from one rank's buffer to the next (0 = stride * words: packed shards)
   const uint32_t* tile_pos;  // frame tile -> its position in the deal order (rank = pos % nranks, shard tile k =
                              // pos / nranks); NULL = interleave (pos = the tile index)
 };
@@ -238,8 +239,14 @@ int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t
 // Counters of a frame gather: stage this rank's block (ctr may be NULL = zeros; hash may be NULL = 0) for the
 // all-gather, and reduce the gathered blocks of nranks ranks into out (sums; status bits OR-ed, plus
 // STATUS_PLAN_MISMATCH when two ranks' plan hashes differ).
-int launch_counters_stage(const uint64_t* ctr, const uint32_t* hash, uint64_t* send, void* stream);
-int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t* out, void* stream);
+// A frame gather's one collective carries, per rank, a packed block of 32-bit words (GATHER_HEAD + 2 x stride_tiles,
+// rounded up to even, then the BGRA8 shard): [0, 2 GATHER_CTR) the counter block (GATHER_CTR u64), then the measured
+// tile costs -- stride_tiles sums, stride_tiles maxima (zeros past the table) -- then the to_srgb_u8 bytes.
+// launch_gather_pack writes the first two parts (ctr / hash NULL = zeros, meas = the workspace's 2 x TILE_SORT_MAX
+// measured costs, NULL = zeros); launch_counters_reduce reads nranks blocks `rank_words` apart.
+int launch_gather_pack(const uint64_t* ctr, const uint32_t* hash, const uint32_t* meas, uint32_t stride_tiles,
+                       uint32_t* send, void* stream);
+int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t rank_words, uint64_t* out, void* stream);
 int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t words, uint32_t* frame,
                           void* stream);
 

@@ -669,7 +669,8 @@ __global__ void __launch_bounds__(256) frame_assemble_kernel(const FrameGeom g, 
     const uint32_t pos = g.tile_pos ? g.tile_pos[t] : t;
     const uint32_t r = pos % g.nranks, k = pos / g.nranks;
     const uint64_t slot = (uint64_t)k * g.tw * g.th + (uint64_t)(j % g.th) * g.tw + i % g.tw;
-    const uint32_t* s = src + ((uint64_t)r * g.stride + slot) * words;
+    const uint64_t rw = g.rank_words ? g.rank_words : g.stride * words;
+    const uint32_t* s = src + (uint64_t)r * rw + slot * words;
     for (uint32_t w = 0; w < words; w++) frame[px * words + w] = s[w];
   }
 }
@@ -849,21 +850,29 @@ int launch_tile_plan(const uint32_t* cost, uint32_t n, uint32_t nranks, uint32_t
   return (int)hipGetLastError();
 }
 
-// Counters of a frame gather (rp_kernel.h launch_counters_stage / _reduce): one tiny block each.
-__global__ void counters_stage_kernel(const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ hash,
-                                      uint64_t* __restrict__ send) {
-  const uint32_t i = threadIdx.x;
-  if (i >= GATHER_CTR) return;
-  uint64_t v = 0;
-  if (i < CTR_N) v = ctr ? ctr[i] : 0ull;
-  else if (i == GATHER_CTR_HASH) v = hash ? ((uint64_t)hash[1] << 32 | hash[0]) : 0ull;
-  send[i] = v;
+// The packed block of a frame gather (rp_kernel.h launch_gather_pack) and the counter reduction.  Small kernels
+// without LDS that fit beside in-flight render waves.
+__global__ void __launch_bounds__(256) gather_pack_kernel(const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ hash,
+                                                          const uint32_t* __restrict__ meas, uint32_t st,
+                                                          uint32_t* __restrict__ send) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < GATHER_CTR) {
+    uint64_t v = 0;
+    if (i < CTR_N) v = ctr ? ctr[i] : 0ull;
+    else if (i == GATHER_CTR_HASH) v = hash ? ((uint64_t)hash[1] << 32 | hash[0]) : 0ull;
+    reinterpret_cast<uint64_t*>(send)[i] = v;
+  }
+  if (i < 2 * st) {  // sums [0, st), maxima [st, 2 st): the measured table holds TILE_SORT_MAX of each
+    const uint32_t half = i < st ? 0u : 1u, k = i - half * st;
+    send[2 * GATHER_CTR + i] = meas && k < (uint32_t)TILE_SORT_MAX ? meas[half * TILE_SORT_MAX + k] : 0u;
+  }
 }
-__global__ void counters_reduce_kernel(const uint64_t* __restrict__ g, uint32_t nranks, uint64_t* __restrict__ out) {
+__global__ void counters_reduce_kernel(const uint64_t* __restrict__ g, uint32_t nranks, uint64_t rank_u64,
+                                       uint64_t* __restrict__ out) {
   if (threadIdx.x != 0) return;
   uint64_t rays = 0, samples = 0, pixels = 0, status = 0;
   for (uint32_t r = 0; r < nranks; r++) {
-    const uint64_t* b = g + (uint64_t)r * GATHER_CTR;
+    const uint64_t* b = g + (uint64_t)r * rank_u64;
     rays += b[CTR_RAYS];
     samples += b[CTR_SAMPLES];
     pixels += b[CTR_PIXELS];
@@ -875,12 +884,16 @@ __global__ void counters_reduce_kernel(const uint64_t* __restrict__ g, uint32_t 
   out[CTR_PIXELS] = pixels;
   out[CTR_STATUS] = status;
 }
-int launch_counters_stage(const uint64_t* ctr, const uint32_t* hash, uint64_t* send, void* stream) {
-  hipLaunchKernelGGL(counters_stage_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, ctr, hash, send);
+int launch_gather_pack(const uint64_t* ctr, const uint32_t* hash, const uint32_t* meas, uint32_t stride_tiles,
+                       uint32_t* send, void* stream) {
+  const uint32_t n = 2 * stride_tiles > GATHER_CTR ? 2 * stride_tiles : GATHER_CTR;
+  hipLaunchKernelGGL(gather_pack_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctr, hash, meas,
+                     stride_tiles, send);
   return (int)hipGetLastError();
 }
-int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t* out, void* stream) {
-  hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, nranks, out);
+int launch_counters_reduce(const uint64_t* gathered, uint32_t nranks, uint64_t rank_words, uint64_t* out, void* stream) {
+  hipLaunchKernelGGL(counters_reduce_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, gathered, nranks, rank_words / 2,
+                     out);
   return (int)hipGetLastError();
 }
 

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "a08c61e694992271"
+#define RP_BUILD_ID "9da3ce01dfd95a72"
