@@ -909,7 +909,11 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
       kp.prim_hint = w->d_hint;
       kp.dv_sps = rpk::make_div32(t.sps);
       const uint64_t items = per_tile * t.n_shard_tiles;
-      int e = rpk::launch_primary(ks, kp, ctr, w->d_queue + rpk::QUEUE_PRIM, grid_for(items * rpk::RENDER_BLOCK), stream);
+      // 8-wide trees traverse lane by lane with the render kernel's spill runs (its grid); the 4-wide packet traversal
+      // keeps its stack in LDS and runs at its own occupancy (<= 96 VGPRs: 5 waves per SIMD)
+      const int pgrid = ks.node_format == rpl::NODES_W8 ? grid_for(items * rpk::RENDER_BLOCK)
+                                                        : (int)std::min<uint64_t>(items, (uint64_t)s->num_cu * 20);
+      int e = rpk::launch_primary(ks, kp, ctr, w->d_queue + rpk::QUEUE_PRIM, pgrid, stream);
       if (e != 0) return fail(RP_EHIP, std::string("primary pass launch: ") + hipGetErrorString((hipError_t)e));
       w->frame_flags |= RP_FRAME_PRIMARY_PASS;
     }

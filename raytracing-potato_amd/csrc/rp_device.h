@@ -1074,6 +1074,152 @@ RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V
   hr.km = t.bestm;
 }
 
+// Packet traversal of a coherent wave (the primary pass, rp_kernel.hip primary_kernel; Node4 / Node4Q trees).  The 64
+// lanes' rays leave one pixel quad within a sample's jitter, so the wave walks ONE stack of (entry, lane mask) pairs:
+// at an inner node (a wave-uniform address: one fetch for the wave) each lane of the entry's mask tests the four child
+// boxes with its own conservative slab test and closest hit so far, a child is taken with the mask of the lanes that
+// hit it, nearest first in the order of the mask's first lane; at a leaf the mask's lanes run the exact f64 tests.  A
+// lane tests every subtree its own test accepts (the visit order only changes which exact-t tie wins), so each lane
+// gets its closest hit as in trav_step.  The stack lives in LDS (entries at stk_e, masks at stk_m, `cap` entries),
+// written by lane 0 and read by the wave.
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+template <uint32_t NF>
+RPK_INLINE void packet_traverse(const KScene& S, lds_u32* stk_e, lds_u64* stk_m, uint32_t cap,
+                                uint64_t live, const Ray32& r, V3 o, V3 d, double tmin, TravState& ts,
+                                bool& overflow, TravDiag* td = nullptr) {
+  static_assert(NF == rpl::NODES_F32 || NF == rpl::NODES_Q8, "packet traversal: 4-wide trees");
+  const uint32_t lane = __lane_id();
+  uint32_t cur = S.root, sp = 0;
+  uint64_t m = live;
+  double best = ts.best;
+  float best32 = f32_up(best);
+  const char* nb = reinterpret_cast<const char*>(S.nodes);
+  for (;;) {
+    const bool in = (m >> lane) & 1ull;
+    if (m != 0 && !(cur & rpl::ENTRY_LEAF)) {
+      DIAG(if (td && in) td->visits++;)
+      f2 NX[2], FX[2], NY[2], FY[2], NZ[2], FZ[2];
+      uint4 ch;
+      if constexpr (NF == rpl::NODES_Q8) {
+        const uint32_t no = cur << 6;
+        const float4 c0 = *reinterpret_cast<const float4*>(nb + no);
+        const uint4 c1 = *reinterpret_cast<const uint4*>(nb + (no + 16u));
+        const uint4 c2 = *reinterpret_cast<const uint4*>(nb + (no + 32u));
+        ch = *reinterpret_cast<const uint4*>(nb + (no + 48u));
+        const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
+        const float Bnx = fmaf(c0.x, r.ix, r.nbx), Bny = fmaf(c0.y, r.iy, r.nby), Bnz = fmaf(c0.z, r.iz, r.nbz);
+        const float Bfx = fmaf(c0.x, r.ix, r.fbx), Bfy = fmaf(c0.y, r.iy, r.fby), Bfz = fmaf(c0.z, r.iz, r.fbz);
+        const uint32_t qnx = __builtin_amdgcn_perm(c1.w, c1.z, r.sx), qfx = __builtin_amdgcn_perm(c1.z, c1.w, r.sx);
+        const uint32_t qny = __builtin_amdgcn_perm(c2.y, c2.x, r.sy), qfy = __builtin_amdgcn_perm(c2.x, c2.y, r.sy);
+        const uint32_t qnz = __builtin_amdgcn_perm(c2.w, c2.z, r.sz), qfz = __builtin_amdgcn_perm(c2.z, c2.w, r.sz);
+        const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az};
+        const f2 bnx = {Bnx, Bnx}, bny = {Bny, Bny}, bnz = {Bnz, Bnz}, bfx = {Bfx, Bfx}, bfy = {Bfy, Bfy}, bfz = {Bfz, Bfz};
+#define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+          NX[q] = pk_fma(RPK_Q2(qnx, q), ax, bnx);
+          FX[q] = pk_fma(RPK_Q2(qfx, q), ax, bfx);
+          NY[q] = pk_fma(RPK_Q2(qny, q), ay, bny);
+          FY[q] = pk_fma(RPK_Q2(qfy, q), ay, bfy);
+          NZ[q] = pk_fma(RPK_Q2(qnz, q), az, bnz);
+          FZ[q] = pk_fma(RPK_Q2(qfz, q), az, bfz);
+        }
+#undef RPK_Q2
+      } else {
+        const uint32_t no = cur << 7;
+        const float4 nx = *reinterpret_cast<const float4*>(nb + (no + r.sx));
+        const float4 fx = *reinterpret_cast<const float4*>(nb + (no + (r.sx ^ 16u)));
+        const float4 ny = *reinterpret_cast<const float4*>(nb + (no + r.sy));
+        const float4 fy = *reinterpret_cast<const float4*>(nb + (no + (r.sy ^ 16u)));
+        const float4 nz = *reinterpret_cast<const float4*>(nb + (no + r.sz));
+        const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.sz ^ 16u)));
+        ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
+        const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
+        const f2 nbx = {r.nbx, r.nbx}, nby = {r.nby, r.nby}, nbz = {r.nbz, r.nbz};
+        const f2 fbx = {r.fbx, r.fbx}, fby = {r.fby, r.fby}, fbz = {r.fbz, r.fbz};
+        NX[0] = pk_fma(f2{nx.x, nx.y}, ix, nbx); NX[1] = pk_fma(f2{nx.z, nx.w}, ix, nbx);
+        FX[0] = pk_fma(f2{fx.x, fx.y}, ix, fbx); FX[1] = pk_fma(f2{fx.z, fx.w}, ix, fbx);
+        NY[0] = pk_fma(f2{ny.x, ny.y}, iy, nby); NY[1] = pk_fma(f2{ny.z, ny.w}, iy, nby);
+        FY[0] = pk_fma(f2{fy.x, fy.y}, iy, fby); FY[1] = pk_fma(f2{fy.z, fy.w}, iy, fby);
+        NZ[0] = pk_fma(f2{nz.x, nz.y}, iz, nbz); NZ[1] = pk_fma(f2{nz.z, nz.w}, iz, nbz);
+        FZ[0] = pk_fma(f2{fz.x, fz.y}, iz, fbz); FZ[1] = pk_fma(f2{fz.z, fz.w}, iz, fbz);
+      }
+      const uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
+      float tn[4];
+      uint64_t cm[4];
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+          const int c = 2 * q + e;
+          const float TN = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
+          const float TF = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
+          const bool hit = in && fmaf(TN, 1.0f - 0x1p-19f, -0x1p-100f) <= TF && cc[c] != rpl::ENTRY_EMPTY;
+          tn[c] = hit ? TN : __builtin_huge_valf();
+          cm[c] = __ballot(hit);
+        }
+      }
+      // nearest first in the order of the mask's first lane (children it misses after the ones it hits)
+      const int lead = __builtin_ctzll(m);
+      float lt[4];
+      uint32_t ce[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tn[c]), lead));
+        lt[c] = !cm[c] ? __builtin_inff() : (v == __builtin_inff() ? 0x1.fffffep127f : v);  // others' hits after the lead's
+        ce[c] = __builtin_amdgcn_readfirstlane(cc[c]);
+      }
+#define RPK_PSWAP(a, b)                                                                 \
+      if (lt[b] < lt[a]) {                                                              \
+        const float t_ = lt[a]; lt[a] = lt[b]; lt[b] = t_;                              \
+        const uint32_t e_ = ce[a]; ce[a] = ce[b]; ce[b] = e_;                           \
+        const uint64_t m_ = cm[a]; cm[a] = cm[b]; cm[b] = m_;                           \
+      }
+      RPK_PSWAP(0, 1) RPK_PSWAP(2, 3) RPK_PSWAP(0, 2) RPK_PSWAP(1, 3) RPK_PSWAP(1, 2)
+#undef RPK_PSWAP
+      // push the farther children with lanes, far first; take the nearest
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        if (cm[c]) {
+          if (sp < cap) {
+            if (lane == 0) {
+              stk_e[sp] = ce[c];
+              stk_m[sp] = cm[c];
+            }
+            sp++;
+          } else {
+            overflow = true;
+          }
+        }
+      }
+      if (cm[0]) {
+        cur = ce[0];
+        m = cm[0];
+        continue;
+      }
+    } else if (m != 0) {
+      // a leaf: the exact f64 tests of its primitives by the mask's lanes
+      const uint32_t k0 = cur & rpl::LEAF_FIRST_MASK, n = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
+      for (uint32_t k = k0; k < k0 + n; k++) {
+        if (in) {
+          DIAG(if (td) td->tests++;)
+          prim_test(S, k, o, d, tmin, best, ts);
+        }
+      }
+      best32 = f32_up(best);
+    }
+    if (sp == 0) break;
+    --sp;
+    cur = __builtin_amdgcn_readfirstlane(stk_e[sp]);
+    const uint64_t mm = stk_m[sp];
+    m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(mm >> 32)) << 32) |
+        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)mm);
+  }
+  ts.best = best;
+  ts.cur = rpl::ENTRY_EMPTY;
+  ts.leaf = 0u;
+}
+
 // Hit record of the closest primitive (hittable.rs:59-62, 103-107).
 struct Surf {
   V3 p, n;

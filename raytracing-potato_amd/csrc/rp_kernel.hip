@@ -454,21 +454,29 @@ __global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
     DIAG(const uint32_t v0 = td.visits;)
     DIAG({ const uint64_t t = stamp(); c_setup += t - t_prev; t_prev = t; })
     const KScene S = load_scene(A);
-    const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + lane) * (S.stack_depth - S.lds_depth) : 0u;
     TravState ts;
     trav_begin<NF>(S, o, d, RAY_EPSILON, INF, ts);
     Ray32 r;
     setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
-    bool done = !valid || trav_done(ts);
-    while (__ballot(!done) != 0) {
-      if (!done) {
-        DIAG(d_steps += lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()) ? 1u : 0u;)
+    if constexpr (NF != rpl::NODES_W8) {
+      // 4-wide trees: one packet traversal for the wave (a stack of entry + lane-mask pairs at the front of the LDS)
+      lds_u32* se = (lds_u32*)lds_stack;
+      lds_u64* sm = (lds_u64*)(lds_stack + ((S.stack_depth + 1u) & ~1u));
+      DIAG(d_steps++;)
+      packet_traverse<NF>(S, se, sm, S.stack_depth, __ballot(valid), r, o, d, RAY_EPSILON, ts, overflow DIAG(, &td));
+    } else {
+      const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + lane) * (S.stack_depth - S.lds_depth) : 0u;
+      bool done = !valid || trav_done(ts);
+      while (__ballot(!done) != 0) {
+        if (!done) {
+          DIAG(d_steps += lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()) ? 1u : 0u;)
 #ifdef RPK_DIAG
-        trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
+          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
 #else
-        trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
+          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
 #endif
-        done = trav_done(ts);
+          done = trav_done(ts);
+        }
       }
     }
     DIAG({ const uint64_t t = stamp(); c_trav += t - t_prev; t_prev = t; })
@@ -503,7 +511,8 @@ __global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
 }
 
 int launch_primary(const KScene& s, const KParams& p, uint64_t* counters, uint32_t* queue, int grid, void* stream) {
-  const size_t lds = (size_t)s.lds_depth * BLOCK * sizeof(uint32_t);
+  // the per-lane stack (8-wide trees) or the packet stack: stack_depth entries of 4 + 8 bytes
+  const size_t lds = std::max((size_t)s.lds_depth * BLOCK * sizeof(uint32_t), (size_t)(s.stack_depth + 2) * 12);
   const bool spill = s.lds_depth < s.stack_depth;
   KArgs a;
   a.S = s;

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "9da3ce01dfd95a72"
+#define RP_BUILD_ID "86181f92ded443df"
