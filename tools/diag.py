@@ -16,7 +16,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=32)
-    ap.add_argument("--shards", type=int, default=1, help="render shard 0 of N (per-rank work of an N-GPU run)")
+    ap.add_argument("--shards", type=int, default=1, help="render shard --shard of N (per-rank work of an N-GPU run)")
+    ap.add_argument("--shard", type=int, default=0)
+    ap.add_argument("--balanced", action="store_true", help="the balanced tile plan (RP_SHARD_BALANCED), learned from a "
+                                                            "whole-frame render of every shard first (tools/shard_scaling.py)")
     ap.add_argument("--sps", type=int, default=0, help="samples_per_stream (the RNG contract; 0 = 32, >= spp: one "
                                                        "stream per pixel)")
     ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value")
@@ -26,13 +29,18 @@ def main():
     from rtpotato import _ffi as F, scenes
     from rtpotato.render import DeviceScene
     scene, params = scenes.config_scene(a.config)
-    params = replace(params, spp=a.spp, shard=0, num_shards=a.shards, samples_per_stream=a.sps)
+    params = replace(params, spp=a.spp, shard=a.shard, num_shards=a.shards, samples_per_stream=a.sps,
+                     shard_map=1 if a.balanced else 0)
     opts = {}
     for kv in a.opt:
         k, v = kv.split("=", 1)
         opts[k] = float(v) if k == "cost_traverse" else (v if not v.lstrip("-").isdigit() else int(v))
     ds = DeviceScene(scene, options=opts)
     ds.render(replace(params, spp=1))  # warm
+    if a.balanced and a.shards > 1:
+        sys.path.insert(0, os.path.join(REPO, "tools"))
+        from shard_scaling import learned_table
+        ds.set_tile_costs(params, learned_table(ds, params, a.shards), a.shards)
     NDIAG = 416  # rp_kernel.h DIAG_N
     buf = (ctypes.c_uint64 * NDIAG)()
     F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))

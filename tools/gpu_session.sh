@@ -33,14 +33,15 @@ echo "start $(date +%T)" > $P
 step() { echo "$1 $(date +%T)" >> $P; }
 made() { echo "$1: $2" >> $M; }  # output file: command
 frames() { case $1 in C5) echo "3 1" ;; C4) echo "4 1" ;; *) echo "10 2" ;; esac; }
-pmc() {  # lib cfg name counters...
+pmc() {  # lib cfg name counters...   (PMC_BENCH_ARGS: the bench frames, default one frame; PMC_LABEL: output suffix)
   local lib=$1 cfg=$2 name=$3; shift 3
-  local out=gpurun_out/${TAG}_${cfg}_pmc_$name cmd
-  cmd="rocprofv3 --pmc $* -- python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline"
+  local out=gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_pmc_$name cmd
+  local ba=${PMC_BENCH_ARGS:---steps 1 --warmup 0}
+  cmd="rocprofv3 --pmc $* -- python3 bench.py --config $cfg $ba --no-cpu-baseline --contract-steps 0"
   step "pmc $cfg $name"
   made "$out" "RP_LIB=$lib $cmd"
   RP_LIB=$lib timeout -s KILL 300 rocprofv3 --pmc "$@" -d $out -o run --output-format csv -- \
-    python3 bench.py --config $cfg --steps 1 --warmup 0 --no-cpu-baseline > $out.json 2> $out.err
+    python3 bench.py --config $cfg $ba --no-cpu-baseline --contract-steps 0 > $out.json 2> $out.err
 }
 LIB=raytracing-potato_amd/lib/librp.so
 libpath() { [ "$1" = main ] && echo $LIB || echo raytracing-potato_amd/lib/librp_$1.so; }
@@ -98,14 +99,14 @@ for s in ${STEPS:-tests}; do
       pmc $LIB $cfg fetch FETCH_SIZE &&
       pmc $LIB $cfg write WRITE_SIZE &&
       pmc $LIB $cfg l2 TCC_HIT_sum TCC_MISS_sum || exit 1
-      lc=$(echo $cfg | tr A-Z a-z)
+      lc=$(echo $cfg | tr A-Z a-z)${PMC_LABEL:+_$PMC_LABEL}
+      pre=gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_pmc
       made gpurun_out/${TAG}_${lc}_roofline.json "python3 tools/roofline.py --config $cfg over the six pmc passes above"
-      python3 tools/roofline.py --config $cfg --bench gpurun_out/${TAG}_${cfg}_pmc_sq.json \
-        $([ -f gpurun_out/${TAG}_${cfg}_diag.json ] && echo --diag gpurun_out/${TAG}_${cfg}_diag.json) \
+      python3 tools/roofline.py --config $cfg --bench ${pre}_sq.json ${PMC_BENCH_ARGS:+--all-dispatches} \
+        $([ -f gpurun_out/${TAG}_${cfg}_diag.json ] && [ -z "${PMC_LABEL:-}" ] && echo --diag gpurun_out/${TAG}_${cfg}_diag.json) \
         --out gpurun_out/${TAG}_${lc}_roofline.json \
-        gpurun_out/${TAG}_${cfg}_pmc_sq gpurun_out/${TAG}_${cfg}_pmc_mix64 gpurun_out/${TAG}_${cfg}_pmc_mix32 \
-        gpurun_out/${TAG}_${cfg}_pmc_fetch gpurun_out/${TAG}_${cfg}_pmc_write gpurun_out/${TAG}_${cfg}_pmc_l2 \
-        > gpurun_out/${TAG}_${cfg}_roofline.log 2>&1 || exit 1 ;;
+        ${pre}_sq ${pre}_mix64 ${pre}_mix32 ${pre}_fetch ${pre}_write ${pre}_l2 \
+        > gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_roofline.log 2>&1 || exit 1 ;;
     units_*)  # the longest measured unit per tile (product build): tools/unit_times.py
       cfg=${s#units_}
       step "units $cfg"

@@ -37,9 +37,10 @@ SIMDS = 1024
 PEAK_CLOCK = 2.4e9
 
 
-def read_pass(d):
+def read_pass(d, all_dispatches=False):
     """{counter: value} of the frame kernel's dispatch in one pass (rows of a dispatch summed), and its
-    duration in ns."""
+    duration in ns.  all_dispatches: every frame-kernel dispatch of the pass summed (frames in flight), the mean
+    duration, and their count."""
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
@@ -51,10 +52,16 @@ def read_pass(d):
             dur[did] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
     if not per:
         raise SystemExit(f"no {KERNEL} rows under {d}")
+    if all_dispatches:
+        tot = collections.defaultdict(float)
+        for v in per.values():
+            for k, x in v.items():
+                tot[k] += x
+        return dict(tot), sum(dur.values()) / len(dur), len(per)
     if len(per) != 1:
         raise SystemExit(f"{d}: {len(per)} frame-kernel dispatches (expected one: --steps 1 --warmup 0)")
     did = next(iter(per))
-    return dict(per[did]), dur[did]
+    return dict(per[did]), dur[did], 1
 
 
 def lanes_per_ray(diag, region):
@@ -90,15 +97,22 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--diag", help="tools/diag.py record of the same build and frame")
     ap.add_argument("--node-bytes", type=int, default=0, help="bytes one node visit loads (0: C5 -> 64 (q8), else 112)")
+    ap.add_argument("--all-dispatches", action="store_true",
+                    help="sum every frame-kernel dispatch of each pass (a run of several frames, e.g. shards in flight); "
+                         "per-ray figures use rays_per_frame x dispatches")
     ap.add_argument("passes", nargs="+")
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
     rays = float(bench["config"]["rays_per_frame"])
-    c, durs = {}, {}
+    c, durs, ndisp = {}, {}, set()
     for d in a.passes:
-        vals, ns = read_pass(d)
+        vals, ns, nd = read_pass(d, a.all_dispatches)
         c.update(vals)
         durs[os.path.basename(d.rstrip("/"))] = ns
+        ndisp.add(nd)
+    if len(ndisp) != 1:
+        raise SystemExit(f"passes saw different dispatch counts {sorted(ndisp)}")
+    rays *= ndisp.pop()
     rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     build = bench.get("roofline", {}).get("build_id")
     rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays, "counters": c,
@@ -121,7 +135,7 @@ def main():
             "active_inst_any": round(c["SQ_ACTIVE_INST_ANY"] / w, 4),
             "closure": round((c["SQ_WAIT_ANY"] + c["SQ_WAIT_INST_ANY"] + c["SQ_ACTIVE_INST_ANY"]) / w, 4),
             "waves": c.get("SQ_WAVES")}
-    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c:
+    if "GRBM_GUI_ACTIVE" in c and "SQ_INSTS_VALU" in c and not a.all_dispatches:
         ns = next((v for k, v in durs.items() if v > 0), None)
         if ns:
             clk = c["GRBM_GUI_ACTIVE"] / 8.0 / (ns * 1e-9)
