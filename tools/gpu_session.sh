@@ -84,9 +84,9 @@ for s in ${STEPS:-tests}; do
     trace_*)
       cfg=${s#trace_}; read st wu <<< "$(frames $cfg)"
       step "trace $cfg"
-      made gpurun_out/${TAG}_${cfg}_trace "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline ${BENCH_ARGS:-}"
+      made gpurun_out/${TAG}_${cfg}_trace "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 ${BENCH_ARGS:-}"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${cfg}_trace -o run --output-format csv -- \
-        python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline ${BENCH_ARGS:-} \
+        python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 ${BENCH_ARGS:-} \
         > gpurun_out/${TAG}_${cfg}_bench_under_rocprof.json 2> gpurun_out/${TAG}_${cfg}_trace.err || exit 1 ;;
     pmc_*)
       cfg=${s#pmc_}
