@@ -210,6 +210,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 3 on several)")
+    ap.add_argument("--frames-per-launch", type=int, default=1,
+                    help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
+                         "the frame of seed + f * B * W * H); a step is still one frame, --steps must be a multiple")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic, one GPU: render only shard --shard of this many (the per-rank work of an N-GPU "
                          "run), no gather; not a bench line")
@@ -223,6 +226,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[],
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
+    L = args.frames_per_launch
+    if L < 1 or args.steps % L or (args.warmup and args.warmup % L):
+        ap.error("--steps and --warmup must be multiples of --frames-per-launch")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -273,10 +279,10 @@ def main():
     streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
     wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
     for w in wss:
-        ds.reserve(sp, w)  # batch sums + gather staging: nothing is allocated inside the timed loop
+        ds.reserve_frames(sp, L, w)  # batch sums + gather staging: nothing is allocated inside the timed loop
     from rtpotato.scene import shard_slot_count
     nslots = shard_slot_count(sp)
-    bufs = [torch.zeros(3 * max(1, nslots), dtype=torch.float64, device=dev) for _ in range(F_)]
+    bufs = [torch.zeros(3 * max(1, nslots) * L, dtype=torch.float64, device=dev) for _ in range(F_)]
     ctrs = [torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev) for _ in range(F_)]
     freed = [None] * F_  # event: the gather of the buffer's previous frame is done
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
@@ -291,7 +297,10 @@ def main():
             st.wait_event(freed[i])
         if k_start is not None:
             k_start.record(st)
-        ds.render_device(spx, bufs[i], ctrs[i], stream=st, workspace=wss[i])
+        if L == 1:
+            ds.render_device(spx, bufs[i], ctrs[i], stream=st, workspace=wss[i])
+        else:  # L frames in one launch: the lanes a frame's tail leaves run the next frame's units
+            ds.render_frames_device(spx, L, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         if k_end is not None:
             k_end.record(st)
         if st is not main_stream:
@@ -301,29 +310,32 @@ def main():
         if args.shard_of:
             freed[i] = done if st is not main_stream else None
             return
-        # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks), on the main stream
-        ds.frame_gather(comm, spx, bufs[i], frame_bgra=frame, counters=ctrs[i], stream=main_stream,
-                        workspace=wss[i])
+        # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks, once), on the main stream
+        n3 = 3 * max(1, nslots)
+        for f in range(L):
+            ds.frame_gather(comm, spx, bufs[i][f * n3:(f + 1) * n3], frame_bgra=frame,
+                            counters=ctrs[i] if f == 0 else None, stream=main_stream, workspace=wss[i])
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 
-    for w in range(args.warmup):
+    for w in range(args.warmup // L):
         step()
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup {w} done")
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    launches = args.steps // L  # a step is one frame; one launch renders L of them
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(launches):
         step(starts[k], ends[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kernel_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps / 1e3
+    kernel_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps / 1e3  # per frame
     if F_ > 1:
         # overlapping frames: a frame's events also span the neighbour frames' work, so the kernel rate is
         # priced on the per-frame throughput time instead
@@ -332,7 +344,7 @@ def main():
     bad = [c[3] for c in cs if c[3] != 0]
     if bad:  # RP_STATUS_* bits (OR-ed over the ranks by the gather): stack overflow, plan mismatch
         raise RuntimeError(f"render kernel reported status {bad}: frame refused")
-    rays_step, samples_step = cs[0][0], cs[0][1]  # summed over the ranks by rp_frame_gather
+    rays_step, samples_step = cs[0][0] / L, cs[0][1] / L  # summed over the ranks by rp_frame_gather, per frame
     tmax = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -347,16 +359,17 @@ def main():
     if csteps > 0 and params.spp > (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM):
         pc = replace(params, samples_per_stream=params.spp)
         spc = shard_params(pc, rank, world)
+        csteps = -(-csteps // L) * L
         for w in wss:
-            ds.reserve(spc, w)
-        for _ in range(F_):  # one frame per in-flight workspace: each learns this contract's tile costs
+            ds.reserve_frames(spc, L, w)
+        for _ in range(F_):  # one launch per in-flight workspace: each learns this contract's tile costs
             step(spx=spc)
             torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        for _ in range(csteps):
+        for _ in range(csteps // L):
             step(spx=spc)
         torch.cuda.synchronize()
         if world > 1:
@@ -367,7 +380,7 @@ def main():
         cc = [c.cpu().tolist() for c in ctrs]
         if any(c[3] != 0 for c in cc):
             raise RuntimeError(f"render kernel reported status {[c[3] for c in cc]} under the one-stream contract")
-        crays = cc[0][0]
+        crays = cc[0][0] // L
         contract = {"samples_per_stream": params.spp, "steps": csteps, "warmup": F_,
                     "ms_per_step": round(float(tc.item()) / csteps * 1e3, 3),
                     "value": round(crays * csteps / float(tc.item()) / 1e6, 3), "unit": "Mrays/s",
@@ -459,7 +472,7 @@ def main():
                        "max_bounce": params.max_bounce, "seed": params.seed,
                        "samples_per_stream": params.samples_per_stream or 32, "tile": [params.tile_w, params.tile_h],
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
-                       "frames_in_flight": F_,
+                       "frames_in_flight": F_, "frames_per_launch": L,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
                        "msamples_per_s": round(samples_step * args.steps / elapsed_max / 1e6, 1),

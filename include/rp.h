@@ -368,6 +368,25 @@ int rp_workspace_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_r
                             uint32_t* costs, uint32_t n);
 int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                                 const uint32_t* costs, uint32_t ranks);
+/* Several frames in ONE persistent launch (ABI v8).  Frame f = 0 .. n_frames - 1 is exactly the frame of `params` with
+ * its sample batches numbered f * B .. f * B + B - 1, B = ceil(spp / samples_per_stream) -- i.e. the frame rp_render_device
+ * renders with params.seed + f * B * width * height (the RNG contract's seeds of batches past the frame's own): n_frames
+ * independent frames of the same scene, camera and sampling.  The queues hand out the frames' units one frame after
+ * the other, so the lanes a frame's tail leaves take the next frame's units at once instead of idling in sparse waves
+ * (a frame's tail: ~4 % of a C3 frame, ~20 % of an 8-way C3 shard).  d_shard_rgb holds n_frames shard
+ * buffers back to back (3 x rp_shard_pixel_count doubles each), d_shard_fg (nullable) n_frames x pixel count floats;
+ * d_counters: the n_frames frames' counts summed (status bits OR-ed).  The workspace must be reserved for n_frames
+ * (rp_workspace_reserve_frames; it also reserves what rp_workspace_reserve does).  The shard's tiles (a balanced plan)
+ * and their order are made once for the launch: from the workspace's learned cost table, or from a probe of frame 0 --
+ * a probed plan follows its seed, so a balanced shard of frame f > 1 may hold other tiles than rp_render_device's frame
+ * of that seed would (the pixels are the same; rp_workspace_tile_map gives the launch's deal).  Megakernel engine only;
+ * the coherent primary pass and the learned unit order do not apply.  n_frames <= RP_MAX_FRAMES. */
+#define RP_MAX_FRAMES 64
+int rp_workspace_reserve_frames(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                                uint32_t n_frames);
+int rp_render_frames_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
+                               const rp_render_params* params, uint32_t n_frames, double* d_shard_rgb,
+                               float* d_shard_fg, uint64_t* d_counters, void* stream);
 /* How the last render enqueued with `workspace` (NULL = the scene's) was scheduled (ABI v8): RP_FRAME_* bits.
  * Host state only (no device synchronisation); results never depend on any of it. */
 enum {

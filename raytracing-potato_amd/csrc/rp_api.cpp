@@ -454,12 +454,13 @@ int grow(A*& a, B*& b, uint64_t& cap, uint64_t units, uint64_t na, uint64_t nb, 
 
 // Grow the workspace's reservation for renders of params' shape (synchronous): the multi-batch sums and,
 // with `gather`, the staging and receive buffers of rp_frame_gather.
-int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gather) {
+int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gather, uint32_t n_frames = 1) {
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
   DeviceGuard g(s->device);
-  const uint64_t units = t.nbatch > 1 ? t.n_slots * t.nbatch : 0;
+  const uint64_t units = t.nbatch > 1 ? t.n_slots * t.nbatch * n_frames : 0;
   if ((rc = grow(w->d_partial, w->d_partial_hits, w->partial_units, units, 3, 1, "sample-batch workspace"))) return rc;
   // the coherent primary pass's hints: 4 bytes per shard slot and sample (C3 2.1 GB, C5 17 GB of the 288 GB HBM); a
   // frame past PRIM_HINT_MAX_BYTES renders without the pass
@@ -716,9 +717,12 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
 
 // The render of one shard on `stream` (rp_render_device_ws's body).
 int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
-                 float* d_fg, uint64_t* d_counters, void* stream) {
+                 float* d_fg, uint64_t* d_counters, void* stream, uint32_t n_frames = 1) {
   if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
   if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
+  if (n_frames > 1 && s->opt.engine != RP_ENGINE_MEGAKERNEL)
+    return fail(RP_EINVAL, "several frames per launch: megakernel engine only");
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
@@ -735,8 +739,8 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   if (t.n_slots == 0) return RP_OK;
   if (p->spp == 0) {
     // main.rs:86-87 with num_samples = 0: (0,0,0) / 0 and 0 / 0 are NaN; all-ones bits are a NaN.
-    RP_HIP(hipMemsetAsync(d_rgb, 0xff, sizeof(double) * 3 * t.n_slots, st));
-    if (d_fg) RP_HIP(hipMemsetAsync(d_fg, 0xff, sizeof(float) * t.n_slots, st));
+    RP_HIP(hipMemsetAsync(d_rgb, 0xff, sizeof(double) * 3 * t.n_slots * n_frames, st));
+    if (d_fg) RP_HIP(hipMemsetAsync(d_fg, 0xff, sizeof(float) * t.n_slots * n_frames, st));
     return RP_OK;
   }
   rpk::KParams kp{};
@@ -761,7 +765,10 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.trav_threshold = s->opt.trav_threshold;
   kp.spp_batch = t.sps;  // the RNG contract's samples per stream (rp_render_params.samples_per_stream)
   kp.nbatch = t.nbatch;
-  kp.n_queue = t.n_slots * kp.nbatch;
+  kp.n_queue = t.n_slots * kp.nbatch * n_frames;  // every frame's units
+  kp.n_frames = n_frames;
+  kp.dv_tiles = rpk::make_div32(std::max(1u, t.n_shard_tiles));
+  kp.out_stride = 3 * t.n_slots;
   // Per-XCD queues (rp.h RP_QUEUES_*): groups of blocks blockIdx mod 8 share an XCD (MI355X_MICROARCH.md,
   // observed round-robin dispatch; speed only -- any placement gives the same image).  The stage-split engine
   // keeps the single queue.
@@ -784,7 +791,9 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.dv_chunk = rpk::make_div32(kp.queue_chunk);
   if (kp.nbatch > 1) {
     if (kp.n_queue > w->partial_units)
-      return fail(RP_EINVAL, "workspace not reserved for this frame's sample batches: call rp_workspace_reserve");
+      return fail(RP_EINVAL, n_frames > 1 ? "workspace not reserved for these frames' sample batches: call "
+                                            "rp_workspace_reserve_frames"
+                                          : "workspace not reserved for this frame's sample batches: call rp_workspace_reserve");
     kp.partial = w->d_partial;
     kp.partial_hits = w->d_partial_hits;
   }
@@ -808,6 +817,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     rpk::KParams pk = kp;
     pk.probe = 1;
     pk.spp = 1;
+    pk.n_frames = 1;
     pk.shard = shard;
     pk.nshards = nshards;
     pk.n_shard_tiles = n_tiles;
@@ -898,7 +908,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // 64 before the path loop, which then starts every sample at its closest hit.  Needs the workspace's hint buffer
   // (rp_workspace_reserve); without it, or with a lens, camera rays traverse in the path loop.
   const uint64_t n_hints = t.n_slots * p->spp;
-  if (primary_on(s) && cam->lens_radius == 0.0 && w->d_hint && n_hints <= w->hint_cap) {
+  if (n_frames == 1 && primary_on(s) && cam->lens_radius == 0.0 && w->d_hint && n_hints <= w->hint_cap) {
     kp.prim_quads_x = (t.tw + 1) / 2;
     kp.prim_sgroups = (p->spp + rpk::PRIM_SAMPLES - 1) / rpk::PRIM_SAMPLES;
     const uint64_t per_tile = (uint64_t)kp.prim_quads_x * ((t.th + 1) / 2) * kp.prim_sgroups;
@@ -923,7 +933,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   // every render stores its units' durations for the next one.
   const uint64_t n_units = t.n_slots * t.nbatch;
   const uint32_t ugeom[8] = {p->width, p->height, t.tw, t.th, p->spp, t.sps, t.shard, t.shards};
-  const bool ufit = units_on(s) && w->d_ucost && n_units <= w->ucost_cap && (!t.balanced || t.shards == 1);
+  const bool ufit = n_frames == 1 && units_on(s) && w->d_ucost && n_units <= w->ucost_cap && (!t.balanced || t.shards == 1);
   if (ufit && w->ucost_valid && std::memcmp(ugeom, w->ucost_geom, sizeof ugeom) == 0) {
     int e = rpk::launch_unit_order(w->d_ucost, n_units, w->d_ukey, w->d_ukey2, w->d_usort, w->usort_bytes, w->d_uorder,
                                    stream);
@@ -945,8 +955,14 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
               : rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
   if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
   if (kp.nbatch > 1) {
-    e = rpk::launch_reduce_batches(kp, d_rgb, d_fg, stream);
-    if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
+    for (uint32_t f = 0; f < n_frames; f++) {  // each frame's batch sums, added in batch order
+      rpk::KParams kf = kp;
+      kf.partial = kp.partial + 3 * (uint64_t)f * t.n_slots * kp.nbatch;
+      kf.partial_hits = kp.partial_hits + (uint64_t)f * t.n_slots * kp.nbatch;
+      e = rpk::launch_reduce_batches(kf, d_rgb + (uint64_t)f * kp.out_stride, d_fg ? d_fg + (uint64_t)f * t.n_slots : nullptr,
+                                     stream);
+      if (e != 0) return fail(RP_EHIP, std::string("reduce launch: ") + hipGetErrorString((hipError_t)e));
+    }
   }
   // a whole frame on one device: its measured costs are the next frame's table (several ranks: the frame gather's)
   if (measure && t.shards == 1 && t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX) {
@@ -1263,6 +1279,20 @@ int rp_render_device(rp_scene* s, const rp_camera* cam, const rp_render_params* 
 int rp_render_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
                         float* d_fg, uint64_t* d_counters, void* stream) {
   return render_shard(s, w, cam, p, d_rgb, d_fg, d_counters, stream);
+}
+
+int rp_workspace_reserve_frames(rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t n_frames) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  return ws_reserve(s, w, p, true, n_frames);
+}
+
+int rp_render_frames_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,
+                               uint32_t n_frames, double* d_rgb, float* d_fg, uint64_t* d_counters, void* stream) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (!w) w = &s->ws0;
+  return render_shard(s, w, cam, p, d_rgb, d_fg, d_counters, stream, n_frames);
 }
 
 int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* out_rgb, float* out_fg,

@@ -1685,7 +1685,8 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
   // The queue a wave increments is wave-uniform (`tries` moves for the whole wave once any lane finds the
   // queue drained -- then it is drained for every lane), so the compiler folds the lanes' atomicAdd into one
   // wave atomic (ballot + mbcnt); a per-lane atomic on one word cost C3 +35 %.
-  const uint32_t G = max(A->P.queue_groups, 1u), K = A->P.n_shard_tiles;
+  // several frames per launch: n_frames x n_shard_tiles virtual tiles (rp_kernel.h KParams::n_frames)
+  const uint32_t G = max(A->P.queue_groups, 1u), K = A->P.n_shard_tiles * (PROBE ? 1u : A->P.n_frames);
   const uint32_t home = G > 1 ? blockIdx.x % G : 0u;
   for (uint32_t tries = 0;;) {
     uint32_t g = home + tries;
@@ -1714,6 +1715,11 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     // batch-major, ab32)
     const uint32_t local = PROBE ? rem / A->P.nbatch : RPK_UDIV(rem, dv_nbatch);
     batch = rem - local * A->P.nbatch;
+    if (!PROBE && A->P.n_frames > 1) {  // virtual tile -> frame f, its tile k; the unit carries its global batch
+      const uint32_t f = RPK_UDIV(k, dv_tiles);
+      k -= f * A->P.n_shard_tiles;
+      batch += f * A->P.nbatch;
+    }
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order
     slot = k * tile_px + local;                     // output slot: shard tile order (rp_shard_unpack)
     const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
@@ -1730,9 +1736,12 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
 RPK_INLINE uint64_t unit_seed(KArgsPtr A, uint32_t pi, uint32_t pj, uint32_t batch) {
   return A->P.seed + (uint64_t)batch * A->P.W * A->P.H + (uint64_t)pj * A->P.W + pi;
 }
+// The frame of a unit's (global) batch and its batch within the frame (several frames per launch: KParams::n_frames).
+RPK_INLINE uint32_t unit_frame(KArgsPtr A, uint32_t batch) { return A->P.n_frames > 1 ? RPK_UDIV(batch, dv_nbatch) : 0u; }
 // Samples in this unit's batch.
 RPK_INLINE uint32_t unit_spp(KArgsPtr A, uint32_t batch) {
-  return min(A->P.spp_batch, A->P.spp - batch * A->P.spp_batch);
+  const uint32_t b = batch - unit_frame(A, batch) * A->P.nbatch;
+  return min(A->P.spp_batch, A->P.spp - b * A->P.spp_batch);
 }
 
 // Camera::shoot (render.rs:32-52) from the jittered frame coordinates (ju, jv) and the UnitDisk sample (dx, dy): one

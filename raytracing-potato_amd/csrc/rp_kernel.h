@@ -125,6 +125,14 @@ struct KParams {
   const uint32_t* unit_order;
   uint32_t order_chunk;
   Div32 dv_ochunk, dv_tile_px;  // make_div32(order_chunk), make_div32(tw * th)
+  // Several frames in one launch (rp.h rp_render_frames_device_ws): frame f is the frame of these params whose sample
+  // batches are f * nbatch .. f * nbatch + nbatch - 1 of the RNG contract (seed + (f nbatch + b) W H + j W + i); the
+  // queues hand out n_frames x n_shard_tiles virtual tiles (frame f's tile k = f * n_shard_tiles + k), a unit carries its
+  // global batch f * nbatch + b, and frame f writes out + f * out_stride (out_fg + f * n_slots) or its batch sums at
+  // partial + 3 (f * n_slots + slot) * nbatch.  The lanes a frame's tail leaves take the next frame's units at once.
+  uint32_t n_frames;            // >= 1
+  Div32 dv_tiles;               // make_div32(n_shard_tiles)
+  uint64_t out_stride;          // doubles between frames' shard buffers (3 * n_slots)
 };
 
 // Cost-ordered tile scheduling.  A frame's tail (waves holding a few lanes that still finish the last

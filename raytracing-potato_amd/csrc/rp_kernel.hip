@@ -257,14 +257,18 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             atomicAdd(&A->P.tile_cost[k], r);
             atomicMax(&A->P.tile_cost[TILE_SORT_MAX + k], r);
           } else if (A->P.nbatch == 1) {
+            // (the unit's frame: its global batch, nbatch being 1)
             const double spp = (double)A->P.spp;
-            double* out = A->out;
+            double* out = A->out + (uint64_t)batch * A->P.out_stride;
             out[3 * (uint64_t)slot + 0] = sum_x / spp;
             out[3 * (uint64_t)slot + 1] = sum_y / spp;
             out[3 * (uint64_t)slot + 2] = sum_z / spp;
-            if (A->out_fg) A->out_fg[slot] = (float)((double)hits / spp);
+            if (A->out_fg) A->out_fg[(uint64_t)batch * A->P.n_slots + slot] = (float)((double)hits / spp);
           } else {  // one batch of several: its sum, reduced in batch order by reduce_batches
-            const uint64_t u = (uint64_t)slot * A->P.nbatch + batch;
+            // (frame f's sums follow frame f - 1's: index (f n_slots + slot) nbatch + b = slot nbatch + global batch
+            // + f (n_slots - 1) nbatch)
+            const uint64_t u = (uint64_t)slot * A->P.nbatch + batch +
+                               (uint64_t)unit_frame(A, batch) * (A->P.n_slots - 1) * A->P.nbatch;
             double* part = A->P.partial;
             part[3 * u + 0] = sum_x;
             part[3 * u + 1] = sum_y;
@@ -283,7 +287,7 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
               meas_k = slot / (A->P.tw * A->P.th);
             }
           }
-          ended_pixel = batch == 0;
+          ended_pixel = batch == unit_frame(A, batch) * A->P.nbatch;  // the pixel's first batch of its frame
           DIAG(if (!PROBE) {
             const uint32_t b = tbin(t_pix);
             atomicAdd(&A->diag[128 + b], (unsigned long long)(lane_rays - rays_pix));

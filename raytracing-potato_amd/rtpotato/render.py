@@ -111,6 +111,12 @@ class DeviceScene:
         p = params.to_c()
         F.check(F.rp().rp_workspace_reserve(self.handle, workspace.handle if workspace else None, ctypes.byref(p)))
 
+    def reserve_frames(self, params: RenderParams, n_frames: int, workspace: "Workspace | None" = None) -> None:
+        """rp_workspace_reserve_frames: rp_workspace_reserve, plus the batch sums of n_frames frames per launch."""
+        p = params.to_c()
+        F.check(F.rp().rp_workspace_reserve_frames(self.handle, workspace.handle if workspace else None,
+                                                   ctypes.byref(p), n_frames))
+
     def tile_map(self, params: RenderParams, workspace: "Workspace | None" = None) -> np.ndarray:
         """rp_workspace_tile_map: the frame's deal order (shard s's k-th tile = map[s + k * num_shards]) -- the
         balanced plan the last render of this frame in `workspace` made, or the interleave's identity."""
@@ -181,6 +187,25 @@ class DeviceScene:
             F.check(F.rp().rp_render_device_ws(self.handle, workspace.handle, ctypes.byref(cam), ctypes.byref(p),
                                                out.data_ptr(), fgp, counters.data_ptr(),
                                                ctypes.c_void_p(s.cuda_stream)))
+
+    def render_frames_device(self, params: RenderParams, n_frames: int, out, counters, fg=None, camera=None,
+                             stream=None, workspace: "Workspace | None" = None) -> None:
+        """rp_render_frames_device_ws: n_frames frames in one launch -- frame f is render_device's frame of `params` with
+        seed + f * ceil(spp / samples_per_stream) * width * height.  out: torch f64, >= n_frames * 3 * shard_slot_count
+        elements (frame f at f * 3 * slots); fg: n_frames * slots floats or None; counters: the frames' sums.  The
+        workspace needs reserve_frames(params, n_frames) when the frame has more than one sample batch."""
+        import torch
+        cam = (camera or self.scene.camera).to_c()
+        p = params.to_c()
+        n = shard_slot_count(params)
+        assert out.dtype == torch.float64 and out.is_cuda and out.numel() >= 3 * n * n_frames
+        assert fg is None or fg.numel() >= n * n_frames
+        assert counters.dtype == torch.int64 and counters.numel() >= F.RP_COUNTERS_LEN
+        s = stream if stream is not None else torch.cuda.current_stream(out.device)
+        F.check(F.rp().rp_render_frames_device_ws(self.handle, workspace.handle if workspace else None,
+                                                  ctypes.byref(cam), ctypes.byref(p), n_frames, out.data_ptr(),
+                                                  fg.data_ptr() if fg is not None else None, counters.data_ptr(),
+                                                  ctypes.c_void_p(s.cuda_stream)))
 
     def to_bgra8(self, params: RenderParams, shard_rgb, out, stream=None) -> None:
         """Output stage on the device (rp_shard_to_bgra8): the shard's linear f64 RGB (`shard_rgb`, torch

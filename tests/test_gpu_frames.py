@@ -1,0 +1,153 @@
+"""Several frames per persistent launch (include/rp.h rp_render_frames_device_ws, rp_device.h fetch_pixel).
+
+Frame f of a launch of n_frames is, by the contract, the frame rp_render_device renders with seed + f * B * W * H
+(B = the frame's sample batches): every unit is seeded by its pixel and its global batch, so the schedule -- units of
+frames f and f + 1 in one wave, a frame's tail run by the next frame's lanes -- cannot change a pixel.  Each frame must
+equal its single-frame render bit for bit, the counters must be the frames' sums, and one frame is checked against the
+oracle directly.  Cases: one stream per pixel (B = 1) and multi-batch frames (B > 1, partial sums reduced per frame),
+ragged tiles, shards of the interleave and of the balanced plan, spp 0 (NaN frames), argument errors.
+"""
+import numpy as np
+import pytest
+from dataclasses import replace
+
+from parity import assert_parity, compare, oracle_render
+
+pytestmark = pytest.mark.gpu
+
+
+def _scene(name, w, h, spp, **kw):
+    from rtpotato import scenes
+    from rtpotato.scene import RenderParams
+    sc = scenes.configure(scenes.CATALOGUE[name](**kw), w, h)
+    return sc, RenderParams(w, h, spp, 8, scenes.DEFAULT_SEED)
+
+
+def _nbatch(p):
+    from rtpotato import _ffi as F
+    sps = p.samples_per_stream or F.RP_SAMPLES_PER_STREAM
+    return max(1, -(-p.spp // sps)) if p.spp else 1
+
+
+def _frames_vs_singles(ds, p, n_frames, table=None):
+    """(multi-frame shard buffers, single-frame shard buffers) as numpy arrays of (n_frames, slots, 3), fg the same,
+    and both counter blocks."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.scene import shard_slot_count
+    n = shard_slot_count(p)
+    dev = torch.device("cuda", 0)
+    w = ds.workspace()
+    ds.reserve_frames(p, n_frames, w)
+    if table is not None:
+        ds.set_tile_costs(p, table, p.num_shards, w)
+    out = torch.full((n_frames * 3 * max(n, 1),), -1.0, dtype=torch.float64, device=dev)
+    fg = torch.full((n_frames * max(n, 1),), -1.0, dtype=torch.float32, device=dev)
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+    ds.render_frames_device(p, n_frames, out, ctr, fg=fg, workspace=w)
+    torch.cuda.synchronize()
+    singles, sfg, sctr = [], [], torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+    stride = _nbatch(p) * p.width * p.height
+    for f in range(n_frames):
+        o = torch.full((3 * max(n, 1),), -1.0, dtype=torch.float64, device=dev)
+        g = torch.full((max(n, 1),), -1.0, dtype=torch.float32, device=dev)
+        c = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+        ds.render_device(replace(p, seed=p.seed + f * stride), o, c, fg=g, workspace=w)
+        torch.cuda.synchronize()
+        singles.append(o[:3 * n].cpu().numpy())
+        sfg.append(g[:n].cpu().numpy())
+        sctr[:3] += c[:3]
+        sctr[3] |= c[3]
+    w.close()
+    multi = out[:n_frames * 3 * n].cpu().numpy().reshape(n_frames, n, 3)
+    mfg = fg[:n_frames * n].cpu().numpy().reshape(n_frames, n)
+    return multi, np.stack(singles).reshape(n_frames, n, 3), mfg, np.stack(sfg), ctr.cpu().numpy(), sctr.cpu().numpy()
+
+
+def _assert_same(multi, single, mfg, sfg, ctr, sctr):
+    assert np.array_equal(multi.view(np.uint64), single.view(np.uint64))
+    assert np.array_equal(mfg.view(np.uint32), sfg.view(np.uint32))
+    assert ctr.tolist() == sctr.tolist(), (ctr, sctr)
+    assert ctr[3] == 0
+
+
+@pytest.mark.parametrize("sps", [48, 0, 7, 16])
+@pytest.mark.parametrize("n_frames", [1, 3])
+def test_frames_equal_single_renders(gpu, sps, n_frames):
+    """bunny_full 72 x 40 at 48 spp on 16 x 16 tiles (ragged last row and column): one stream per pixel (B = 1), the
+    default 32 (B = 2, a short last batch), 7 (B = 7) and 16 samples per stream (B = 3)."""
+    sc, p = _scene("bunny_full", 72, 40, 48)
+    p = replace(p, samples_per_stream=sps, tile_w=16, tile_h=16)
+    with gpu.DeviceScene(sc) as ds:
+        _assert_same(*_frames_vs_singles(ds, p, n_frames))
+
+
+@pytest.mark.parametrize("name", ["variants_sky", "glass_bunny", "earth"])
+def test_frames_scenes(gpu, name):
+    sc, p = _scene(name, 48, 32, 24)
+    with gpu.DeviceScene(sc) as ds:
+        _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=8), 4))
+
+
+@pytest.mark.parametrize("shard_map", [0, 1])
+def test_frames_shards(gpu, shard_map):
+    """Shard 1 of 3, interleaved and of the balanced plan.  The plan and the tile order are made once per launch, for
+    all its frames; a probed plan depends on the probe's seed (frame 0's), so the balanced case installs a cost table
+    (what an N-rank job does after its first gathered frame) and every render deals the same tiles."""
+    sc, p = _scene("bunny_full", 64, 48, 32)
+    p = replace(p, shard=1, num_shards=3, shard_map=shard_map, tile_w=8, tile_h=8, samples_per_stream=16)
+    table = None
+    if shard_map:
+        rng = np.random.default_rng(5)
+        table = rng.integers(1, 1 << 20, size=(2, 48), dtype=np.uint32)
+    with gpu.DeviceScene(sc) as ds:
+        _assert_same(*_frames_vs_singles(ds, p, 5, table))
+
+
+def test_frames_against_oracle(gpu):
+    """Frame 2 of a 3-frame launch is the oracle's frame of seed + 2 B W H."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.scene import shard_slot_count
+    sc, p = _scene("bunny_full", 40, 24, 12)
+    p = replace(p, samples_per_stream=5, tile_w=8, tile_h=8)
+    n = shard_slot_count(p)
+    dev = torch.device("cuda", 0)
+    with gpu.DeviceScene(sc) as ds:
+        ds.reserve_frames(p, 3)
+        out = torch.zeros(3 * 3 * n, dtype=torch.float64, device=dev)
+        ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+        ds.render_frames_device(p, 3, out, ctr)
+        torch.cuda.synchronize()
+        shard = out[2 * 3 * n:3 * 3 * n].cpu().numpy()
+    q = replace(p, seed=p.seed + 2 * _nbatch(p) * p.width * p.height)
+    ref, _, _ = oracle_render(sc, q, threads=8)
+    from rtpotato.render import unpack_shard
+    rgb = unpack_shard(q, shard)
+    assert_parity(compare(rgb, ref))
+
+
+def test_frames_spp0_and_errors(gpu):
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.scene import shard_slot_count
+    sc, p = _scene("two_balls", 16, 16, 0)
+    n = shard_slot_count(p)
+    dev = torch.device("cuda", 0)
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+    with gpu.DeviceScene(sc) as ds:
+        out = torch.zeros(2 * 3 * n, dtype=torch.float64, device=dev)
+        ds.render_frames_device(p, 2, out, ctr)
+        torch.cuda.synchronize()
+        assert torch.isnan(out).all()
+        q = replace(p, spp=8, samples_per_stream=2)
+        with pytest.raises(F.RPError):
+            ds.render_frames_device(q, 0, out, ctr)
+        with pytest.raises(F.RPError):
+            ds.render_frames_device(q, F.RP_MAX_FRAMES + 1, torch.zeros(3 * n * 65, dtype=torch.float64, device=dev), ctr)
+        ds.reserve(q)  # one frame's batch sums: two frames do not fit
+        with pytest.raises(F.RPError, match="rp_workspace_reserve_frames"):
+            ds.render_frames_device(q, 2, out, ctr)
+    with gpu.DeviceScene(sc, options={"engine": "wavefront"}) as ds:
+        with pytest.raises(F.RPError):
+            ds.render_frames_device(replace(p, spp=2), 2, out, ctr)
