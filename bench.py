@@ -5,16 +5,16 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One step = one frame of the config (1920x1080x256 spp bunny scene with full materials by default),
-tile-sharded across the N ranks (the balanced tile plan, RP_SHARD_BALANCED: tiles dealt by a probed cost; strong
-scaling: the frame is fixed), rendered by the
-persistent HIP kernel (librp.so) from scene data resident in HBM, followed by librp's frame gather
-(rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per pixel over
-xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
-output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the
-RCCL communicator and takes the barrier and max-time reduction.  With N > 1 three frames are in flight (frame k
-renders on stream k % 3 with its own rp_workspace), so the end of one frame overlaps the start of the next
-(--inflight); one GPU renders one frame at a time, so the render kernel's launch duration (HIP events, the rocprofv3
-kernel trace) is the frame time the roofline is priced on (--inflight 3 there: -1.2 %).
+tile-sharded across the N ranks (the balanced tile plan, RP_SHARD_BALANCED: tiles dealt by a learned cost; strong
+scaling: the frame is fixed), rendered by the persistent HIP kernel (librp.so) from scene data resident in HBM, followed
+by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per
+pixel over xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
+output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
+communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered L = 8 to a
+launch (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
+config's frame of seed + f * B * W * H, every frame traced, shaded and gathered in full.  The rate of lone frames (one
+per launch) is reported beside it (single_frame).  With N > 1 three launches are in flight on their own streams and
+workspaces (--inflight; an 8-way C3 shard: 26.0 / 25.9 / 25.7 ms per frame with 1 / 2 / 3).
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is
 used.
 
@@ -24,7 +24,8 @@ roofline: per ray of the render kernel, from the committed profile
 launch's rays, over the launch's duration (HIP events on its stream):
   achieved / frac = memory-side bytes from the PMC counters (2 x FETCH_SIZE + WRITE_SIZE, the gfx950 correction of
              MI355X_MICROARCH.md; Infinity-Cache hits are counted, so an upper bound of HBM traffic) against the 8 TB/s
-             HBM peak -- the HBM roofline fraction; traffic = those bytes per launch;
+             HBM peak -- the HBM roofline fraction; traffic = those bytes per launch (kernel_ms: its mean duration; a
+             launch renders frames_per_launch frames);
   binding_frac = the fraction of its own roof of what binds the kernel: the larger of the VALU-issue fraction and frac;
   l2_level = the kernel's ALGORITHMIC bytes (its node visits x node bytes + primitive tests x 80 B + the closest hit's
              records + texels + keystream, from the diagnostic build's counts) at this rate, against the guide's
@@ -195,8 +196,8 @@ def cpu_baseline(config: str, runs_plan, spp_override: int = 0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=3)  # one frame per in-flight workspace: each learns its tile costs
+    ap.add_argument("--steps", type=int, default=8)  # one launch of 8 frames
+    ap.add_argument("--warmup", type=int, default=8)  # spread over the in-flight workspaces: each learns its tile costs
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
     ap.add_argument("--samples-per-stream", type=int, default=0,
@@ -210,9 +211,13 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 3 on several)")
-    ap.add_argument("--frames-per-launch", type=int, default=1,
+    ap.add_argument("--frames-per-launch", type=int, default=8,
                     help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
-                         "the frame of seed + f * B * W * H); a step is still one frame, --steps must be a multiple")
+                         "the frame of seed + f * B * W * H); a step is still one frame (K frames in launches of <= L)")
+    ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved"),
+                    help="RP_FRAME_ORDER_* of a launch of several frames")
+    ap.add_argument("--no-single-frame", action="store_true",
+                    help="skip the single-frame-per-launch timing reported beside a frame-sequence headline")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic, one GPU: render only shard --shard of this many (the per-rank work of an N-GPU "
                          "run), no gather; not a bench line")
@@ -227,8 +232,8 @@ def main():
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
     args = ap.parse_args()
     L = args.frames_per_launch
-    if L < 1 or args.steps % L or (args.warmup and args.warmup % L):
-        ap.error("--steps and --warmup must be multiples of --frames-per-launch")
+    if not 1 <= L <= 64 or args.steps < 1:
+        ap.error("--frames-per-launch must be 1..64 (RP_MAX_FRAMES), --steps >= 1")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -267,14 +272,18 @@ def main():
     sp = shard_params(params, rank, world) if not args.shard_of else shard_params(params, args.shard, args.shard_of)
     with stdout_to_stderr():
         comm = bootstrap_comm(rank, world, local)
-    # Frames in flight: frame k renders on stream k % F with its own workspace and shard buffer, so the end of
-    # one frame (its last units leave most of the GPU idle) overlaps the start of the next; the frame gathers
-    # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop.
-    # Per-rank work of an 8-GPU C3 frame (8-way shards on one GPU): 26.7 ms mean with three frames in flight against
-    # 25.8 ms of work (profiles/r3/c3_v47_shards_inflight_traced.json).  One GPU, whole frames: C3 209.6 -> 207.0 ms,
-    # C5 1,611 -> 1,592 ms with three (profiles/r3/ab/if2_*), but overlapping launches no longer have a launch duration
-    # equal to the frame time, which the roofline (HIP events, rocprofv3 kernel trace) is priced on: one at a time there
+    # Frames per launch (rp_render_frames_device_ws): one persistent launch renders L frames, frame f of
+    # it the frame of seed + f * B * W * H, and hands out the frames' k-th tiles of the cost order together
+    # (RP_FRAME_ORDER_INTERLEAVED).  The GPU's 262,144 resident lanes hold 1.6 % of a C3 frame's 16.6 M units and 12.5 %
+    # of an 8-way shard's: the wider the band of the cost order in flight, the more lanes of a wave idle beside longer
+    # paths (VALU / ray +10 %, L2 hit rate 0.72 vs 0.75 for a shard).  Interleaving L frames narrows the band L times:
+    # C3 207.1 -> 202.5 ms per frame at L = 8, an 8-way shard 28.6 -> 26.1 ms, the one-stream contract 261 -> 204 ms
+    # (profiles/r5/c3_frames_per_launch_ab.json).  A step is still one frame: K steps = K frames in launches of <= L.
+    # Frames in flight: launch k renders on stream k % F with its own workspace and shard buffers; the frame gathers
+    # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop, whose launch
+    # duration (HIP events, the rocprofv3 kernel trace) is the time of its L frames the roofline is priced on.
     F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
+    order = args.frame_order
     main_stream = torch.cuda.current_stream(dev)
     streams = [main_stream] if F_ == 1 else [torch.cuda.Stream(dev) for _ in range(F_)]
     wss = [None] + [ds.workspace() for _ in range(F_ - 1)]
@@ -282,13 +291,20 @@ def main():
         ds.reserve_frames(sp, L, w)  # batch sums + gather staging: nothing is allocated inside the timed loop
     from rtpotato.scene import shard_slot_count
     nslots = shard_slot_count(sp)
-    bufs = [torch.zeros(3 * max(1, nslots) * L, dtype=torch.float64, device=dev) for _ in range(F_)]
+    n3 = 3 * max(1, nslots)
+    bufs = [torch.zeros(n3 * L, dtype=torch.float64, device=dev) for _ in range(F_)]
     ctrs = [torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev) for _ in range(F_)]
-    freed = [None] * F_  # event: the gather of the buffer's previous frame is done
+    nfr = [1] * F_  # frames of the buffer's last launch (its counters are their sums)
+    freed = [None] * F_  # event: the gathers of the buffer's previous launch are done
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
-    def step(k_start=None, k_end=None, spx=None):
+    def split(n, parts):
+        """n frames in `parts` launches of near-equal size (each <= L)."""
+        return [n // parts + (1 if j < n % parts else 0) for j in range(parts)] if n else []
+
+    def step(n, k_start=None, k_end=None, spx=None):
+        """One launch of n <= L frames on the next workspace, then their gathers."""
         spx = spx if spx is not None else sp
         i = state["k"] % F_
         state["k"] += 1
@@ -299,8 +315,9 @@ def main():
             k_start.record(st)
         if L == 1:
             ds.render_device(spx, bufs[i], ctrs[i], stream=st, workspace=wss[i])
-        else:  # L frames in one launch: the lanes a frame's tail leaves run the next frame's units
-            ds.render_frames_device(spx, L, bufs[i], ctrs[i], stream=st, workspace=wss[i])
+        else:
+            ds.render_frames_device(spx, n, bufs[i], ctrs[i], stream=st, workspace=wss[i], order=order)
+        nfr[i] = n
         if k_end is not None:
             k_end.record(st)
         if st is not main_stream:
@@ -310,80 +327,91 @@ def main():
         if args.shard_of:
             freed[i] = done if st is not main_stream else None
             return
-        # output stage + RCCL all-gather + de-interleave (+ counters summed over ranks, once), on the main stream
-        n3 = 3 * max(1, nslots)
-        for f in range(L):
+        # per frame: output stage + RCCL all-gather + de-interleave (+ counters summed over ranks, once), main stream
+        for f in range(n):
             ds.frame_gather(comm, spx, bufs[i][f * n3:(f + 1) * n3], frame_bgra=frame,
                             counters=ctrs[i] if f == 0 else None, stream=main_stream, workspace=wss[i])
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 
-    for w in range(args.warmup // L):
-        step()
+    def run(spx, nframes, events=True):
+        """nframes frames in launches of <= L (max-over-ranks seconds, launch events, rays per frame, samples)."""
+        sizes = split(nframes, -(-nframes // L))
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in sizes]
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
-        log(f"[rank {rank}] warmup {w} done")
-    launches = args.steps // L  # a step is one frame; one launch renders L of them
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(launches)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(launches):
-        step(starts[k], ends[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_s = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps / 1e3  # per frame
+        t0 = time.perf_counter()
+        for n, (s0, s1) in zip(sizes, ev):
+            step(n, s0 if events else None, s1 if events else None, spx=spx)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        cs = [c.cpu().tolist() for c in ctrs]
+        bad = [c[3] for c in cs if c[3] != 0]
+        if bad:  # RP_STATUS_* bits (OR-ed over the ranks by the gather): stack overflow, plan mismatch
+            raise RuntimeError(f"render kernel reported status {bad}: frame refused")
+        last = (state["k"] - 1) % F_  # summed over the ranks by rp_frame_gather
+        return (float(tm.item()), [s0.elapsed_time(s1) / 1e3 for s0, s1 in ev] if events else None,
+                cs[last][0] / nfr[last], cs[last][1] / nfr[last], sizes)
+
+    # warm-up: W frames over min(F, W) launches at least -- every in-flight workspace learns its tile costs
+    for w, n in enumerate(split(args.warmup, max(-(-args.warmup // L), min(F_, args.warmup)))):
+        step(n)
+        torch.cuda.synchronize()
+        log(f"[rank {rank}] warmup launch {w} ({n} frames) done")
+    elapsed_max, kdur, rays_step, samples_step, sizes = run(sp, args.steps)
+    kernel_s = sum(kdur) / args.steps  # per frame: launch durations over the frames they rendered
+    kernel_launch_ms = sum(kdur) / len(kdur) * 1e3
     if F_ > 1:
-        # overlapping frames: a frame's events also span the neighbour frames' work, so the kernel rate is
-        # priced on the per-frame throughput time instead
-        kernel_s = elapsed / args.steps
-    cs = [c.cpu().tolist() for c in ctrs]
-    bad = [c[3] for c in cs if c[3] != 0]
-    if bad:  # RP_STATUS_* bits (OR-ed over the ranks by the gather): stack overflow, plan mismatch
-        raise RuntimeError(f"render kernel reported status {bad}: frame refused")
-    rays_step, samples_step = cs[0][0] / L, cs[0][1] / L  # summed over the ranks by rp_frame_gather, per frame
-    tmax = torch.tensor([elapsed], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    elapsed_max = float(tmax.item())
+        # overlapping launches: a launch's events also span the neighbours' work, so the kernel rate is priced on the
+        # per-frame throughput time instead
+        kernel_s = elapsed_max / args.steps
     value = rays_step * args.steps / elapsed_max / 1e6
+
+    # single-frame latency beside the frame-sequence throughput: one frame per launch, sequential, same workspaces
+    single = None
+    if L > 1 and not args.no_single_frame:
+        nsf = 3
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(nsf):
+            step(1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tm = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        r1 = ctrs[(state["k"] - 1) % F_][0].item()
+        single = {"frames": nsf, "ms_per_frame": round(float(tm.item()) / nsf * 1e3, 3),
+                  "value": round(r1 * nsf / float(tm.item()) / 1e6, 3), "unit": "Mrays/s",
+                  "note": "one frame per launch (rp_render_frames_device_ws, n_frames 1) on the same streams and "
+                          "workspaces: the rate of lone frames; the headline renders frame sequences of frames_per_launch "
+                          "frames per launch"}
 
     # SURVEY.md 8c's RNG contract itself (VERDICT r4 #2): one StdRng stream per pixel running the unchanged body of
     # main.rs:70-86 over all spp (samples_per_stream = spp), timed the same way after the headline frames
     contract = None
     csteps = args.contract_steps if args.contract_steps >= 0 else (
-        3 if not (args.samples_per_stream or args.shard_of or args.spp or args.tile) else 0)
+        (L if L > 1 else 3) if not (args.samples_per_stream or args.shard_of or args.spp or args.tile) else 0)
     if csteps > 0 and params.spp > (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM):
         pc = replace(params, samples_per_stream=params.spp)
         spc = shard_params(pc, rank, world)
-        csteps = -(-csteps // L) * L
         for w in wss:
             ds.reserve_frames(spc, L, w)
         for _ in range(F_):  # one launch per in-flight workspace: each learns this contract's tile costs
-            step(spx=spc)
+            step(1, spx=spc)
             torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(csteps // L):
-            step(spx=spc)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        tc = torch.tensor([time.perf_counter() - t1], dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(tc, op=dist.ReduceOp.MAX)
-        cc = [c.cpu().tolist() for c in ctrs]
-        if any(c[3] != 0 for c in cc):
-            raise RuntimeError(f"render kernel reported status {[c[3] for c in cc]} under the one-stream contract")
-        crays = cc[0][0] // L
-        contract = {"samples_per_stream": params.spp, "steps": csteps, "warmup": F_,
-                    "ms_per_step": round(float(tc.item()) / csteps * 1e3, 3),
-                    "value": round(crays * csteps / float(tc.item()) / 1e6, 3), "unit": "Mrays/s",
+        tcs, _, crays, _, csz = run(spc, csteps, events=False)
+        contract = {"samples_per_stream": params.spp, "steps": csteps, "warmup": F_, "launches": csz,
+                    "ms_per_step": round(tcs / csteps * 1e3, 3),
+                    "value": round(crays * csteps / tcs / 1e6, 3), "unit": "Mrays/s",
                     "rays_per_frame": int(crays),
                     "note": "SURVEY.md 8c: one StdRng::seed_from_u64(seed + j*W + i) stream per pixel over all spp "
                             "(main.rs:70-86 unchanged); the headline uses streams of samples_per_stream samples"}
@@ -394,14 +422,16 @@ def main():
         rec = kernel_record(args.config) if args.spp == 0 and args.samples_per_stream == 0 and args.tile == 0 else None
         build = F.rp().rp_build_id().decode()
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-                "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_s * 1e3, 3), "build_id": build}
+                "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_launch_ms, 3),
+                "kernel_ms_per_frame": round(kernel_s * 1e3, 3), "frames_per_launch": sizes, "build_id": build}
+        fpl = args.steps / len(sizes)  # frames per launch, mean
         if rec and rec.get("build_id") != build:
             roof["stale_record"] = f"{rec['source']} was measured on build {rec.get('build_id')}; not used"
             rec = None
         binding = None
         if rec:
-            traffic = rec["traffic_bytes_per_ray"] * local_rays
-            tr_gbs = traffic / kernel_s / 1e9
+            traffic = rec["traffic_bytes_per_ray"] * local_rays * fpl  # per launch
+            tr_gbs = traffic / fpl / kernel_s / 1e9
             tr_frac = tr_gbs / HBM_PEAK_GBS
             issue = rec["valu_per_ray"] * local_rays / kernel_s
             valu_frac = issue / VALU_ISSUE_PEAK
@@ -483,6 +513,7 @@ def main():
             "binding_frac": round(binding[1], 4) if binding else None,
             "binding_resource": binding[0] if binding else None,
             "cpu_baseline": None,
+            "single_frame": single,
             "contract_one_stream": contract,
         }
         if world == 1 and not args.no_cpu_baseline and not args.shard_of:

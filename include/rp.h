@@ -380,12 +380,18 @@ int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const 
  * and their order are made once for the launch: from the workspace's learned cost table, or from a probe of frame 0 --
  * a probed plan follows its seed, so a balanced shard of frame f > 1 may hold other tiles than rp_render_device's frame
  * of that seed would (the pixels are the same; rp_workspace_tile_map gives the launch's deal).  Megakernel engine only;
- * the coherent primary pass and the learned unit order do not apply.  n_frames <= RP_MAX_FRAMES. */
+ * the coherent primary pass and the learned unit order do not apply.  n_frames <= RP_MAX_FRAMES.
+ * frame_order (RP_FRAME_ORDER_*): SEQUENTIAL hands out frame 0's units, then frame 1's, ...; INTERLEAVED hands out the
+ * frames' k-th tiles of the cost order together, for k = 0, 1, ... -- the units in flight at any moment come from a
+ * narrower band of the cost order (fewer lanes idle in a wave whose neighbours run longer paths), every frame ends near
+ * the launch's end.  AUTO = INTERLEAVED.  The frames' pixels do not depend on it. */
 #define RP_MAX_FRAMES 64
+enum { RP_FRAME_ORDER_AUTO = 0, RP_FRAME_ORDER_SEQUENTIAL = 1, RP_FRAME_ORDER_INTERLEAVED = 2 };
 int rp_workspace_reserve_frames(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                                 uint32_t n_frames);
 int rp_render_frames_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,
-                               const rp_render_params* params, uint32_t n_frames, double* d_shard_rgb,
+                               const rp_render_params* params, uint32_t n_frames, uint32_t frame_order,
+                               double* d_shard_rgb,
                                float* d_shard_fg, uint64_t* d_counters, void* stream);
 /* How the last render enqueued with `workspace` (NULL = the scene's) was scheduled (ABI v8): RP_FRAME_* bits.
  * Host state only (no device synchronisation); results never depend on any of it. */

@@ -717,12 +717,14 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
 
 // The render of one shard on `stream` (rp_render_device_ws's body).
 int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p, double* d_rgb,
-                 float* d_fg, uint64_t* d_counters, void* stream, uint32_t n_frames = 1) {
+                 float* d_fg, uint64_t* d_counters, void* stream, uint32_t n_frames = 1,
+                 uint32_t frame_order = RP_FRAME_ORDER_AUTO) {
   if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
   if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
   if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
   if (n_frames > 1 && s->opt.engine != RP_ENGINE_MEGAKERNEL)
     return fail(RP_EINVAL, "several frames per launch: megakernel engine only");
+  if (frame_order > RP_FRAME_ORDER_INTERLEAVED) return fail(RP_EINVAL, "frame_order must be an RP_FRAME_ORDER_* value");
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
@@ -768,6 +770,8 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.n_queue = t.n_slots * kp.nbatch * n_frames;  // every frame's units
   kp.n_frames = n_frames;
   kp.dv_tiles = rpk::make_div32(std::max(1u, t.n_shard_tiles));
+  kp.dv_frames = rpk::make_div32(n_frames);
+  kp.frames_inter = n_frames > 1 && frame_order != RP_FRAME_ORDER_SEQUENTIAL ? 1u : 0u;
   kp.out_stride = 3 * t.n_slots;
   // Per-XCD queues (rp.h RP_QUEUES_*): groups of blocks blockIdx mod 8 share an XCD (MI355X_MICROARCH.md,
   // observed round-robin dispatch; speed only -- any placement gives the same image).  The stage-split engine
@@ -1289,10 +1293,11 @@ int rp_workspace_reserve_frames(rp_scene* s, rp_workspace* w, const rp_render_pa
 }
 
 int rp_render_frames_device_ws(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,
-                               uint32_t n_frames, double* d_rgb, float* d_fg, uint64_t* d_counters, void* stream) {
+                               uint32_t n_frames, uint32_t frame_order, double* d_rgb, float* d_fg, uint64_t* d_counters,
+                               void* stream) {
   if (!s) return fail(RP_EINVAL, "scene is NULL");
   if (!w) w = &s->ws0;
-  return render_shard(s, w, cam, p, d_rgb, d_fg, d_counters, stream, n_frames);
+  return render_shard(s, w, cam, p, d_rgb, d_fg, d_counters, stream, n_frames, frame_order);
 }
 
 int rp_render(rp_scene* s, const rp_camera* cam, const rp_render_params* p, double* out_rgb, float* out_fg,

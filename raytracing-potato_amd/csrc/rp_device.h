@@ -1716,8 +1716,15 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
     const uint32_t local = PROBE ? rem / A->P.nbatch : RPK_UDIV(rem, dv_nbatch);
     batch = rem - local * A->P.nbatch;
     if (!PROBE && A->P.n_frames > 1) {  // virtual tile -> frame f, its tile k; the unit carries its global batch
-      const uint32_t f = RPK_UDIV(k, dv_tiles);
-      k -= f * A->P.n_shard_tiles;
+      uint32_t f;
+      if (A->P.frames_inter) {
+        const uint32_t r = RPK_UDIV(k, dv_frames);
+        f = k - r * A->P.n_frames;
+        k = r;
+      } else {
+        f = RPK_UDIV(k, dv_tiles);
+        k -= f * A->P.n_shard_tiles;
+      }
       batch += f * A->P.nbatch;
     }
     if (!PROBE && A->P.tile_order) k = A->P.tile_order[k];  // the queue hands out shard tiles in cost order

@@ -127,11 +127,13 @@ struct KParams {
   Div32 dv_ochunk, dv_tile_px;  // make_div32(order_chunk), make_div32(tw * th)
   // Several frames in one launch (rp.h rp_render_frames_device_ws): frame f is the frame of these params whose sample
   // batches are f * nbatch .. f * nbatch + nbatch - 1 of the RNG contract (seed + (f nbatch + b) W H + j W + i); the
-  // queues hand out n_frames x n_shard_tiles virtual tiles (frame f's tile k = f * n_shard_tiles + k), a unit carries its
-  // global batch f * nbatch + b, and frame f writes out + f * out_stride (out_fg + f * n_slots) or its batch sums at
-  // partial + 3 (f * n_slots + slot) * nbatch.  The lanes a frame's tail leaves take the next frame's units at once.
+  // queues hand out n_frames x n_shard_tiles virtual tiles -- frame by frame (virtual tile f * n_shard_tiles + k is frame
+  // f's k-th tile) or, frames_inter, rank by rank (virtual tile k * n_frames + f: the frames' k-th tiles of the cost order
+  // together) -- a unit carries its global batch f * nbatch + b, and frame f writes out + f * out_stride (out_fg + f *
+  // n_slots) or its batch sums at partial + 3 (f * n_slots + slot) * nbatch.
   uint32_t n_frames;            // >= 1
-  Div32 dv_tiles;               // make_div32(n_shard_tiles)
+  uint32_t frames_inter;        // 1: rank by rank
+  Div32 dv_tiles, dv_frames;    // make_div32(n_shard_tiles), make_div32(n_frames)
   uint64_t out_stride;          // doubles between frames' shard buffers (3 * n_slots)
 };
 

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "ac6fb22190a82126"
+#define RP_BUILD_ID "ab01c2b8503132aa"

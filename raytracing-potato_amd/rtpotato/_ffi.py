@@ -40,6 +40,7 @@ RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
 RP_ABI_VERSION = 8
 RP_MAX_FRAMES = 64
+RP_FRAME_ORDER_AUTO, RP_FRAME_ORDER_SEQUENTIAL, RP_FRAME_ORDER_INTERLEAVED = 0, 1, 2
 
 
 class rp_hittable(Structure):
@@ -215,7 +216,7 @@ def rp() -> ctypes.CDLL:
     lib.rp_workspace_frame_info.argtypes = [c_void_p, c_void_p, POINTER(c_uint32)]
     lib.rp_workspace_reserve_frames.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32]
     lib.rp_render_frames_device_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_camera), POINTER(rp_render_params),
-                                               c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
+                                               c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.rp_workspace_set_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_frame_assemble_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32, c_void_p,
                                          c_void_p]

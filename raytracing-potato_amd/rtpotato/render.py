@@ -189,11 +189,12 @@ class DeviceScene:
                                                ctypes.c_void_p(s.cuda_stream)))
 
     def render_frames_device(self, params: RenderParams, n_frames: int, out, counters, fg=None, camera=None,
-                             stream=None, workspace: "Workspace | None" = None) -> None:
+                             stream=None, workspace: "Workspace | None" = None, order="auto") -> None:
         """rp_render_frames_device_ws: n_frames frames in one launch -- frame f is render_device's frame of `params` with
         seed + f * ceil(spp / samples_per_stream) * width * height.  out: torch f64, >= n_frames * 3 * shard_slot_count
         elements (frame f at f * 3 * slots); fg: n_frames * slots floats or None; counters: the frames' sums.  The
-        workspace needs reserve_frames(params, n_frames) when the frame has more than one sample batch."""
+        workspace needs reserve_frames(params, n_frames) when the frame has more than one sample batch.  order: "auto" |
+        "sequential" | "interleaved" (RP_FRAME_ORDER_*)."""
         import torch
         cam = (camera or self.scene.camera).to_c()
         p = params.to_c()
@@ -203,7 +204,10 @@ class DeviceScene:
         assert counters.dtype == torch.int64 and counters.numel() >= F.RP_COUNTERS_LEN
         s = stream if stream is not None else torch.cuda.current_stream(out.device)
         F.check(F.rp().rp_render_frames_device_ws(self.handle, workspace.handle if workspace else None,
-                                                  ctypes.byref(cam), ctypes.byref(p), n_frames, out.data_ptr(),
+                                                  ctypes.byref(cam), ctypes.byref(p), n_frames,
+                                                  {"auto": F.RP_FRAME_ORDER_AUTO, "sequential": F.RP_FRAME_ORDER_SEQUENTIAL,
+                                                   "interleaved": F.RP_FRAME_ORDER_INTERLEAVED}.get(order, order),
+                                                  out.data_ptr(),
                                                   fg.data_ptr() if fg is not None else None, counters.data_ptr(),
                                                   ctypes.c_void_p(s.cuda_stream)))
 

@@ -29,7 +29,7 @@ def _nbatch(p):
     return max(1, -(-p.spp // sps)) if p.spp else 1
 
 
-def _frames_vs_singles(ds, p, n_frames, table=None):
+def _frames_vs_singles(ds, p, n_frames, table=None, order="auto"):
     """(multi-frame shard buffers, single-frame shard buffers) as numpy arrays of (n_frames, slots, 3), fg the same,
     and both counter blocks."""
     import torch
@@ -44,7 +44,7 @@ def _frames_vs_singles(ds, p, n_frames, table=None):
     out = torch.full((n_frames * 3 * max(n, 1),), -1.0, dtype=torch.float64, device=dev)
     fg = torch.full((n_frames * max(n, 1),), -1.0, dtype=torch.float32, device=dev)
     ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
-    ds.render_frames_device(p, n_frames, out, ctr, fg=fg, workspace=w)
+    ds.render_frames_device(p, n_frames, out, ctr, fg=fg, workspace=w, order=order)
     torch.cuda.synchronize()
     singles, sfg, sctr = [], [], torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
     stride = _nbatch(p) * p.width * p.height
@@ -71,15 +71,16 @@ def _assert_same(multi, single, mfg, sfg, ctr, sctr):
     assert ctr[3] == 0
 
 
+@pytest.mark.parametrize("order", ["sequential", "interleaved"])
 @pytest.mark.parametrize("sps", [48, 0, 7, 16])
 @pytest.mark.parametrize("n_frames", [1, 3])
-def test_frames_equal_single_renders(gpu, sps, n_frames):
+def test_frames_equal_single_renders(gpu, sps, n_frames, order):
     """bunny_full 72 x 40 at 48 spp on 16 x 16 tiles (ragged last row and column): one stream per pixel (B = 1), the
     default 32 (B = 2, a short last batch), 7 (B = 7) and 16 samples per stream (B = 3)."""
     sc, p = _scene("bunny_full", 72, 40, 48)
     p = replace(p, samples_per_stream=sps, tile_w=16, tile_h=16)
     with gpu.DeviceScene(sc) as ds:
-        _assert_same(*_frames_vs_singles(ds, p, n_frames))
+        _assert_same(*_frames_vs_singles(ds, p, n_frames, order=order))
 
 
 @pytest.mark.parametrize("name", ["variants_sky", "glass_bunny", "earth"])
@@ -89,8 +90,9 @@ def test_frames_scenes(gpu, name):
         _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=8), 4))
 
 
+@pytest.mark.parametrize("order", ["sequential", "interleaved"])
 @pytest.mark.parametrize("shard_map", [0, 1])
-def test_frames_shards(gpu, shard_map):
+def test_frames_shards(gpu, shard_map, order):
     """Shard 1 of 3, interleaved and of the balanced plan.  The plan and the tile order are made once per launch, for
     all its frames; a probed plan depends on the probe's seed (frame 0's), so the balanced case installs a cost table
     (what an N-rank job does after its first gathered frame) and every render deals the same tiles."""
@@ -101,7 +103,7 @@ def test_frames_shards(gpu, shard_map):
         rng = np.random.default_rng(5)
         table = rng.integers(1, 1 << 20, size=(2, 48), dtype=np.uint32)
     with gpu.DeviceScene(sc) as ds:
-        _assert_same(*_frames_vs_singles(ds, p, 5, table))
+        _assert_same(*_frames_vs_singles(ds, p, 5, table, order))
 
 
 def test_frames_against_oracle(gpu):
@@ -143,6 +145,8 @@ def test_frames_spp0_and_errors(gpu):
         q = replace(p, spp=8, samples_per_stream=2)
         with pytest.raises(F.RPError):
             ds.render_frames_device(q, 0, out, ctr)
+        with pytest.raises(F.RPError):
+            ds.render_frames_device(q, 2, out, ctr, order=3)
         with pytest.raises(F.RPError):
             ds.render_frames_device(q, F.RP_MAX_FRAMES + 1, torch.zeros(3 * n * 65, dtype=torch.float64, device=dev), ctr)
         ds.reserve(q)  # one frame's batch sums: two frames do not fit

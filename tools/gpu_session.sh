@@ -11,7 +11,7 @@
 #   shardtrace_<CFG>   rocprofv3 --kernel-trace around one tools/shard_scaling.py run (SHARD_NS, SHARD_ARGS)
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
-#   pmc_<CFG>          six rocprofv3 --pmc passes over one bench frame -> tools/roofline.py record (+ diag if present)
+#   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ diag if present)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
 #   coherence_<CFG>    tools/primary_coherence.py under rocprofv3 --kernel-trace: camera-ray traversal rate by ray order
@@ -32,11 +32,13 @@ echo "start $(date +%T)" > $P
 : > $M
 step() { echo "$1 $(date +%T)" >> $P; }
 made() { echo "$1: $2" >> $M; }  # output file: command
-frames() { case $1 in C5) echo "3 1" ;; C4) echo "4 1" ;; *) echo "10 2" ;; esac; }
+frames() { case $1 in C5) echo "3 1" ;; C4) echo "4 1" ;; *) echo "16 8" ;; esac; }
+# one launch of the bench's frames per launch (C5: 3 frames), the default PMC pass workload
+pmcframes() { case $1 in C5) echo "--steps 3 --warmup 0 --no-single-frame" ;; *) echo "--steps 8 --warmup 0 --no-single-frame" ;; esac; }
 pmc() {  # lib cfg name counters...   (PMC_BENCH_ARGS: the bench frames, default one frame; PMC_LABEL: output suffix)
   local lib=$1 cfg=$2 name=$3; shift 3
   local out=gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_pmc_$name cmd
-  local ba=${PMC_BENCH_ARGS:---steps 1 --warmup 0}
+  local ba=${PMC_BENCH_ARGS:-$(pmcframes $cfg)}
   cmd="rocprofv3 --pmc $* -- python3 bench.py --config $cfg $ba --no-cpu-baseline --contract-steps 0"
   step "pmc $cfg $name"
   made "$out" "RP_LIB=$lib $cmd"

@@ -2,8 +2,9 @@
 
     python tools/roofline.py --config C3 --bench BENCH.json --out OUT.json PASS_DIR [PASS_DIR ...]
 
-Each PASS_DIR is the -d directory of one `rocprofv3 --pmc ... -- python3 bench.py --steps 1 --warmup 0`
-run (one dispatch of the frame kernel per run); BENCH.json is that bench's stdout line (its rays per frame).
+Each PASS_DIR is the -d directory of one `rocprofv3 --pmc ... -- python3 bench.py --steps 8 --warmup 0`
+run (one dispatch of the frame kernel per run, rendering its frames_per_launch frames); BENCH.json is that bench's
+stdout line (its rays per frame and frames per launch).
 The record bench.py prices its `roofline` with (kernel_record()): per ray of the frame kernel
   - traffic_bytes_per_ray: memory-side bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; FETCH_SIZE doubled,
     the gfx950 correction of MI355X_MICROARCH.md "HBM"; Infinity-Cache hits are counted, so this is an upper
@@ -104,6 +105,9 @@ def main():
     a = ap.parse_args()
     bench = json.loads(open(a.bench).read().strip().splitlines()[-1])
     rays = float(bench["config"]["rays_per_frame"])
+    sizes = bench.get("roofline", {}).get("frames_per_launch") or [1]  # frames of each launch (bench.py)
+    if isinstance(sizes, int):
+        sizes = [sizes]
     c, durs, ndisp = {}, {}, set()
     for d in a.passes:
         vals, ns, nd = read_pass(d, a.all_dispatches)
@@ -112,10 +116,14 @@ def main():
         ndisp.add(nd)
     if len(ndisp) != 1:
         raise SystemExit(f"passes saw different dispatch counts {sorted(ndisp)}")
-    rays *= ndisp.pop()
+    nd = ndisp.pop()
+    if nd != len(sizes) and not (nd == 1 and len(set(sizes)) == 1):
+        raise SystemExit(f"{nd} dispatches per pass, the bench made {len(sizes)} launches {sizes}")
+    rays *= sum(sizes) if nd == len(sizes) else sizes[0]  # the dispatches' frames
     rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     build = bench.get("roofline", {}).get("build_id")
-    rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays, "counters": c,
+    rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays,
+           "frames_per_launch": sizes, "counters": c,
            "kernel_ns_per_pass": durs, "bench_ms_per_step": bench.get("ms_per_step")}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
         fetch, write = 2.0 * c["FETCH_SIZE"] * 1024.0, c["WRITE_SIZE"] * 1024.0
