@@ -117,9 +117,12 @@ def main():
     if len(ndisp) != 1:
         raise SystemExit(f"passes saw different dispatch counts {sorted(ndisp)}")
     nd = ndisp.pop()
-    if nd != len(sizes) and not (nd == 1 and len(set(sizes)) == 1):
+    if nd == len(sizes):
+        rays *= sum(sizes)  # the timed launches' frames
+    elif len(set(sizes)) == 1:
+        rays *= sizes[0] * nd  # launches of one size (warm-up launches included with --all-dispatches)
+    else:
         raise SystemExit(f"{nd} dispatches per pass, the bench made {len(sizes)} launches {sizes}")
-    rays *= sum(sizes) if nd == len(sizes) else sizes[0]  # the dispatches' frames
     rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     build = bench.get("roofline", {}).get("build_id")
     rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays,
