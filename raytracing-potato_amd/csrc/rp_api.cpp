@@ -779,8 +779,12 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   uint32_t qmode = s->opt.unit_queues == RP_QUEUES_AUTO ? (uint32_t)DEF_UNIT_QUEUES : s->opt.unit_queues;
   if (s->opt.engine == RP_ENGINE_WAVEFRONT) qmode = RP_QUEUES_SINGLE;
   kp.queue_groups = qmode == RP_QUEUES_SINGLE ? 1u : (uint32_t)rpk::QUEUE_GROUPS;
+  // (interleaved frames: a chunk of n_frames virtual tiles is one tile of every frame, so by default one XCD renders a tile
+  // for all the launch's frames -- its L2 serves the same pixels' rays n_frames times: C3 -1.3 %, 8-way shards -1.9 %
+  // against chunks of one)
+  const uint32_t chunk_auto = kp.frames_inter ? n_frames : 1u;
   kp.queue_chunk = qmode == RP_QUEUES_XCD_REGIONS ? (t.n_shard_tiles + kp.queue_groups - 1) / kp.queue_groups
-                  : kp.queue_groups > 1 && s->opt.queue_chunk ? s->opt.queue_chunk : 1u;
+                  : kp.queue_groups > 1 ? (s->opt.queue_chunk ? s->opt.queue_chunk : chunk_auto) : 1u;
   if (kp.queue_chunk == 0) kp.queue_chunk = 1;
   // a 32-bit queue word takes its units, plus one failed fetch per resident lane after the last unit (single
   // queue) or one per fetch that passes a drained queue on the way to another (per-XCD queues)
