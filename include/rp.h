@@ -265,8 +265,9 @@ typedef struct rp_scene_options {
                                lanes still look for a leaf (0 -> 8 for scenes within the 256 MB Infinity Cache,
                                16 above; 1..64) */
   uint32_t unit_queues;     /* RP_QUEUES_*: how the render blocks share out the units */
-  uint32_t queue_chunk;     /* XCD_TILES: consecutive tiles of the order dealt to one queue at a time (0 -> 1; a launch of
-                               n interleaved frames: n, one tile of every frame) */
+  uint32_t queue_chunk;     /* XCD_TILES: consecutive tiles of the order dealt to one queue at a time (0: up to 8 while
+                               every queue gets >= 16 chunks; a launch of n interleaved frames: rounded up to a multiple
+                               of n, whole tiles of every frame) */
   uint32_t debug_stack_depth; /* TESTS ONLY (0 = off): traversal-stack entries per lane, 8..4096, instead of the
                                depth the tree needs.  Too small a stack drops entries -- wrong frames -- and the
                                render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */

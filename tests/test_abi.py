@@ -111,7 +111,7 @@ def test_scene_options_defaults_without_gpu():
             o.probe_n) == (0, 4, 0.7, 4, 0, 0, 0, 16)
     assert o.node_format == 0  # RP_NODES_AUTO: q8 for host trees of >= 2^21 hittables, f32 otherwise
     assert o.leaf_break == 0   # auto: 8 for cache-resident scenes, 16 above 256 MB
-    assert o.unit_queues == 0 and o.queue_chunk == 0  # RP_QUEUES_AUTO: per-XCD queues, tile by tile
+    assert o.unit_queues == 0 and o.queue_chunk == 0  # RP_QUEUES_AUTO: per-XCD queues; 0: chunks of 8 tiles
     assert o.collapse == 0  # RP_COLLAPSE_AUTO: the SAH-optimal 4-wide collapse
     o = scene_options(builder="gpu", lds_depth=17, node_format="q8")
     assert o.builder == 2 and o.lds_depth == 17 and o.node_format == 2

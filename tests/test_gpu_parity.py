@@ -433,7 +433,8 @@ def test_tile_orders_bitwise(gpu):
 
 
 @pytest.mark.parametrize("queues", [{"unit_queues": "single"}, {"unit_queues": "xcd_tiles"},
-                                    {"unit_queues": "xcd_regions"}, {"unit_queues": "xcd_tiles", "queue_chunk": 3}])
+                                    {"unit_queues": "xcd_regions"}, {"unit_queues": "xcd_tiles", "queue_chunk": 3},
+                                    {"unit_queues": "xcd_tiles", "queue_chunk": 1}])
 def test_unit_queues_bitwise(gpu, queues):
     """options.unit_queues / queue_chunk (one device-wide unit queue, or one per XCD group of blocks serving
     every 8th tile, every 8th chunk of tiles or an eighth of the tile order, stealing once drained) changes the
