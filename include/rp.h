@@ -287,8 +287,9 @@ typedef struct rp_stats {
 typedef struct rp_scene rp_scene;   /* opaque: device-resident scene + acceleration structure */
 typedef struct rp_workspace rp_workspace;  /* opaque: per-frame device state of a render (see below) */
 
-/* Library / device queries.  rp_build_id: a hash of the render kernel's sources this library was built from
- * (profile records of the kernel carry it; a record of another build is stale). */
+/* Library / device queries.  rp_build_id: a hash of the machine code that decides a frame's per-ray work -- the render
+ * kernel, the tree builders and the scheduling code -- this library was built from (profile records of the kernel carry
+ * it; a record of another build is stale). */
 int rp_abi_version(void);
 const char* rp_build_id(void);
 const char* rp_last_error(void);

@@ -1133,7 +1133,6 @@ int rp_abi_version(void) { return RP_ABI_VERSION; }
 #ifndef RP_BUILD_ID
 #define RP_BUILD_ID "unknown"
 #endif
-const char* rp_build_id(void) { return RP_BUILD_ID; }
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 
