@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "ab01c2b8503132aa"
+#define RP_BUILD_ID "acbbfb2c68f12470"
