@@ -10,7 +10,8 @@
 #                      SHARD_ARGS (or SHARD_ARGS_<L> for a labelled run), library SHARD_LIB_<L> (default main)
 #   shardtrace_<CFG>   rocprofv3 --kernel-trace around one tools/shard_scaling.py run (SHARD_NS, SHARD_ARGS)
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
-#   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration)
+#   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration: every launch
+#                      of the run renders the bench's frames per launch, no lone-frame or contract launches)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ diag if present)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
@@ -32,7 +33,7 @@ echo "start $(date +%T)" > $P
 : > $M
 step() { echo "$1 $(date +%T)" >> $P; }
 made() { echo "$1: $2" >> $M; }  # output file: command
-frames() { case $1 in C5) echo "3 1" ;; C4) echo "4 1" ;; *) echo "16 8" ;; esac; }
+frames() { case $1 in C5) echo "3 3" ;; C4) echo "4 1" ;; *) echo "16 8" ;; esac; }
 # one launch of the bench's frames per launch (C5: 3 frames), the default PMC pass workload
 pmcframes() { case $1 in C5) echo "--steps 3 --warmup 0 --no-single-frame" ;; *) echo "--steps 8 --warmup 0 --no-single-frame" ;; esac; }
 pmc() {  # lib cfg name counters...   (PMC_BENCH_ARGS: the bench frames, default one frame; PMC_LABEL: output suffix)
@@ -86,9 +87,9 @@ for s in ${STEPS:-tests}; do
     trace_*)
       cfg=${s#trace_}; read st wu <<< "$(frames $cfg)"
       step "trace $cfg"
-      made gpurun_out/${TAG}_${cfg}_trace "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 ${BENCH_ARGS:-}"
+      made gpurun_out/${TAG}_${cfg}_trace "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 --no-single-frame ${BENCH_ARGS:-}"
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${cfg}_trace -o run --output-format csv -- \
-        python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 ${BENCH_ARGS:-} \
+        python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 --no-single-frame ${BENCH_ARGS:-} \
         > gpurun_out/${TAG}_${cfg}_bench_under_rocprof.json 2> gpurun_out/${TAG}_${cfg}_trace.err || exit 1 ;;
     pmc_*)
       cfg=${s#pmc_}
