@@ -155,3 +155,26 @@ def test_frames_spp0_and_errors(gpu):
     with gpu.DeviceScene(sc, options={"engine": "wavefront"}) as ds:
         with pytest.raises(F.RPError):
             ds.render_frames_device(replace(p, spp=2), 2, out, ctr)
+
+
+@pytest.mark.parametrize("shard", [None, 3])
+def test_frames_c3_full_size(gpu, shard):
+    """bench.py's workload at full size: C3 (1920x1080x256, 32-sample streams) rendered 8 frames to a launch in the
+    interleaved order with the default queue chunks -- each of the launch's frames equals its lone render (seed + f B W H)
+    bit for bit, with the summed counts; also shard 3 of an 8-way balanced deal (the N = 8 per-rank work) under an
+    installed cost table (as every rank holds one after its first gathered frame).  The lone renders are themselves
+    oracle-checked at this size (test_gpu_configs.py)."""
+    from rtpotato import scenes
+    scene, params = scenes.config_scene("C3")
+    table = None
+    if shard is not None:
+        n_tiles = -(-params.width // params.tile_w) * -(-params.height // params.tile_h)
+        table = np.random.default_rng(11).integers(1, 1 << 20, size=(2, n_tiles), dtype=np.uint32)
+        params = replace(params, shard=shard, num_shards=8, shard_map=1)
+    with gpu.DeviceScene(scene) as ds:
+        multi, single, mfg, sfg, ctr, sctr = _frames_vs_singles(ds, params, 8, table)
+    _assert_same(multi, single, mfg, sfg, ctr, sctr)
+    px = params.width * params.height // (1 if shard is None else 8)
+    assert abs(int(ctr[2]) - 8 * px) <= 8 * 1024 and ctr[1] == 256 * ctr[2]  # every pixel of every frame, 256 samples
+    if shard is None:
+        assert ctr[2] == 8 * px
