@@ -193,6 +193,13 @@ def cpu_baseline(config: str, runs_plan, spp_override: int = 0):
     return out
 
 
+def launch_sizes(n: int, per_launch: int, min_launches: int = 0) -> list:
+    """n frames in the fewest launches of <= per_launch frames (at least min_launches), sizes as equal as they can be:
+    20 frames, 8 per launch -> [7, 7, 6]."""
+    parts = max(-(-n // per_launch), min_launches) if n > 0 else 0
+    return [n // parts + (1 if j < n % parts else 0) for j in range(parts)]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -299,10 +306,6 @@ def main():
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
 
-    def split(n, parts):
-        """n frames in `parts` launches of near-equal size (each <= L)."""
-        return [n // parts + (1 if j < n % parts else 0) for j in range(parts)] if n else []
-
     def step(n, k_start=None, k_end=None, spx=None):
         """One launch of n <= L frames on the next workspace, then their gathers."""
         spx = spx if spx is not None else sp
@@ -336,7 +339,7 @@ def main():
 
     def run(spx, nframes, events=True):
         """nframes frames in launches of <= L (max-over-ranks seconds, launch events, rays per frame, samples)."""
-        sizes = split(nframes, -(-nframes // L))
+        sizes = launch_sizes(nframes, L)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in sizes]
         if world > 1:
             dist.barrier()
@@ -359,7 +362,7 @@ def main():
                 cs[last][0] / nfr[last], cs[last][1] / nfr[last], sizes)
 
     # warm-up: W frames over min(F, W) launches at least -- every in-flight workspace learns its tile costs
-    for w, n in enumerate(split(args.warmup, max(-(-args.warmup // L), min(F_, args.warmup)))):
+    for w, n in enumerate(launch_sizes(args.warmup, L, min(F_, args.warmup))):
         step(n)
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup launch {w} ({n} frames) done")

@@ -226,3 +226,20 @@ def test_profile_records_price_fractions_below_one():
         assert 0 < rec["traffic_bytes_per_ray"] * rate / 1e9 / b.HBM_PEAK_GBS <= 1.0, cfg
         assert 0 < rec["algorithmic_bytes_per_ray"] * rate / 1e9 / b.L2_GATHER_GBS <= 1.0, cfg
         assert 0 < rec["valu_per_ray"] * rate / b.VALU_ISSUE_PEAK <= 1.0, cfg
+
+
+def test_bench_launch_sizes():
+    """bench.py splits K frames into the fewest launches of <= L frames, sizes near-equal (the driver's --steps 20 at
+    8 per launch: 7 + 7 + 6), and spreads the warm-up over the in-flight workspaces."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert b.launch_sizes(20, 8) == [7, 7, 6]
+    assert b.launch_sizes(16, 8) == [8, 8] and b.launch_sizes(8, 8) == [8] and b.launch_sizes(5, 8) == [5]
+    assert b.launch_sizes(0, 8) == [] and b.launch_sizes(3, 1) == [1, 1, 1]
+    assert b.launch_sizes(5, 8, 3) == [2, 2, 1] and b.launch_sizes(2, 8, 2) == [1, 1]
+    for n in range(1, 70):
+        for L in (1, 3, 8, 16):
+            s = b.launch_sizes(n, L)
+            assert sum(s) == n and max(s) <= L and max(s) - min(s) <= 1 and len(s) == -(-n // L)
