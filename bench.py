@@ -305,6 +305,7 @@ def main():
     freed = [None] * F_  # event: the gathers of the buffer's previous launch are done
     frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
     state = {"k": 0}
+    launches_all = []  # (frames, start, end) of every launch of this process, warm-up and side runs included
 
     def step(n, k_start=None, k_end=None, spx=None):
         """One launch of n <= L frames on the next workspace, then their gathers."""
@@ -314,15 +315,16 @@ def main():
         st = streams[i]
         if freed[i] is not None:
             st.wait_event(freed[i])
-        if k_start is not None:
-            k_start.record(st)
+        if k_start is None:
+            k_start, k_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        launches_all.append((n, k_start, k_end))
+        k_start.record(st)
         if L == 1:
             ds.render_device(spx, bufs[i], ctrs[i], stream=st, workspace=wss[i])
         else:
             ds.render_frames_device(spx, n, bufs[i], ctrs[i], stream=st, workspace=wss[i], order=order)
         nfr[i] = n
-        if k_end is not None:
-            k_end.record(st)
+        k_end.record(st)
         if st is not main_stream:
             done = torch.cuda.Event()
             done.record(st)
@@ -426,6 +428,10 @@ def main():
         build = F.rp().rp_build_id().decode()
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
                 "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_launch_ms, 3),
+                # every launch of this process (warm-up, timed, single_frame, contract): what a rocprofv3 kernel summary of
+                # the same command averages
+                "kernel_ms_all_launches": round(sum(a.elapsed_time(b) for _, a, b in launches_all) / len(launches_all), 3),
+                "launches_all": [nn for nn, _, _ in launches_all],
                 "kernel_ms_per_frame": round(kernel_s * 1e3, 3), "frames_per_launch": sizes, "build_id": build}
         fpl = args.steps / len(sizes)  # frames per launch, mean
         if rec and rec.get("build_id") != build:

@@ -12,6 +12,7 @@
 #   diag_<CFG>         tools/diag.py with the diagnostic build (phase shares, node visits, lane utilisation)
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration: every launch
 #                      of the run renders the bench's frames per launch, no lone-frame or contract launches)
+#   tracedrv_<CFG>     rocprofv3 --kernel-trace --stats around the driver's command (--steps 20 --warmup 5)
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ diag if present)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
@@ -91,6 +92,14 @@ for s in ${STEPS:-tests}; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${cfg}_trace -o run --output-format csv -- \
         python3 bench.py --config $cfg --steps $st --warmup $wu --no-cpu-baseline --contract-steps 0 --no-single-frame ${BENCH_ARGS:-} \
         > gpurun_out/${TAG}_${cfg}_bench_under_rocprof.json 2> gpurun_out/${TAG}_${cfg}_trace.err || exit 1 ;;
+    tracedrv_*)  # rocprofv3 --kernel-trace --stats around the driver's own command (--steps 20 --warmup 5): compare its
+      # average with the line's roofline.kernel_ms_all_launches (every launch of the process, side runs included)
+      cfg=${s#tracedrv_}
+      step "tracedrv $cfg"
+      made gpurun_out/${TAG}_${cfg}_tracedrv "rocprofv3 --kernel-trace --stats -- python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline"
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_${cfg}_tracedrv -o run --output-format csv -- \
+        python3 bench.py --config $cfg --steps 20 --warmup 5 --no-cpu-baseline \
+        > gpurun_out/${TAG}_${cfg}_bench_drv_under_rocprof.json 2> gpurun_out/${TAG}_${cfg}_tracedrv.err || exit 1 ;;
     pmc_*)
       cfg=${s#pmc_}
       pmc $LIB $cfg sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU \
