@@ -178,3 +178,21 @@ def test_frames_c3_full_size(gpu, shard):
     assert abs(int(ctr[2]) - 8 * px) <= 8 * 1024 and ctr[1] == 256 * ctr[2]  # every pixel of every frame, 256 samples
     if shard is None:
         assert ctr[2] == 8 * px
+
+
+@pytest.mark.parametrize("opt", [{"node_format": "q8"}, {"node_format": "w8"}, {"lds_depth": 8},
+                                 {"unit_queues": "single"}, {"tile_order": "morton"}])
+def test_frames_node_formats_and_options(gpu, opt):
+    """Every node format (q8: the large-scene kernel, whose hits carry no material out of the traversal; w8), the
+    spilled stack, one device-wide queue and Z-order tiles: 3 interleaved frames per launch equal their lone renders."""
+    sc, p = _scene("bunny_full", 64, 40, 24)
+    with gpu.DeviceScene(sc, options=opt) as ds:
+        _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=8, tile_w=16, tile_h=16), 3))
+
+
+def test_frames_lens_camera(gpu):
+    """three_balls (lens_radius 0.1: the UnitDisk draw moves the camera ray) and the catalogue's texture scenes."""
+    for name in ("three_balls", "more_balls"):
+        sc, p = _scene(name, 48, 32, 16)
+        with gpu.DeviceScene(sc) as ds:
+            _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=4), 4))
