@@ -46,32 +46,41 @@ def _render_ws(ds, sp, w):
     torch.cuda.synchronize()
 
 
-def inflight_time(ds, sp, F, frames, table=None):
-    """Steady per-frame time of shard sp with F frames in flight (bench.py's loop without the gather): frames
-    alternate over F streams and workspaces; one warm-up round, then `frames` frames timed together."""
+def inflight_time(ds, sp, F, frames, table=None, per_launch=1):
+    """Steady per-frame time of shard sp with F launches in flight (bench.py's loop without the gather): launches of
+    per_launch frames (rp_render_frames_device_ws, interleaved) alternate over F streams and workspaces; one warm-up
+    round, then `frames` frames (in launches of per_launch) timed together."""
     import time
     import torch
     from rtpotato.scene import shard_slot_count
     dev = torch.device("cuda", 0)
     streams = [torch.cuda.Stream(dev) for _ in range(F)]
     wss = [ds.workspace() for _ in range(F)]
+    L = per_launch
     for w in wss:
-        ds.reserve(sp, w)
+        ds.reserve_frames(sp, L, w)
         if table is not None:
             ds.set_tile_costs(sp, table, sp.num_shards, w)
     n = shard_slot_count(sp)
-    bufs = [torch.zeros(3 * max(1, n), dtype=torch.float64, device=dev) for _ in range(F)]
+    bufs = [torch.zeros(3 * max(1, n) * L, dtype=torch.float64, device=dev) for _ in range(F)]
     ctrs = [torch.zeros(4, dtype=torch.int64, device=dev) for _ in range(F)]
+
+    def launch(i):
+        if L == 1:
+            ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+        else:
+            ds.render_frames_device(sp, L, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+
     for i in range(F):
-        ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+        launch(i)
     torch.cuda.synchronize()
+    launches = max(1, frames // L)
     t0 = time.perf_counter()
-    for k in range(frames):
-        i = k % F
-        ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+    for k in range(launches):
+        launch(k % F)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / frames
-    rays = int(ctrs[0][0])
+    dt = (time.perf_counter() - t0) / (launches * L)
+    rays = int(ctrs[0][0]) // L
     assert all(int(c[3]) == 0 for c in ctrs)
     for w in wss:
         w.close()
@@ -89,6 +98,8 @@ def main():
                     help="frames in flight (> 1: each shard renders --frames frames on this many streams and "
                          "workspaces, as bench.py does for N > 1; its time is the steady per-frame time)")
     ap.add_argument("--frames", type=int, default=9)
+    ap.add_argument("--per-launch", type=int, default=1,
+                    help="frames per launch (> 1: rp_render_frames_device_ws, interleaved, as bench.py renders them)")
     ap.add_argument("--learned", type=int, default=1,
                     help="1: schedule balanced N > 1 shards from a learned cost table (what every rank holds after "
                          "its first gathered frame: the measured costs of all shards, combined through the deal order "
@@ -108,6 +119,7 @@ def main():
     ds = DeviceScene(scene, options=options)
     ds.render(replace(params, spp=4))  # warm
     out = {"config": a.config, "tile": [params.tile_w, params.tile_h], "reps": a.reps, "inflight": a.inflight,
+           "per_launch": a.per_launch,
            "scene_options": options or "defaults", "per_map": {}}
     import statistics
     for mp in a.maps.split(","):
@@ -120,8 +132,8 @@ def main():
                 sp = replace(params, shard=s, num_shards=n, shard_map=smap)
                 if table is not None:
                     ds.set_tile_costs(sp, table, n)
-                if a.inflight > 1:
-                    t, r = inflight_time(ds, sp, a.inflight, a.frames, table)
+                if a.inflight > 1 or a.per_launch > 1:
+                    t, r = inflight_time(ds, sp, a.inflight, a.frames, table, a.per_launch)
                     times.append(t)
                     rays += r
                     continue
