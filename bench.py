@@ -10,7 +10,7 @@ scaling: the frame is fixed), rendered by the persistent HIP kernel (librp.so) f
 by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per
 pixel over xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
 output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
-communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered L = 8 to a
+communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered L = 16 to a
 launch (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
 config's frame of seed + f * B * W * H, every frame traced, shaded and gathered in full.  The rate of lone frames (one
 per launch) is reported beside it (single_frame).  With N > 1 three launches are in flight on their own streams and
@@ -203,7 +203,7 @@ def launch_sizes(n: int, per_launch: int, min_launches: int = 0) -> list:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=8)  # one launch of 8 frames
+    ap.add_argument("--steps", type=int, default=16)  # one launch of 16 frames
     ap.add_argument("--warmup", type=int, default=8)  # spread over the in-flight workspaces: each learns its tile costs
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
@@ -218,7 +218,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 3 on several)")
-    ap.add_argument("--frames-per-launch", type=int, default=8,
+    ap.add_argument("--frames-per-launch", type=int, default=16,
                     help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
                          "the frame of seed + f * B * W * H); a step is still one frame (K frames in launches of <= L)")
     ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved"),
@@ -285,10 +285,16 @@ def main():
     # of an 8-way shard's: the wider the band of the cost order in flight, the more lanes of a wave idle beside longer
     # paths (VALU / ray +10 %, L2 hit rate 0.72 vs 0.75 for a shard).  Interleaving L frames narrows the band L times:
     # C3 207.1 -> 202.5 ms per frame at L = 8, an 8-way shard 28.6 -> 26.1 ms, the one-stream contract 261 -> 204 ms
-    # (profiles/r5/c3_frames_per_launch_ab.json).  A step is still one frame: K steps = K frames in launches of <= L.
+    # (profiles/r5/c3_frames_per_launch_ab.json); with one tile of every frame per queue chunk (v56) C3 205.3 / 199.4 /
+    # 198.5 / 197.2 ms at L = 1 / 8 / 16 / 32 (c3_frames_chunk_auto_sweep.json, c3_frames_per_launch_large.json).  A step is still one frame: K steps = K frames in launches of <= L.
     # Frames in flight: launch k renders on stream k % F with its own workspace and shard buffers; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop, whose launch
     # duration (HIP events, the rocprofv3 kernel trace) is the time of its L frames the roofline is priced on.
+    # (a launch's units -- slots x sample batches x frames -- stay below 2^31, rp_api.cpp's unit-decode bound: C5, 16.8 M
+    # pixels of 8 batches, takes at most 15 frames a launch)
+    from rtpotato.scene import shard_slot_count
+    units_frame = max(1, shard_slot_count(sp)) * max(1, -(-params.spp // (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM)))
+    L = max(1, min(L, ((1 << 31) - 1) // units_frame))
     F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
     order = args.frame_order
     main_stream = torch.cuda.current_stream(dev)

@@ -34,9 +34,9 @@ echo "start $(date +%T)" > $P
 : > $M
 step() { echo "$1 $(date +%T)" >> $P; }
 made() { echo "$1: $2" >> $M; }  # output file: command
-frames() { case $1 in C5) echo "3 3" ;; C4) echo "4 1" ;; *) echo "16 8" ;; esac; }
-# one launch of the bench's frames per launch (C5: 3 frames), the default PMC pass workload
-pmcframes() { case $1 in C5) echo "--steps 3 --warmup 0 --no-single-frame" ;; *) echo "--steps 8 --warmup 0 --no-single-frame" ;; esac; }
+frames() { case $1 in C5) echo "3 3" ;; C4) echo "4 4" ;; *) echo "32 16" ;; esac; }
+# one launch of the bench's frames per launch (C3: 16 frames; C5: 3), the default PMC pass workload
+pmcframes() { case $1 in C5) echo "--steps 3 --warmup 0 --no-single-frame" ;; C4) echo "--steps 8 --warmup 0 --no-single-frame" ;; *) echo "--steps 16 --warmup 0 --no-single-frame" ;; esac; }
 pmc() {  # lib cfg name counters...   (PMC_BENCH_ARGS: the bench frames, default one frame; PMC_LABEL: output suffix)
   local lib=$1 cfg=$2 name=$3; shift 3
   local out=gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_pmc_$name cmd
