@@ -200,6 +200,12 @@ def launch_sizes(n: int, per_launch: int, min_launches: int = 0) -> list:
     return [n // parts + (1 if j < n % parts else 0) for j in range(parts)]
 
 
+def frames_per_launch_cap(per_launch: int, slots: int, batches: int) -> int:
+    """Frames per launch, at most what keeps a launch's units (slots x sample batches x frames) below 2^31, the unit
+    decode's bound in rp_api.cpp: a C5 frame (16.8 M pixels of 8 batches) takes at most 15 a launch."""
+    return max(1, min(per_launch, ((1 << 31) - 1) // (max(1, slots) * max(1, batches))))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -290,11 +296,9 @@ def main():
     # Frames in flight: launch k renders on stream k % F with its own workspace and shard buffers; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop, whose launch
     # duration (HIP events, the rocprofv3 kernel trace) is the time of its L frames the roofline is priced on.
-    # (a launch's units -- slots x sample batches x frames -- stay below 2^31, rp_api.cpp's unit-decode bound: C5, 16.8 M
-    # pixels of 8 batches, takes at most 15 frames a launch)
     from rtpotato.scene import shard_slot_count
-    units_frame = max(1, shard_slot_count(sp)) * max(1, -(-params.spp // (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM)))
-    L = max(1, min(L, ((1 << 31) - 1) // units_frame))
+    L = frames_per_launch_cap(L, shard_slot_count(sp),
+                              -(-params.spp // (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM)))
     F_ = args.inflight if args.inflight > 0 else (1 if world == 1 else 3)
     order = args.frame_order
     main_stream = torch.cuda.current_stream(dev)

@@ -243,3 +243,17 @@ def test_bench_launch_sizes():
         for L in (1, 3, 8, 16):
             s = b.launch_sizes(n, L)
             assert sum(s) == n and max(s) <= L and max(s) - min(s) <= 1 and len(s) == -(-n // L)
+
+
+def test_bench_frames_per_launch_cap():
+    """bench.py keeps a launch's units below 2^31 (rp_api.cpp refuses more): C3 takes its 16 frames, C5 15, C4 (1,024 spp,
+    32 batches) 16 of its 32 allowed."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    c3 = 60 * 34 * 1024  # 32 x 32 tiles of a 1920 x 1080 frame
+    assert b.frames_per_launch_cap(16, c3, 8) == 16 and b.frames_per_launch_cap(64, c3, 32) == 32
+    c5 = 128 * 128 * 1024
+    assert b.frames_per_launch_cap(16, c5, 8) == 15 and b.frames_per_launch_cap(16, c5, 8) * c5 * 8 < 1 << 31
+    assert b.frames_per_launch_cap(1, 0, 0) == 1 and b.frames_per_launch_cap(8, 1 << 31, 1) == 1
