@@ -8,8 +8,8 @@ One step = one frame of the config (1920x1080x256 spp bunny scene with full mate
 tile-sharded across the N ranks (the balanced tile plan, RP_SHARD_BALANCED: tiles dealt by a learned cost; strong
 scaling: the frame is fixed), rendered by the persistent HIP kernel (librp.so) from scene data resident in HBM, followed
 by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per
-pixel over xGMI, and the device-side de-interleave into frame order on every rank (the body of the reference's
-output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
+pixel over xGMI (one collective per launch for all its frames, rp_frames_gather), and the device-side de-interleave into
+frame order on every rank (the body of the reference's output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
 communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered L = 16 to a
 launch (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
 config's frame of seed + f * B * W * H, every frame traced, shaded and gathered in full.  The rate of lone frames (one
@@ -313,7 +313,7 @@ def main():
     ctrs = [torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev) for _ in range(F_)]
     nfr = [1] * F_  # frames of the buffer's last launch (its counters are their sums)
     freed = [None] * F_  # event: the gathers of the buffer's previous launch are done
-    frame = torch.zeros(params.height * params.width * 4, dtype=torch.uint8, device=dev)
+    frames = torch.zeros(params.height * params.width * 4 * L, dtype=torch.uint8, device=dev)  # a launch's frames
     state = {"k": 0}
     launches_all = []  # (frames, start, end) of every launch of this process, warm-up and side runs included
 
@@ -342,10 +342,14 @@ def main():
         if args.shard_of:
             freed[i] = done if st is not main_stream else None
             return
-        # per frame: output stage + RCCL all-gather + de-interleave (+ counters summed over ranks, once), main stream
-        for f in range(n):
-            ds.frame_gather(comm, spx, bufs[i][f * n3:(f + 1) * n3], frame_bgra=frame,
-                            counters=ctrs[i] if f == 0 else None, stream=main_stream, workspace=wss[i])
+        # the launch's frames: output stage + ONE RCCL all-gather of their BGRA8 shards + de-interleave into n frames
+        # (+ the launch's counters summed over the ranks), on the main stream
+        if L == 1:
+            ds.frame_gather(comm, spx, bufs[i], frame_bgra=frames, counters=ctrs[i], stream=main_stream,
+                            workspace=wss[i])
+        else:
+            ds.frames_gather(comm, spx, n, bufs[i], frames_bgra=frames, counters=ctrs[i], stream=main_stream,
+                             workspace=wss[i])
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 

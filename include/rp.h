@@ -473,6 +473,15 @@ int rp_comm_info(const rp_comm* comm, int* nranks, int* rank, int* device);
 int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                     const double* d_shard_rgb, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, void* stream);
+/* rp_frame_gather for the n_frames shards of one rp_render_frames_device_ws launch (d_shard_rgb: its n_frames shard
+ * buffers back to back) in ONE all-gather: every rank's packed block carries its counter block (the launch's sums),
+ * its measured tile costs and the n_frames shards' BGRA8 bytes one after the other; d_frames_bgra (nullable) receives
+ * n_frames assembled frames of width*height*4 bytes back to back.  BGRA8 only (rp_frame_gather gathers f64 frames).
+ * One collective per launch instead of one per frame: an RCCL all-gather kernel waits for a CU the render waves leave
+ * (DESIGN.md 6).  The workspace must be reserved with rp_workspace_reserve_frames for n_frames. */
+int rp_frames_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
+                     uint32_t n_frames, const double* d_shard_rgb, uint8_t* d_frames_bgra, uint64_t* d_counters,
+                     void* stream);
 /* The frame assembly step alone, for callers that move the shards with their own collective (MPI, a
  * torch.distributed all-gather): d_gathered holds params->num_shards shard buffers of `stride` slots each
  * (rp_gather_stride: the largest shard, shard 0), rank r's at slot r * stride, `words_per_slot` 32-bit words

@@ -435,8 +435,10 @@ uint64_t pack_head(const Tiling& t) {
   const uint64_t st = (t.n_tiles + t.shards - 1) / t.shards;
   return 2ull * rpk::GATHER_CTR + ((2 * st + 1) & ~1ull);
 }
-uint64_t pack_words(const Tiling& t, bool bgra) {
-  return pack_head(t) + (bgra ? ((stage_slots(t) + 1) & ~1ull) : 0ull);
+uint64_t bgra_words(const Tiling& t) { return (stage_slots(t) + 1) & ~1ull; }
+// (a gather of n frames' shards -- rp_frames_gather -- packs their BGRA8 bytes one after the other behind one head)
+uint64_t pack_words(const Tiling& t, bool bgra, uint32_t n_frames = 1) {
+  return pack_head(t) + (bgra ? n_frames * bgra_words(t) : 0ull);
 }
 
 // Grow a pair of device buffers (a, b) of na, nb elements per unit to `units` units (synchronous).
@@ -506,7 +508,7 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
     if ((rc = grow1(w->d_gather_rgb, rgb_g_cap, stride * t.shards * 3, "gather buffers"))) return rc;
     w->gs_slots = rgb_cap / 3;
     w->gather_slots = rgb_g_cap / 3;
-    const uint64_t pw = pack_words(t, true);
+    const uint64_t pw = pack_words(t, true, n_frames);  // rp_frames_gather: all of a launch's frames in one block
     if ((rc = grow1(w->d_pack_send, w->pack_words, pw, "gather block"))) return rc;
     if ((rc = grow1(w->d_pack_recv, w->pack_recv_words, pw * t.shards, "gathered blocks"))) return rc;
   }
@@ -998,12 +1000,15 @@ struct GatherPlan {
   uint64_t stride;  // slots per rank buffer
   uint32_t stride_tiles;  // tiles per rank buffer (shard 0's count)
   uint64_t head;          // words of the packed block before the BGRA8 bytes (pack_head)
+  uint32_t nf;            // frames whose BGRA8 bytes the block carries (rp_frames_gather; 1 otherwise)
   rpk::FrameGeom geom;
   const uint32_t* plan_hash;  // the workspace's plan hash (balanced frames), NULL = interleave
 };
 
-int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_render_params* p, GatherPlan& gp) {
+int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_render_params* p, GatherPlan& gp,
+                uint32_t nf = 1) {
   if (!s || !w || w->scene != s) return fail(RP_EINVAL, "scene / workspace mismatch");
+  gp.nf = nf;
   int rc = make_tiling(p, gp.t);
   if (rc) return rc;
   if ((int)gp.t.shards != nranks || (int)gp.t.shard != rank)
@@ -1011,9 +1016,10 @@ int gather_plan(rp_scene* s, rp_workspace* w, int nranks, int rank, const rp_ren
   gp.stride = stage_slots(gp.t);
   gp.stride_tiles = (gp.t.n_tiles + gp.t.shards - 1) / gp.t.shards;
   gp.head = pack_head(gp.t);
-  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || pack_words(gp.t, true) > w->pack_words ||
-      pack_words(gp.t, true) * nranks > w->pack_recv_words)
-    return fail(RP_EINVAL, "workspace not reserved for this frame's gather: call rp_workspace_reserve");
+  if (gp.stride > w->gs_slots || gp.stride * (uint64_t)nranks > w->gather_slots || pack_words(gp.t, true, nf) > w->pack_words ||
+      pack_words(gp.t, true, nf) * nranks > w->pack_recv_words)
+    return fail(RP_EINVAL, nf > 1 ? "workspace not reserved for these frames' gather: call rp_workspace_reserve_frames"
+                                  : "workspace not reserved for this frame's gather: call rp_workspace_reserve");
   gp.geom.W = p->width;
   gp.geom.H = p->height;
   gp.geom.tw = gp.t.tw;
@@ -1042,9 +1048,9 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
   const uint32_t* meas = gp.t.n_tiles <= (uint32_t)rpk::TILE_SORT_MAX ? w->d_meas : nullptr;
   int e = rpk::launch_gather_pack(d_counters, gp.plan_hash, meas, gp.stride_tiles, w->d_pack_send, st);
   if (e != 0) return fail(RP_EHIP, std::string("gather pack launch: ") + hipGetErrorString((hipError_t)e));
-  if (bgra && gp.t.n_slots) {
-    e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb, gp.t.n_slots, reinterpret_cast<uint8_t*>(w->d_pack_send + gp.head),
-                              st);
+  for (uint32_t f = 0; bgra && gp.t.n_slots && f < gp.nf; f++) {  // frame f's bytes at head + f x bgra_words
+    e = rpk::launch_srgb_bgra(srgb_table(), d_shard_rgb + 3 * gp.t.n_slots * (uint64_t)f, gp.t.n_slots,
+                              reinterpret_cast<uint8_t*>(w->d_pack_send + gp.head + bgra_words(gp.t) * f), st);
     if (e != 0) return fail(RP_EHIP, std::string("output stage launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (rgb && gp.t.n_slots && d_shard_rgb != w->d_gs_rgb)
@@ -1058,7 +1064,7 @@ int gather_stage(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const doubl
 // RCCL all-gather kernel on gfx950 needs 37.7 KB of LDS and 256 VGPRs per lane, so with frames in flight each one
 // waits ~8-24 ms for a CU the render waves leave (profiles/r5/c3_gather_lds_wait.json).
 int gather_collectives(ncclComm_t comm, rp_workspace* w, const GatherPlan& gp, bool bgra, bool rgb, hipStream_t st) {
-  RP_NCCL(ncclAllGather(w->d_pack_send, w->d_pack_recv, pack_words(gp.t, bgra), ncclUint32, comm, st));
+  RP_NCCL(ncclAllGather(w->d_pack_send, w->d_pack_recv, pack_words(gp.t, bgra, gp.nf), ncclUint32, comm, st));
   if (rgb) RP_NCCL(ncclAllGather(w->d_gs_rgb, w->d_gather_rgb, 3 * gp.stride, ncclFloat64, comm, st));
   return RP_OK;
 }
@@ -1072,7 +1078,7 @@ int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_re
   } else {
     // rank r's sums at r * block + 2 GATHER_CTR, its maxima stride_tiles further
     const uint32_t* sums = w->d_pack_recv + 2 * rpk::GATHER_CTR;
-    int e = rpk::launch_learn_costs(sums, sums + gp.stride_tiles, (uint32_t)pack_words(gp.t, bgra), gp.geom.nranks,
+    int e = rpk::launch_learn_costs(sums, sums + gp.stride_tiles, (uint32_t)pack_words(gp.t, bgra, gp.nf), gp.geom.nranks,
                                     gp.t.n_tiles, gp.t.balanced ? w->d_plan : nullptr, w->d_fcost, st);
     if (e != 0) return fail(RP_EHIP, std::string("cost table launch: ") + hipGetErrorString((hipError_t)e));
     set_fcost(w, p, gp.t, gp.geom.nranks);
@@ -1087,14 +1093,15 @@ int gather_learn(rp_scene* s, rp_workspace* w, const GatherPlan& gp, const rp_re
 int gather_assemble(rp_scene* s, rp_workspace* w, const GatherPlan& gp, uint8_t* d_frame_bgra, double* d_frame_rgb,
                     uint64_t* d_counters, hipStream_t st) {
   DeviceGuard g(s->device);
-  const uint64_t block = pack_words(gp.t, d_frame_bgra != nullptr);
+  const uint64_t block = pack_words(gp.t, d_frame_bgra != nullptr, gp.nf);
   int e = rpk::launch_counters_reduce(reinterpret_cast<const uint64_t*>(w->d_pack_recv), gp.geom.nranks, block,
                                       d_counters ? d_counters : w->d_ctr, st);
   if (e != 0) return fail(RP_EHIP, std::string("counter reduce launch: ") + hipGetErrorString((hipError_t)e));
-  if (d_frame_bgra) {
+  for (uint32_t f = 0; d_frame_bgra && f < gp.nf; f++) {  // frame f into its own W x H x 4 bytes
     rpk::FrameGeom fg = gp.geom;
     fg.rank_words = block;
-    e = rpk::launch_frame_assemble(fg, w->d_pack_recv + gp.head, 1, reinterpret_cast<uint32_t*>(d_frame_bgra), st);
+    e = rpk::launch_frame_assemble(fg, w->d_pack_recv + gp.head + bgra_words(gp.t) * f, 1,
+                                   reinterpret_cast<uint32_t*>(d_frame_bgra + 4ull * gp.geom.W * gp.geom.H * f), st);
     if (e != 0) return fail(RP_EHIP, std::string("frame assembly launch: ") + hipGetErrorString((hipError_t)e));
   }
   if (d_frame_rgb) {
@@ -1565,6 +1572,25 @@ int rp_frame_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_pa
   if ((rc = gather_collectives(c->comm, w, gp, bgra, rgb, st))) return rc;
   if ((rc = gather_learn(s, w, gp, p, bgra, st))) return rc;
   return gather_assemble(s, w, gp, d_frame_bgra, d_frame_rgb, d_counters, st);
+}
+
+int rp_frames_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t n_frames,
+                     const double* d_shard_rgb, uint8_t* d_frames_bgra, uint64_t* d_counters, void* stream) {
+  if (!c || !s || !d_shard_rgb) return fail(RP_EINVAL, "comm, scene and shards must be non-NULL");
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
+  if (!w) w = &s->ws0;
+  if (c->device != s->device) return fail(RP_EINVAL, "the communicator's device is not the scene's");
+  if (reinterpret_cast<uintptr_t>(d_frames_bgra) % 4 != 0) return fail(RP_EINVAL, "d_frames_bgra must be 4-byte aligned");
+  GatherPlan gp;
+  int rc = gather_plan(s, w, c->nranks, c->rank, p, gp, n_frames);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const bool bgra = d_frames_bgra != nullptr;
+  DeviceGuard g(s->device);
+  if ((rc = gather_stage(s, w, gp, d_shard_rgb, bgra, false, d_counters, st))) return rc;
+  if ((rc = gather_collectives(c->comm, w, gp, bgra, false, st))) return rc;
+  if ((rc = gather_learn(s, w, gp, p, bgra, st))) return rc;
+  return gather_assemble(s, w, gp, d_frames_bgra, nullptr, d_counters, st);
 }
 
 int rp_render_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,

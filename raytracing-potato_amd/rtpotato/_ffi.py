@@ -137,7 +137,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
               "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
               "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times",
-              "rp_workspace_frame_info", "rp_workspace_reserve_frames", "rp_render_frames_device_ws"]
+              "rp_workspace_frame_info", "rp_workspace_reserve_frames", "rp_render_frames_device_ws", "rp_frames_gather"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_selfcheck_ex", "rph_bvh_traversal_stats_ex", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64", "rph_make_div32"]
@@ -215,6 +215,8 @@ def rp() -> ctypes.CDLL:
     lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_workspace_frame_info.argtypes = [c_void_p, c_void_p, POINTER(c_uint32)]
     lib.rp_workspace_reserve_frames.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32]
+    lib.rp_frames_gather.argtypes = [c_void_p, c_void_p, c_void_p, POINTER(rp_render_params), c_uint32, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]
     lib.rp_render_frames_device_ws.argtypes = [c_void_p, c_void_p, POINTER(rp_camera), POINTER(rp_render_params),
                                                c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.rp_workspace_set_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]

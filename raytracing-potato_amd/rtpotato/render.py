@@ -243,6 +243,23 @@ class DeviceScene:
                                        counters.data_ptr() if counters is not None else None,
                                        ctypes.c_void_p(s.cuda_stream)))
 
+    def frames_gather(self, comm: "Comm", params: RenderParams, n_frames: int, shard_rgb, frames_bgra=None,
+                      counters=None, stream=None, workspace: "Workspace | None" = None) -> None:
+        """rp_frames_gather: the n_frames shards of one render_frames_device launch (`shard_rgb`, back to back) in one
+        all-gather; `frames_bgra` (torch uint8, n_frames * W*H*4) receives the assembled frames back to back."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(shard_rgb.device)
+        n = params.width * params.height
+        if frames_bgra is not None:
+            assert frames_bgra.dtype == torch.uint8 and frames_bgra.is_cuda and frames_bgra.numel() >= 4 * n * n_frames
+        assert shard_rgb.dtype == torch.float64 and shard_rgb.numel() >= 3 * shard_slot_count(params) * n_frames
+        p = params.to_c()
+        F.check(F.rp().rp_frames_gather(comm.handle, self.handle, workspace.handle if workspace else None,
+                                        ctypes.byref(p), n_frames, shard_rgb.data_ptr(),
+                                        frames_bgra.data_ptr() if frames_bgra is not None else None,
+                                        counters.data_ptr() if counters is not None else None,
+                                        ctypes.c_void_p(s.cuda_stream)))
+
     def render_gather(self, comm: "Comm", params: RenderParams, frame_bgra=None, frame_rgb=None, counters=None,
                       camera=None, stream=None, workspace: "Workspace | None" = None) -> None:
         """rp_render_gather: render this rank's shard and gather the frame (see frame_gather)."""

@@ -196,3 +196,50 @@ def test_frames_lens_camera(gpu):
         sc, p = _scene(name, 48, 32, 16)
         with gpu.DeviceScene(sc) as ds:
             _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=4), 4))
+
+
+@pytest.mark.parametrize("sps", [8, 0])
+def test_frames_gather_equals_per_frame_gathers(gpu, sps):
+    """rp_frames_gather (one all-gather for a launch's frames) on a one-rank RCCL communicator: the n assembled BGRA8
+    frames equal rp_frame_gather's of each frame's shard, byte for byte, and the counters are the launch's; without a
+    frame buffer it still gathers the counters; an unreserved workspace is refused."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.render import Comm, comm_unique_id
+    from rtpotato.scene import shard_slot_count
+    sc, p = _scene("bunny_full", 72, 40, 24)
+    p = replace(p, samples_per_stream=sps, tile_w=16, tile_h=16)
+    n = shard_slot_count(p)
+    dev = torch.device("cuda", 0)
+    nf = 3
+    with gpu.DeviceScene(sc) as ds, Comm(comm_unique_id(), 1, 0, 0) as comm:
+        w = ds.workspace()
+        ds.reserve_frames(p, nf, w)
+        shards = torch.zeros(3 * n * nf, dtype=torch.float64, device=dev)
+        ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+        ds.render_frames_device(p, nf, shards, ctr, workspace=w)
+        c_launch = ctr.clone()
+        frames = torch.zeros(4 * p.width * p.height * nf, dtype=torch.uint8, device=dev)
+        ds.frames_gather(comm, p, nf, shards, frames_bgra=frames, counters=ctr, workspace=w)
+        one = torch.zeros(4 * p.width * p.height, dtype=torch.uint8, device=dev)
+        c1 = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+        per = []
+        for f in range(nf):
+            ds.frame_gather(comm, p, shards[3 * n * f:3 * n * (f + 1)], frame_bgra=one, counters=c1, workspace=w)
+            torch.cuda.synchronize()
+            per.append(one.cpu().numpy().copy())
+        c2 = c_launch.clone()
+        ds.frames_gather(comm, p, nf, shards, counters=c2, workspace=w)
+        torch.cuda.synchronize()
+        got = frames.cpu().numpy().reshape(nf, -1)
+        for f in range(nf):
+            assert np.array_equal(got[f], per[f]), f
+        assert ctr.cpu().tolist() == c_launch.cpu().tolist() == c2.cpu().tolist()
+        assert len(set(bytes(x) for x in got)) == nf  # different seeds: different frames
+        w2 = ds.workspace()
+        ds.reserve(p, w2)
+        ds.render_frames_device(p, 1, shards, ctr, workspace=w2)
+        with pytest.raises(F.RPError, match="rp_workspace_reserve_frames"):
+            ds.frames_gather(comm, p, nf, shards, frames_bgra=frames, counters=ctr, workspace=w2)
+        w2.close()
+        w.close()
