@@ -10,10 +10,10 @@ scaling: the frame is fixed), rendered by the persistent HIP kernel (librp.so) f
 by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one RCCL all-gather of those 4 bytes per
 pixel over xGMI (one collective per launch for all its frames, rp_frames_gather), and the device-side de-interleave into
 frame order on every rank (the body of the reference's output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
-communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered L = 16 to a
-launch (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
+communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered in launches of
+at most L = 32 (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
 config's frame of seed + f * B * W * H, every frame traced, shaded and gathered in full.  The rate of lone frames (one
-per launch) is reported beside it (single_frame).  With N > 1 three launches are in flight on their own streams and
+per launch) is reported beside it (single_frame).  With N > 1 up to three launches are in flight on their own streams and
 workspaces (--inflight; an 8-way C3 shard: 26.0 / 25.9 / 25.7 ms per frame with 1 / 2 / 3).
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is
 used.
@@ -224,7 +224,7 @@ def main():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight: consecutive frames alternate over this many streams and workspaces "
                          "(0 = 1 on one GPU, 3 on several)")
-    ap.add_argument("--frames-per-launch", type=int, default=16,
+    ap.add_argument("--frames-per-launch", type=int, default=32,
                     help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
                          "the frame of seed + f * B * W * H); a step is still one frame (K frames in launches of <= L)")
     ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved"),
@@ -292,7 +292,10 @@ def main():
     # paths (VALU / ray +10 %, L2 hit rate 0.72 vs 0.75 for a shard).  Interleaving L frames narrows the band L times:
     # C3 207.1 -> 202.5 ms per frame at L = 8, an 8-way shard 28.6 -> 26.1 ms, the one-stream contract 261 -> 204 ms
     # (profiles/r5/c3_frames_per_launch_ab.json); with one tile of every frame per queue chunk (v56) C3 205.3 / 199.4 /
-    # 198.5 / 197.2 ms at L = 1 / 8 / 16 / 32 (c3_frames_chunk_auto_sweep.json, c3_frames_per_launch_large.json).  A step is still one frame: K steps = K frames in launches of <= L.
+    # 198.5 / 197.2 ms at L = 1 / 8 / 16 / 32 (c3_frames_chunk_auto_sweep.json, c3_frames_per_launch_large.json).  A step
+    # is still one frame: K steps = K frames in the fewest launches of <= L.  The driver's 20 steps: one launch of 20 at
+    # L = 32, 198.3 ms per frame, against two of 10 at L = 16, 199.1 ms; an 8-way shard's projected N = 8 efficiency
+    # 0.976 vs 0.973 (profiles/r5/c3_v57_driver_cmd_L{16,32}_bench.json, c3_v57_scale_projection_pl{10,20}_f20.json).
     # Frames in flight: launch k renders on stream k % F with its own workspace and shard buffers; the frame gathers
     # (RCCL collectives) run on the main stream in frame order.  F = 1 is the plain sequential loop, whose launch
     # duration (HIP events, the rocprofv3 kernel trace) is the time of its L frames the roofline is priced on.
