@@ -236,6 +236,7 @@ def test_bench_launch_sizes():
     b = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(b)
     assert b.launch_sizes(20, 8) == [7, 7, 6]
+    assert b.launch_sizes(20, 32) == [20] and b.launch_sizes(20, 16) == [10, 10]  # the driver's 20 steps at L = 32 / 16
     assert b.launch_sizes(16, 8) == [8, 8] and b.launch_sizes(8, 8) == [8] and b.launch_sizes(5, 8) == [5]
     assert b.launch_sizes(0, 8) == [] and b.launch_sizes(3, 1) == [1, 1, 1]
     assert b.launch_sizes(5, 8, 3) == [2, 2, 1] and b.launch_sizes(2, 8, 2) == [1, 1]
