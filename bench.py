@@ -11,9 +11,14 @@ by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one R
 pixel over xGMI (one collective per launch for all its frames, rp_frames_gather), and the device-side de-interleave into
 frame order on every rank (the body of the reference's output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
 communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered in launches of
-at most L = 32 (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): frame f of a launch is the
-config's frame of seed + f * B * W * H, every frame traced, shaded and gathered in full.  The rate of lone frames (one
-per launch) is reported beside it (single_frame).  With N > 1 up to three launches are in flight on their own streams and
+at most L = 32 (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): the process renders
+ONE sequence -- warm-up, timed, single-frame and side-leg launches take its next frames, frame f the config's frame of
+seed + f * B * W * H (B sample batches per pixel), so no timed frame repeats a warm-up frame's seeds -- every frame
+traced, shaded and gathered in full.  `value` is that frame-sequence throughput: no frame of a launch is available
+before the launch ends (~L x 0.2 s on C3); the rate of lone frames (one per launch) is reported beside it
+(single_frame).  RNG contract: on one GPU SURVEY.md 8c's one stream per pixel (samples_per_stream = spp), with the
+32-sample streams of N > 1 runs timed beside it (streams_of_32); N > 1: 32-sample streams, the one-stream contract
+beside it (contract_one_stream).  With N > 1 up to three launches are in flight on their own streams and
 workspaces (--inflight; an 8-way C3 shard: 26.0 / 25.9 / 25.7 ms per frame with 1 / 2 / 3).
 The timed region is K steps bracketed by a barrier + torch.cuda.synchronize() on both sides; the max over ranks is
 used.
@@ -93,17 +98,22 @@ def reference_equivalent(config: str):
     return sum(BYTES[k] * per[k] for k in BYTES)
 
 
-def kernel_record(config: str):
-    """The committed per-ray record of the current frame kernel for this config (profiles/current.json ->
-    a tools/roofline.py record over rocprofv3 --pmc passes): memory-side bytes per ray, VALU / SALU
-    instructions per ray, cycle budget."""
+def kernel_record(config: str, sps: int):
+    """The committed per-ray record of the current frame kernel for this config and RNG contract (profiles/current.json
+    -> a tools/roofline.py record over rocprofv3 --pmc passes; key "<config>" or "<config>@<samples_per_stream>", the
+    record's own samples_per_stream must match): memory-side bytes per ray, VALU / SALU instructions per ray, cycle
+    budget."""
     try:
-        rel = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"][config]
+        cur = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"]
     except (OSError, KeyError):
         return None
-    rec = json.load(open(os.path.join(REPO, rel)))
-    rec["source"] = rel
-    return rec
+    for key in (config, f"{config}@{sps}"):
+        if key in cur:
+            rec = json.load(open(os.path.join(REPO, cur[key])))
+            if rec.get("samples_per_stream", 32) == sps:
+                rec["source"] = cur[key]
+                return rec
+    return None
 
 
 class stdout_to_stderr:
@@ -200,10 +210,40 @@ def launch_sizes(n: int, per_launch: int, min_launches: int = 0) -> list:
     return [n // parts + (1 if j < n % parts else 0) for j in range(parts)]
 
 
-def frames_per_launch_cap(per_launch: int, slots: int, batches: int) -> int:
-    """Frames per launch, at most what keeps a launch's units (slots x sample batches x frames) below 2^31, the unit
-    decode's bound in rp_api.cpp: a C5 frame (16.8 M pixels of 8 batches) takes at most 15 a launch."""
-    return max(1, min(per_launch, ((1 << 31) - 1) // (max(1, slots) * max(1, batches))))
+# resident lanes of a launch, at most: 256 CUs x 32 one-wave blocks x 64 lanes (rp_api.cpp render_shard's queue bound)
+LANES_MAX = 256 * 32 * 64
+
+
+def frames_per_launch_cap(per_launch: int, slots: int, batches: int, lanes: int = LANES_MAX) -> int:
+    """Frames per launch, at most what rp_api.cpp render_shard accepts for a launch of n = slots x sample batches x
+    frames units: n < 2^31 (the unit decode) and, with per-XCD queues, 2 n + resident lanes < 2^32 - 1 (a queue word
+    takes its units plus one failed fetch per lane and per drained queue passed): a C5 frame (16.8 M pixels of 8
+    batches) takes at most 15 a launch."""
+    units = min((1 << 31) - 1, (0xFFFFFFFE - lanes) // 2)
+    return max(1, min(per_launch, units // (max(1, slots) * max(1, batches))))
+
+
+U64 = (1 << 64) - 1
+
+
+def frame_seed(seed: int, nbatch: int, width: int, height: int, f: int) -> int:
+    """The RNG-contract seed of frame f of a frame sequence (rp_render_frames_device_ws: frame f of a launch whose
+    params carry `seed` renders with seed + f * B * W * H, B = sample batches per pixel), wrapping like u64."""
+    return (seed + f * nbatch * width * height) & U64
+
+
+class FrameSeq:
+    """The frame sequence of one process: every launch renders the next frames of it, so warm-up, timed, single-frame
+    and side-leg frames have disjoint seeds -- the timed frames' tile costs are learned from earlier
+    frames, as in a real sequence.  launch(p, n) -> the params whose launch renders frames f0 .. f0 + n - 1."""
+
+    def __init__(self):
+        self.next = 0
+
+    def launch(self, seed: int, nbatch: int, width: int, height: int, n: int) -> tuple:
+        f0 = self.next
+        self.next += n
+        return f0, frame_seed(seed, nbatch, width, height, f0)
 
 
 def main():
@@ -214,8 +254,9 @@ def main():
     ap.add_argument("--config", default="C3")
     ap.add_argument("--spp", type=int, default=0, help="override the config's spp (0 = config)")
     ap.add_argument("--samples-per-stream", type=int, default=0,
-                    help="rp_render_params.samples_per_stream, the RNG contract (0 = RP_SAMPLES_PER_STREAM = 32; "
-                         ">= spp: one stream per pixel, SURVEY.md 8c)")
+                    help="rp_render_params.samples_per_stream, the RNG contract (0 = auto: SURVEY.md 8c's one stream "
+                         "per pixel, = spp, on one GPU; RP_SAMPLES_PER_STREAM = 32 for N > 1 and --shard-of; >= spp: "
+                         "one stream per pixel)")
     ap.add_argument("--tile", type=int, default=0,
                     help="tile side in pixels (rp_render_params.tile_w/tile_h; 0 = the config's 32): scheduling only, "
                          "the image does not depend on it")
@@ -238,8 +279,9 @@ def main():
     ap.add_argument("--shard-map", default="auto", choices=("auto", "interleave", "balanced"),
                     help="tile deal across ranks (rp_render_params.shard_map); auto = balanced for N > 1 or --shard-of")
     ap.add_argument("--contract-steps", type=int, default=-1,
-                    help="frames timed after the headline under SURVEY.md 8c's RNG contract itself (one stream per "
-                         "pixel, samples_per_stream = spp), reported as contract_one_stream (-1 = 3 for the default "
+                    help="frames timed after the headline under the other RNG contract: 32-sample streams when the "
+                         "headline is SURVEY.md 8c's one stream per pixel (N = 1), reported as streams_of_32, else the "
+                         "one-stream contract, reported as contract_one_stream (-1 = a launch's worth for the default "
                          "workload, 0 = off)")
     ap.add_argument("--opt", action="append", default=[],
                     help="rp_scene_options field=value (tuning; e.g. --opt trav_threshold=20)")
@@ -267,12 +309,17 @@ def main():
     options = {}
     for kv in args.opt:
         k, v = kv.split("=", 1)
-        options[k] = float(v) if k == "cost_traverse" else (v if k in ("builder", "engine", "node_format", "tile_order", "unit_queues", "collapse", "node_layout", "primary", "unit_order") else int(v))
+        options[k] = float(v) if k == "cost_traverse" else (v if k in ("builder", "node_format", "tile_order", "unit_queues", "collapse", "node_layout", "unit_order") else int(v))
     scene, params = scenes.config_scene(args.config)
     if args.spp:
         params = replace(params, spp=args.spp)
-    if args.samples_per_stream:
-        params = replace(params, samples_per_stream=args.samples_per_stream)
+    # The RNG contract: on one GPU the headline is SURVEY.md 8c's contract itself -- one
+    # StdRng::seed_from_u64(seed + j W + i) per pixel running main.rs:70-86 over all spp -- which renders C3 as fast as
+    # 32-sample streams once a launch holds a frame sequence (BENCH_r05: 196.4 vs 198.4 ms).  N > 1 keeps 32-sample
+    # streams: an 8-way shard of one-stream units is ~1 unit per resident lane and ran 9 % slower.
+    sps_auto = args.samples_per_stream == 0 and world == 1 and not args.shard_of
+    if args.samples_per_stream or sps_auto:
+        params = replace(params, samples_per_stream=args.samples_per_stream or params.spp)
     if args.tile:
         params = replace(params, tile_w=args.tile, tile_h=args.tile)
     t = time.time()
@@ -319,10 +366,14 @@ def main():
     frames = torch.zeros(params.height * params.width * 4 * L, dtype=torch.uint8, device=dev)  # a launch's frames
     state = {"k": 0}
     launches_all = []  # (frames, start, end) of every launch of this process, warm-up and side runs included
+    seq = FrameSeq()  # warm-up, timed, single-frame and side-leg frames: one sequence, disjoint seeds
 
     def step(n, k_start=None, k_end=None, spx=None):
-        """One launch of n <= L frames on the next workspace, then their gathers."""
+        """One launch of n <= L frames (the next n of the process's frame sequence) on the next workspace, then their
+        gathers."""
         spx = spx if spx is not None else sp
+        nb = -(-spx.spp // (spx.samples_per_stream or F.RP_SAMPLES_PER_STREAM))
+        spx = replace(spx, seed=seq.launch(spx.seed, nb, spx.width, spx.height, n)[1])
         i = state["k"] % F_
         state["k"] += 1
         st = streams[i]
@@ -398,6 +449,8 @@ def main():
     single = None
     if L > 1 and not args.no_single_frame:
         nsf = 3
+        for _ in range(F_):  # one lone frame per workspace first: it learns the unit durations a lone frame schedules
+            step(1)          # by (rp_scene_options.unit_order AUTO: one stream per pixel)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -414,34 +467,43 @@ def main():
         single = {"frames": nsf, "ms_per_frame": round(float(tm.item()) / nsf * 1e3, 3),
                   "value": round(r1 * nsf / float(tm.item()) / 1e6, 3), "unit": "Mrays/s",
                   "note": "one frame per launch (rp_render_frames_device_ws, n_frames 1) on the same streams and "
-                          "workspaces: the rate of lone frames; the headline renders frame sequences of frames_per_launch "
-                          "frames per launch"}
+                          "workspaces, after one untimed lone frame per workspace: the rate of lone frames (the learned "
+                          "unit order under one stream per pixel); the headline renders frame sequences of "
+                          "frames_per_launch frames per launch"}
 
-    # SURVEY.md 8c's RNG contract itself: one StdRng stream per pixel running the unchanged body of
-    # main.rs:70-86 over all spp (samples_per_stream = spp), timed the same way after the headline frames
-    contract = None
+    # The other RNG contract, timed the same way after the headline frames: with the one-stream headline (N = 1) the
+    # 32-sample streams N > 1 runs use (streams_of_32), else SURVEY.md 8c's contract itself (contract_one_stream: one
+    # StdRng stream per pixel running the unchanged body of main.rs:70-86 over all spp).
+    side, side_key = None, None
+    one_stream = params.samples_per_stream >= params.spp
     csteps = args.contract_steps if args.contract_steps >= 0 else (
-        (L if L > 1 else 3) if not (args.samples_per_stream or args.shard_of or args.spp or args.tile) else 0)
-    if csteps > 0 and params.spp > (params.samples_per_stream or F.RP_SAMPLES_PER_STREAM):
-        pc = replace(params, samples_per_stream=params.spp)
-        spc = shard_params(pc, rank, world)
+        (L if L > 1 else 3) if (sps_auto or not args.samples_per_stream) and not (args.shard_of or args.spp or args.tile)
+        else 0)
+    if csteps > 0 and params.spp > F.RP_SAMPLES_PER_STREAM:
+        side_key = "streams_of_32" if one_stream else "contract_one_stream"
+        side_sps = F.RP_SAMPLES_PER_STREAM if one_stream else params.spp
+        spc = shard_params(replace(params, samples_per_stream=side_sps), rank, world)
         for w in wss:
             ds.reserve_frames(spc, L, w)
         for _ in range(F_):  # one launch per in-flight workspace: each learns this contract's tile costs
             step(1, spx=spc)
             torch.cuda.synchronize()
         tcs, _, crays, _, csz = run(spc, csteps, events=False)
-        contract = {"samples_per_stream": params.spp, "steps": csteps, "warmup": F_, "launches": csz,
-                    "ms_per_step": round(tcs / csteps * 1e3, 3),
-                    "value": round(crays * csteps / tcs / 1e6, 3), "unit": "Mrays/s",
-                    "rays_per_frame": int(crays),
-                    "note": "SURVEY.md 8c: one StdRng::seed_from_u64(seed + j*W + i) stream per pixel over all spp "
-                            "(main.rs:70-86 unchanged); the headline uses streams of samples_per_stream samples"}
+        side = {"samples_per_stream": side_sps, "steps": csteps, "warmup": F_, "launches": csz,
+                "ms_per_step": round(tcs / csteps * 1e3, 3),
+                "value": round(crays * csteps / tcs / 1e6, 3), "unit": "Mrays/s",
+                "rays_per_frame": int(crays),
+                "note": ("the 32-sample streams (RP_SAMPLES_PER_STREAM) that N > 1 runs use: batch b of a pixel is "
+                         "StdRng::seed_from_u64(seed + b*W*H + j*W + i); the headline is SURVEY.md 8c's one stream per "
+                         "pixel") if one_stream else
+                        ("SURVEY.md 8c: one StdRng::seed_from_u64(seed + j*W + i) stream per pixel over all spp "
+                         "(main.rs:70-86 unchanged); the headline uses streams of samples_per_stream samples")}
 
     if rank == 0:
         local_rays = rays_step / world  # this rank's launch (shards carry near-equal work under the balanced plan)
-        # the per-ray record is of the default workload (its spp and RNG batches)
-        rec = kernel_record(args.config) if args.spp == 0 and args.samples_per_stream == 0 and args.tile == 0 else None
+        # the per-ray record is of the default workload (its spp, RNG contract and tile size)
+        rec = kernel_record(args.config, params.samples_per_stream or F.RP_SAMPLES_PER_STREAM) \
+            if args.spp == 0 and args.tile == 0 else None
         build = F.rp().rp_build_id().decode()
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "traffic": None,
                 "kernel": "rpk::render_kernel<false, *>", "kernel_ms": round(kernel_launch_ms, 3),
@@ -522,11 +584,16 @@ def main():
             "metric": METRIC, "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed_max / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "note": "frame-sequence throughput: the K timed frames in launches of frames_per_launch (no frame is "
+                    "available before its launch ends); single_frame = one frame per launch (lone-frame latency)",
             "data": "reference assets (bunny.obj, earthmap.tga packed in-repo) + synthesized sky panorama",
             "config": {"workload": f"{args.config}: {scenes.CONFIGS[args.config].description}",
                        "width": params.width, "height": params.height, "spp": params.spp,
                        "max_bounce": params.max_bounce, "seed": params.seed,
-                       "samples_per_stream": params.samples_per_stream or 32, "tile": [params.tile_w, params.tile_h],
+                       "samples_per_stream": params.samples_per_stream or 32,
+                       "rng_contract": "SURVEY.md 8c: one stream per pixel" if one_stream else
+                                       f"streams of {params.samples_per_stream or 32} samples",
+                       "tile": [params.tile_w, params.tile_h],
                        "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
                        "frames_in_flight": F_, "frames_per_launch": L,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
@@ -540,7 +607,7 @@ def main():
             "binding_resource": binding[0] if binding else None,
             "cpu_baseline": None,
             "single_frame": single,
-            "contract_one_stream": contract,
+            **({side_key: side} if side_key else {}),
         }
         if world == 1 and not args.no_cpu_baseline and not args.shard_of:
             log("[rank 0] cpu baseline ...")

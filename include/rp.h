@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define RP_ABI_VERSION 8
+#define RP_ABI_VERSION 9
 
 /* Default samples per RNG stream (see "Determinism" above; rp_render_params.samples_per_stream = 0). */
 #define RP_SAMPLES_PER_STREAM 32
@@ -203,10 +203,6 @@ typedef struct rp_render_params {
 /* Builders: HOST = multi-threaded binned SAH on the CPU; DEVICE = LBVH on the GPU (Karras 2012: fastest build,
  * Morton-split tree); PLOC = agglomerative clustering on the GPU (Meister & Bittner 2018: SAH-quality tree). */
 enum { RP_BUILDER_AUTO = 0, RP_BUILDER_HOST = 1, RP_BUILDER_DEVICE = 2, RP_BUILDER_PLOC = 3 };
-/* Render engines (same images bit for bit): the persistent megakernel (traversal and shading on the same
- * lanes) and the stage-split engine (trace and shade passes over a pool of path slots; its renders
- * synchronise the host: the pass loop polls the ray queue). */
-enum { RP_ENGINE_MEGAKERNEL = 0, RP_ENGINE_WAVEFRONT = 1 };
 /* Wide-node formats: 128 B f32 child boxes, or 64 B child boxes quantized to 8 bits per plane in a per-node
  * f32 frame (half the node bytes, more ALU per visit).  AUTO = Q8 for host-built trees of >= 2^21 hittables,
  * F32 otherwise. */
@@ -231,20 +227,13 @@ enum { RP_COLLAPSE_AUTO = 0, RP_COLLAPSE_GREEDY = 1, RP_COLLAPSE_SAH = 2 };
  * line (64-B quantized nodes: a pad slot after odd families; f32 nodes are one line each, so the same as DFS).  Speed
  * only: the image never depends on it. */
 enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
-/* rp_scene_options.primary (ABI v8): the coherent primary pass.  ON: when the camera's lens_radius is 0 (a camera
- * ray's direction then depends only on its jitter, render.rs:36-44,74-82) and the workspace is reserved for it
- * (rp_workspace_reserve: 4 bytes per pixel and sample of the shard), every camera ray of the frame is traced first in
- * waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 samples), and the path loop starts each sample from that
- * closest hit instead of traversing: the same image (the closest hit does not depend on the order rays are traced,
- * up to exact-t ties).  OFF: camera rays traverse in the path loop.  AUTO: the library's choice --
- * ON where it measured faster, else OFF. */
-enum { RP_PRIMARY_AUTO = 0, RP_PRIMARY_OFF = 1, RP_PRIMARY_ON = 2 };
 /* rp_scene_options.unit_order (ABI v8): the order the unit queues hand out a shard's (pixel, sample stream) units.
- * TILES: tile by tile (tile_order), a tile's pixels row-major.  LEARNED: every render stores each unit's duration,
- * and the next frame of the same shape on the same workspace hands out its units longest first (in log-spaced
- * buckets that keep shard order inside; a frame ends with its longest unit), on one device or interleaved shards
- * (a balanced plan's tiles may move between frames: those frames keep TILES).  AUTO = TILES: the learned order lost
- * 6-28 % on C3 and C5.  Results never depend on it. */
+ * TILES: tile by tile (tile_order), a tile's pixels row-major.  LEARNED: every render of one frame per launch stores each
+ * unit's duration, and the next such frame of the same shape on the same workspace hands out its units longest first
+ * (log-spaced buckets, shard order inside; a frame ends with its longest unit), on one device or interleaved shards (a
+ * balanced plan's tiles may move between frames: those frames keep TILES).  AUTO (ABI v9) = LEARNED for one stream per
+ * pixel (samples_per_stream >= spp: lone C3 frames 220 vs 261 ms), TILES for several streams per pixel (32-sample streams:
+ * +4.4 %).  Launches of several frames always use TILES.  Results never depend on it. */
 enum { RP_UNITS_AUTO = 0, RP_UNITS_TILES = 1, RP_UNITS_LEARNED = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster
@@ -258,8 +247,6 @@ typedef struct rp_scene_options {
                                scenes within the 256 MB Infinity Cache, 32 above; 1..64) */
   uint32_t tile_order;      /* RP_TILES_*: the order the unit queue hands out a shard's tiles */
   uint32_t probe_n;         /* cost probe lattice n x n per tile (0 -> 16) */
-  uint32_t engine;          /* RP_ENGINE_*: the persistent megakernel or the stage-split wavefront engine */
-  uint32_t wf_slots;        /* wavefront engine: paths in flight per resident lane (0 -> 2) */
   uint32_t node_format;     /* RP_NODES_* */
   uint32_t leaf_break;      /* speculative traversal: a wave moves to the leaf tests once at most this many of its
                                lanes still look for a leaf (0 -> 8 for scenes within the 256 MB Infinity Cache,
@@ -273,9 +260,10 @@ typedef struct rp_scene_options {
                                render reports RP_STATUS_STACK_OVERFLOW / RP_EINTERNAL: the error path made reachable. */
   uint32_t collapse;        /* RP_COLLAPSE_*: the 4-wide collapse of the host-built tree (ABI v6) */
   uint32_t node_layout;     /* RP_LAYOUT_*: node order of a device-built (PLOC) tree (ABI v7) */
-  uint32_t primary;         /* RP_PRIMARY_*: the coherent primary pass (ABI v8) */
   uint32_t unit_order;      /* RP_UNITS_*: tile order or the learned per-unit order (ABI v8) */
 } rp_scene_options;
+/* ABI v9 removed the measured-and-lost options of v5-v8: `engine` / `wf_slots` (the stage-split
+ * engine) and `primary` (the coherent primary pass). */
 
 typedef struct rp_stats {
   uint64_t rays;      /* root scene.hit() calls, primary + secondary (render.rs:105,133) */
@@ -382,8 +370,7 @@ int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const 
  * (rp_workspace_reserve_frames; it also reserves what rp_workspace_reserve does).  The shard's tiles (a balanced plan)
  * and their order are made once for the launch: from the workspace's learned cost table, or from a probe of frame 0 --
  * a probed plan follows its seed, so a balanced shard of frame f > 1 may hold other tiles than rp_render_device's frame
- * of that seed would (the pixels are the same; rp_workspace_tile_map gives the launch's deal).  Megakernel engine only;
- * the coherent primary pass and the learned unit order do not apply.  n_frames <= RP_MAX_FRAMES.
+ * of that seed would (the pixels are the same; rp_workspace_tile_map gives the launch's deal).  n_frames <= RP_MAX_FRAMES.
  * frame_order (RP_FRAME_ORDER_*): SEQUENTIAL hands out frame 0's units, then frame 1's, ...; INTERLEAVED hands out the
  * frames' k-th tiles of the cost order together, for k = 0, 1, ... -- the units in flight at any moment come from a
  * narrower band of the cost order (fewer lanes idle in a wave whose neighbours run longer paths), every frame ends near
@@ -396,15 +383,21 @@ int rp_render_frames_device_ws(rp_scene* scene, rp_workspace* workspace, const r
                                const rp_render_params* params, uint32_t n_frames, uint32_t frame_order,
                                double* d_shard_rgb,
                                float* d_shard_fg, uint64_t* d_counters, void* stream);
-/* How the last render enqueued with `workspace` (NULL = the scene's) was scheduled (ABI v8): RP_FRAME_* bits.
- * Host state only (no device synchronisation); results never depend on any of it. */
+/* How the last render enqueued with `workspace` (NULL = the scene's) was scheduled (ABI v8): RP_FRAME_* bits (0 after
+ * a render that launched nothing: spp = 0, an empty shard, a refused call).  Host state only (no device
+ * synchronisation); results never depend on any of it.  (Bit 1 belonged to the coherent primary pass, removed in v9.) */
 enum {
-  RP_FRAME_PRIMARY_PASS = 1,  /* the coherent primary pass traced the camera rays (rp_scene_options.primary) */
   RP_FRAME_LEARNED_ORDER = 2, /* tiles ordered / dealt from the workspace's learned cost table */
   RP_FRAME_PROBED = 4,        /* a cost probe launch ran */
   RP_FRAME_UNIT_ORDER = 8     /* units handed out in the learned per-unit order (rp_scene_options.unit_order) */
 };
 int rp_workspace_frame_info(const rp_scene* scene, const rp_workspace* workspace, uint32_t* flags);
+/* Inspection of the learned per-unit order (ABI v9; tests and tools): the last render with `workspace` (NULL = the
+ * scene's) stored each of its units' durations in 100 MHz ticks -- unit u = slot * nbatch + batch in shard order --
+ * when it could learn them (one frame per launch, unit_order LEARNED or AUTO with one stream per pixel, a reserved
+ * workspace), and handed its units out in `order` when its frame_info has RP_FRAME_UNIT_ORDER.  Copies n entries of each
+ * (NULL = skip) to the host; n must not exceed the workspace's reservation.  Synchronises the device. */
+int rp_workspace_unit_order(rp_scene* scene, rp_workspace* workspace, uint32_t* durations, uint32_t* order, uint64_t n);
 /* The deal order of params' frame (one entry per frame tile; shard s's k-th tile is tile_map[s + k*num_shards]):
  * for RP_SHARD_BALANCED the plan the last render of this frame in `workspace` (NULL = the scene's) made, for the
  * interleave 0, 1, 2, ...  n >= the frame's tile count.  Synchronises the device. */

@@ -86,8 +86,6 @@ constexpr uint32_t DEF_MAX_LEAF = 4, DEF_TRAV_THRESHOLD = 24, DEF_ALWAYS_MAX = 4
 constexpr uint32_t DEF_UNIT_QUEUES = RP_QUEUES_XCD_TILES;
 constexpr uint32_t QUEUE_CHUNK_AUTO = 8;  // rp_scene_options.queue_chunk = 0: tiles per queue chunk (render_shard)
 constexpr double DEF_COST_TRAVERSE = 0.7;
-// Largest hint buffer a workspace reserves for the coherent primary pass (4 B per pixel and sample of a shard).
-constexpr uint64_t PRIM_HINT_MAX_BYTES = 64ull << 30;
 // Balanced plans under tile_order = RP_TILES_MORTON deal square blocks of tiles (rpk::launch_tile_plan): 4 x 4, or 2 x 2,
 // as long as every rank still gets >= PLAN_UNITS_MIN of them (balance needs many units per rank), else single tiles.
 // (AUTO is the cost order for every scene since v49, which deals tile by tile; the block deal runs only when a caller
@@ -120,8 +118,6 @@ struct rp_workspace {
   double* d_partial = nullptr;       // per-batch sample sums of multi-batch frames
   uint32_t* d_partial_hits = nullptr;
   uint64_t partial_units = 0;        // capacity of d_partial / d_partial_hits in units
-  int32_t* d_hint = nullptr;         // the coherent primary pass's closest primitive per shard slot and sample
-  uint64_t hint_cap = 0;             // capacity of d_hint in entries
   // the learned per-unit order (rp_sched.hip): each unit's duration in the last render, the sort keys (two buffers),
   // the radix sort's scratch and the order; ucost_geom = the frame shape the durations belong to
   uint32_t* d_ucost = nullptr;
@@ -158,7 +154,6 @@ struct rp_workspace {
   bool fcost_valid = false;
   uint32_t fcost_geom[4] = {0, 0, 0, 0};  // width, height, tile_w, tile_h of the learned table
   uint32_t fcost_ranks = 0;               // ranks whose gather made it (1: a whole-frame render on one device)
-  rpk::WfBuffers wf{};               // the stage-split engine's path-slot pool (engine = wavefront only)
   // A frame gather reads this workspace's measured costs (d_meas) and writes its learned table (d_fcost) on the gather
   // stream; the next render on the workspace reads the table and clears d_meas on ITS stream.  The gather records
   // this event at its end and render_shard waits on it, so a caller with separate render and gather streams cannot
@@ -211,16 +206,11 @@ struct rp_multi {
 namespace {
 
 void ws_release(rp_workspace* w) {
-  for (void* p : {(void*)w->wf.ray, (void*)w->wf.tp, (void*)w->wf.sum, (void*)w->wf.hit, (void*)w->wf.prim,
-                  (void*)w->wf.st, (void*)w->wf.wc})
-    dfree(p);
-  if (w->wf.host_count) (void)hipHostFree(w->wf.host_count);
   for (void* p : {(void*)w->d_ctr, (void*)w->d_probe_ctr, (void*)w->d_queue, (void*)w->d_tile_cost,
                   (void*)w->d_tile_order, (void*)w->d_slab, (void*)w->d_spill, (void*)w->d_partial,
                   (void*)w->d_partial_hits, (void*)w->d_gs_rgb, (void*)w->d_gather_rgb, (void*)w->d_pack_send,
                   (void*)w->d_pack_recv, (void*)w->d_plan, (void*)w->d_meas, (void*)w->d_fcost, (void*)w->d_sort,
-                  (void*)w->d_t0,
-                  (void*)w->d_hint, (void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder,
+                  (void*)w->d_t0, (void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder,
                   w->d_usort})
     dfree(p);
   if (w->ev_gathered) (void)hipEventDestroy(w->ev_gathered);
@@ -242,22 +232,6 @@ int ws_alloc(rp_scene* s, rp_workspace* w) {
       !dalloc(&w->d_t0, lanes) || hipEventCreateWithFlags(&w->ev_gathered, hipEventDisableTiming) != hipSuccess) {
     ws_release(w);
     return fail(RP_ENOMEM, "hipMalloc render workspace");
-  }
-  if (s->opt.engine == RP_ENGINE_WAVEFRONT) {
-    rpk::WfBuffers& b = w->wf;
-    const uint64_t P = lanes * s->opt.wf_slots;
-    if (P >= 0x7fffffffull) {
-      ws_release(w);
-      return fail(RP_EINVAL, "too many wavefront path slots");
-    }
-    b.P = (uint32_t)P;
-    b.poll = 8;
-    if (!dalloc(&b.ray, 2 * 6 * P) || !dalloc(&b.tp, 2 * 3 * P) || !dalloc(&b.sum, 2 * 3 * P) ||
-        !dalloc(&b.hit, 3 * P) || !dalloc(&b.prim, P) || !dalloc(&b.st, 2 * 7 * P) || !dalloc(&b.wc, 4) ||
-        hipHostMalloc(reinterpret_cast<void**>(&b.host_count), sizeof(uint32_t)) != hipSuccess) {
-      ws_release(w);
-      return fail(RP_ENOMEM, "hipMalloc wavefront path slots");
-    }
   }
   return RP_OK;
 }
@@ -370,8 +344,6 @@ rp_scene_options default_options() {
   o.trav_threshold = 0;  // auto (scene_create): DEF_TRAV_THRESHOLD, or 32 for scenes past the Infinity Cache
   o.tile_order = 0;
   o.probe_n = rpk::PROBE_LATTICE_N;
-  o.engine = RP_ENGINE_MEGAKERNEL;
-  o.wf_slots = 2;
   o.debug_stack_depth = 0;
   return o;
 }
@@ -390,9 +362,6 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
   if (o.trav_threshold > 64) return fail(RP_EINVAL, "options.trav_threshold must be 1..64");
   if (o.tile_order > RP_TILES_PROBE) return fail(RP_EINVAL, "options.tile_order must be RP_TILES_*");
   if (o.probe_n == 0) o.probe_n = d.probe_n;
-  if (o.engine > RP_ENGINE_WAVEFRONT) return fail(RP_EINVAL, "options.engine must be RP_ENGINE_*");
-  if (o.wf_slots == 0) o.wf_slots = d.wf_slots;
-  if (o.wf_slots > 64) return fail(RP_EINVAL, "options.wf_slots must be 1..64");
   if (o.node_format > RP_NODES_W8) return fail(RP_EINVAL, "options.node_format must be RP_NODES_*");
   if (o.leaf_break > 64) return fail(RP_EINVAL, "options.leaf_break must be 0..64");
   if (o.unit_queues > RP_QUEUES_XCD_REGIONS) return fail(RP_EINVAL, "options.unit_queues must be RP_QUEUES_*");
@@ -401,7 +370,6 @@ int resolve_options(const rp_scene_options* in, rp_scene_options& o) {
     return fail(RP_EINVAL, "options.debug_stack_depth must be 0 or 8..4096");
   if (o.collapse > RP_COLLAPSE_SAH) return fail(RP_EINVAL, "options.collapse must be RP_COLLAPSE_*");
   if (o.node_layout > RP_LAYOUT_DFS_LINE) return fail(RP_EINVAL, "options.node_layout must be RP_LAYOUT_*");
-  if (o.primary > RP_PRIMARY_ON) return fail(RP_EINVAL, "options.primary must be RP_PRIMARY_*");
   if (o.unit_order > RP_UNITS_LEARNED) return fail(RP_EINVAL, "options.unit_order must be RP_UNITS_*");
   return RP_OK;
 }
@@ -412,20 +380,13 @@ uint64_t stage_slots(const Tiling& t) {
   return (uint64_t)n0 * t.tw * t.th;
 }
 
-// The learned per-unit order (rp.h RP_UNITS_*) is kept for this scene: LEARNED, megakernel engine.  AUTO = TILES:
-// longest-first units lost on both configs and both RNG contracts (C3 261.5 vs 206.4 ms, one stream per pixel 337.8 vs
-// 262.8, C5 1,628.6 vs 1,531.4 ms; profiles/r5/c3_c5_unit_order_ab.json) -- a wave's 64 units are then unrelated
-// pixels, and the neighbouring pixels (and a pixel's batches) of the tile order trace coherent paths.
-bool units_on(const rp_scene* s) {
-  return s->opt.unit_order == RP_UNITS_LEARNED && s->opt.engine == RP_ENGINE_MEGAKERNEL;
-}
-
-// The coherent primary pass runs for this scene (rp.h RP_PRIMARY_*): ON, megakernel engine.  AUTO is OFF: measured
-// against the path loop's own camera-ray traversal it lost on both configs (C3 226.9 vs 205.7 ms: the render kernel's
-// time did not move without its camera rays; C5 1,987 vs 1,528 ms: the render kernel -27 %, the pass +57 %), DESIGN.md
-// 4.8, profiles/r5/c3_c5_primary_pass_ab.json.
-bool primary_on(const rp_scene* s) {
-  return s->opt.primary == RP_PRIMARY_ON && s->opt.engine == RP_ENGINE_MEGAKERNEL;
+// The learned per-unit order (rp.h RP_UNITS_*) for frames of nbatch sample streams per pixel: LEARNED always, AUTO
+// for one stream per pixel (nbatch 1).  Measured with round 6's bucket fix (profiles/r6/c3_unit_order_fix_ab.json,
+// lone C3 frames): one stream per pixel 220.1 ms against 260.8 ms in tile order -- the longest pixels (glass-bunny
+// paths of ~2,000 rays) start first instead of ending the frame -- while 32-sample streams lose 4.4 % (213.8 vs 204.8:
+// a wave's units become pixels scattered over the frame, and their 8 short streams leave no long tail to fix).
+bool units_on(const rp_scene* s, uint32_t nbatch) {
+  return s->opt.unit_order == RP_UNITS_LEARNED || (s->opt.unit_order == RP_UNITS_AUTO && nbatch == 1);
 }
 
 // Words of a rank's packed gather block (rpk::launch_gather_pack): the counter block and 2 x tiles per rank of measured
@@ -465,20 +426,9 @@ int ws_reserve(rp_scene* s, rp_workspace* w, const rp_render_params* p, bool gat
   DeviceGuard g(s->device);
   const uint64_t units = t.nbatch > 1 ? t.n_slots * t.nbatch * n_frames : 0;
   if ((rc = grow(w->d_partial, w->d_partial_hits, w->partial_units, units, 3, 1, "sample-batch workspace"))) return rc;
-  // the coherent primary pass's hints: 4 bytes per shard slot and sample (C3 2.1 GB, C5 17 GB of the 288 GB HBM); a
-  // frame past PRIM_HINT_MAX_BYTES renders without the pass
-  const uint64_t hints = t.n_slots * p->spp;
-  if (primary_on(s) && hints > w->hint_cap &&
-      hints * sizeof(int32_t) <= PRIM_HINT_MAX_BYTES) {
-    dfree(w->d_hint);
-    w->d_hint = nullptr;
-    w->hint_cap = 0;
-    if (!dalloc(&w->d_hint, hints)) return fail(RP_ENOMEM, "hipMalloc primary-pass hints");
-    w->hint_cap = hints;
-  }
-  // the learned per-unit order: 4 + 8 + 8 + 4 bytes per unit and the sort's scratch (C3: 16.6 M units, 400 MB)
+  // the learned per-unit order: 4 + 8 + 8 + 4 bytes per unit and the sort's scratch (C3 one stream: 2.1 M units, 50 MB)
   const uint64_t n_units = t.n_slots * t.nbatch;
-  if (units_on(s) && n_units > w->ucost_cap && n_units < (1ull << 31)) {
+  if (units_on(s, t.nbatch) && n_units > w->ucost_cap && n_units < (1ull << 31)) {
     for (void* q : {(void*)w->d_ucost, (void*)w->d_ukey, (void*)w->d_ukey2, (void*)w->d_uorder, w->d_usort}) dfree(q);
     w->d_ucost = w->d_uorder = nullptr;
     w->d_ukey = w->d_ukey2 = nullptr;
@@ -662,16 +612,18 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->ks.n_always = ps.n_always;
   s->ks.qbound = ps.qbound;
   s->ks.node_format = node_format;
-  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
-  // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
-  s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
-  // Node8Q: groups of two words, per level at most the rest of a node group and one primitive group
+  // Stack sizes are in 32-bit words.  A 4-wide node pushes at most 3 entries (its non-nearest hits) per level below
+  // the root, +3 spare entries for the kernel's branchless push (rp_device.h STACK_SLACK); an entry is two words, the
+  // child and its t_near (rp_device.h trav_step).  Node8Q: groups of two words, per level at most the rest of a node
+  // group and one primitive group, +3 spare words.
+  const uint32_t epw = node_format == rpl::NODES_W8 ? 1u : 2u;  // words per stack entry
+  s->ks.stack_depth = epw * (3 * ps.max_depth + 4 + 3);
   if (node_format == rpl::NODES_W8) s->ks.stack_depth = 4 * (ps.max_depth + 1) + 3;
-  // floor of 17 entries: the spill split below never keeps fewer in LDS (options.lds_depth tests force 17)
-  if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
+  // floor of 17 entries: the spill split below never keeps fewer words in LDS than LDS_FLOOR
+  if (s->ks.stack_depth < epw * 17) s->ks.stack_depth = epw * 17;
   // test-only: a stack too small for the tree (the kernels flag RP_STATUS_STACK_OVERFLOW, never write past it)
   const bool debug_stack = opt.debug_stack_depth != 0;
-  if (debug_stack) s->ks.stack_depth = opt.debug_stack_depth;
+  if (debug_stack) s->ks.stack_depth = epw * opt.debug_stack_depth;
   s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
@@ -691,23 +643,24 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // lanes still traversing before the finished ones shade: C3 24 (16: +0.2 %, 32: +0.7 %), C5 32 (-1.6 %)
   if (s->opt.trav_threshold == 0) s->opt.trav_threshold = s->device_bytes > (256ull << 20) ? 32u : DEF_TRAV_THRESHOLD;
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
-  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
-  // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  options.lds_depth
-  // forces a depth (>= 17) for tests and tuning.
+  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth (whole entries) that still
+  // fits the occupancy of a shallow stack (C3's 31 entries of two words: 9 in LDS for 4 blocks per SIMD).
+  // options.lds_depth forces a depth in entries (>= 8) for tests and tuning.
+  const uint32_t floor_w = node_format == rpl::NODES_W8 ? 17u : 16u;  // LDS words never fewer than this
   s->ks.lds_depth = s->ks.stack_depth;
   int bpc = 0;
   if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   int bpc_spill = 0;
-  if (!debug_stack && rpk::render_blocks_per_cu(17, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
+  if (!debug_stack && rpk::render_blocks_per_cu(floor_w, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
     uint32_t L = s->ks.stack_depth - 1;
     int b = 0;
-    while (L > 17 && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
-    s->ks.lds_depth = L;
+    while (L > floor_w && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
+    s->ks.lds_depth = std::max(floor_w, L - L % epw);
     bpc = bpc_spill;
   }
-  if (!debug_stack && opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
-    s->ks.lds_depth = opt.lds_depth;
-    if (rpk::render_blocks_per_cu(opt.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
+  if (!debug_stack && opt.lds_depth && epw * opt.lds_depth < s->ks.stack_depth) {
+    s->ks.lds_depth = epw * opt.lds_depth;
+    if (rpk::render_blocks_per_cu(s->ks.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   }
   s->blocks_per_cu = bpc;
   phase[4] = lap();
@@ -724,9 +677,8 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
                  uint32_t frame_order = RP_FRAME_ORDER_AUTO) {
   if (!s || !cam || !d_rgb) return fail(RP_EINVAL, "scene, camera and output must be non-NULL");
   if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
+  w->frame_flags = 0;  //  before any return: an spp = 0 or refused render reports no scheduling
   if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
-  if (n_frames > 1 && s->opt.engine != RP_ENGINE_MEGAKERNEL)
-    return fail(RP_EINVAL, "several frames per launch: megakernel engine only");
   if (frame_order > RP_FRAME_ORDER_INTERLEAVED) return fail(RP_EINVAL, "frame_order must be an RP_FRAME_ORDER_* value");
   Tiling t;
   int rc = make_tiling(p, t);
@@ -777,10 +729,8 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.frames_inter = n_frames > 1 && frame_order != RP_FRAME_ORDER_SEQUENTIAL ? 1u : 0u;
   kp.out_stride = 3 * t.n_slots;
   // Per-XCD queues (rp.h RP_QUEUES_*): groups of blocks blockIdx mod 8 share an XCD (MI355X_MICROARCH.md,
-  // observed round-robin dispatch; speed only -- any placement gives the same image).  The stage-split engine
-  // keeps the single queue.
+  // observed round-robin dispatch; speed only -- any placement gives the same image).
   uint32_t qmode = s->opt.unit_queues == RP_QUEUES_AUTO ? (uint32_t)DEF_UNIT_QUEUES : s->opt.unit_queues;
-  if (s->opt.engine == RP_ENGINE_WAVEFRONT) qmode = RP_QUEUES_SINGLE;
   kp.queue_groups = qmode == RP_QUEUES_SINGLE ? 1u : (uint32_t)rpk::QUEUE_GROUPS;
   // Default chunk: up to 8 consecutive (virtual) tiles of the order per queue at a time, while every queue still gets >= 16
   // chunks -- the tiles one XCD runs together are then neighbours in cost and, inside a cost bucket, in Z-order (a whole C3
@@ -865,15 +815,14 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   uint32_t probe_px = 0;
   const uint32_t* frame_cost = nullptr;  // per-frame-tile costs (sum, max) the plan and the shard order use
   w->plan_on = false;
-  w->frame_flags = 0;
   // Scheduling costs.  The megakernel measures every unit's duration into its tile's cost (kp.tile_meas); once a
   // frame of this geometry has been rendered whole on one device, or gathered from all ranks, the workspace holds a
   // learned per-tile table and the next frame schedules from it -- no probe launch.  For a balanced plan over
   // N > 1 ranks the table must come from a gather over the same N ranks: every rank then holds the same bytes and
-  // deals the same plan.  Otherwise a probe (the first frame, the stage-split engine) supplies the costs.
+  // deals the same plan.  Otherwise a probe (the first frame) supplies the costs.
   // (the measured table holds TILE_SORT_MAX tiles: a shard of more tiles -- 8 x 8 tiles at 1080p, say -- is not
   // measured, and its frame keeps the probe / interleave)
-  const bool measure = s->opt.engine == RP_ENGINE_MEGAKERNEL && t.n_shard_tiles <= (uint32_t)rpk::TILE_SORT_MAX;
+  const bool measure = t.n_shard_tiles <= (uint32_t)rpk::TILE_SORT_MAX;
   const bool probe_order = order_mode == RP_TILES_PROBE;
   if (probe_order) order_mode = RP_TILES_COST;
   const bool learned = measure && !probe_order && fcost_matches(w, p, t);
@@ -921,36 +870,15 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     if (e != 0) return fail(RP_EHIP, std::string("tile sort launch: ") + hipGetErrorString((hipError_t)e));
     kp.tile_order = w->d_tile_order;
   }
-  // The coherent primary pass (rp.h RP_PRIMARY_AUTO): camera rays of a lens-less camera traced in neighbouring waves of
-  // 64 before the path loop, which then starts every sample at its closest hit.  Needs the workspace's hint buffer
-  // (rp_workspace_reserve); without it, or with a lens, camera rays traverse in the path loop.
-  const uint64_t n_hints = t.n_slots * p->spp;
-  if (n_frames == 1 && primary_on(s) && cam->lens_radius == 0.0 && w->d_hint && n_hints <= w->hint_cap) {
-    kp.prim_quads_x = (t.tw + 1) / 2;
-    kp.prim_sgroups = (p->spp + rpk::PRIM_SAMPLES - 1) / rpk::PRIM_SAMPLES;
-    const uint64_t per_tile = (uint64_t)kp.prim_quads_x * ((t.th + 1) / 2) * kp.prim_sgroups;
-    // queue g's words count its tiles' items, plus one failed fetch per wave and per queue it passes
-    const uint64_t per_queue = ((t.n_shard_tiles + rpk::QUEUE_GROUPS - 1) / rpk::QUEUE_GROUPS) * per_tile;
-    if (per_tile < (1ull << 31) && per_queue + resident * rpk::QUEUE_GROUPS < 0xffffffffull) {
-      kp.prim_items_tile = (uint32_t)per_tile;
-      kp.prim_hint = w->d_hint;
-      kp.dv_sps = rpk::make_div32(t.sps);
-      const uint64_t items = per_tile * t.n_shard_tiles;
-      // 8-wide trees traverse lane by lane with the render kernel's spill runs (its grid); the 4-wide packet traversal
-      // keeps its stack in LDS and runs at its own occupancy (<= 96 VGPRs: 5 waves per SIMD)
-      const int pgrid = ks.node_format == rpl::NODES_W8 ? grid_for(items * rpk::RENDER_BLOCK)
-                                                        : (int)std::min<uint64_t>(items, (uint64_t)s->num_cu * 20);
-      int e = rpk::launch_primary(ks, kp, ctr, w->d_queue + rpk::QUEUE_PRIM, pgrid, stream);
-      if (e != 0) return fail(RP_EHIP, std::string("primary pass launch: ") + hipGetErrorString((hipError_t)e));
-      w->frame_flags |= RP_FRAME_PRIMARY_PASS;
-    }
-  }
-  // The learned per-unit order (rp.h RP_UNITS_LEARNED): units longest first by the last render's durations on this
-  // workspace -- same frame shape and shard, and not a balanced plan over several ranks (its tiles may move) -- and
-  // every render stores its units' durations for the next one.
+  // The learned per-unit order (rp.h RP_UNITS_*, units_on): units longest first by the last render's durations on this
+  // workspace -- same frame shape and shard, one frame per launch, and not a balanced plan over several ranks (its tiles
+  // may move) -- and such renders store their units' durations for the next one.  The workspace's durations and order
+  // are committed only once the launch is enqueued.
   const uint64_t n_units = t.n_slots * t.nbatch;
   const uint32_t ugeom[8] = {p->width, p->height, t.tw, t.th, p->spp, t.sps, t.shard, t.shards};
-  const bool ufit = n_frames == 1 && units_on(s) && w->d_ucost && n_units <= w->ucost_cap && (!t.balanced || t.shards == 1);
+  const bool ufit = n_frames == 1 && units_on(s, t.nbatch) && w->d_ucost && n_units <= w->ucost_cap &&
+                    (!t.balanced || t.shards == 1);
+  bool uorder = false;
   if (ufit && w->ucost_valid && std::memcmp(ugeom, w->ucost_geom, sizeof ugeom) == 0) {
     int e = rpk::launch_unit_order(w->d_ucost, n_units, w->d_ukey, w->d_ukey2, w->d_usort, w->usort_bytes, w->d_uorder,
                                    stream);
@@ -959,18 +887,20 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     kp.order_chunk = rpk::UNIT_ORDER_CHUNK;
     kp.dv_ochunk = rpk::make_div32(kp.order_chunk);
     kp.dv_tile_px = rpk::make_div32(t.tw * t.th);
-    w->frame_flags |= RP_FRAME_UNIT_ORDER;
+    uorder = true;
   }
   if (ufit) kp.unit_cost = w->d_ucost;
-  w->ucost_valid = ufit;
-  if (ufit) std::memcpy(w->ucost_geom, ugeom, sizeof ugeom);
   RP_HIP(hipMemsetAsync(w->d_meas, 0, sizeof(uint32_t) * 2 * rpk::TILE_SORT_MAX, st));
   kp.tile_meas = measure ? w->d_meas : nullptr;
   w->meas_on = measure;
-  int e = s->opt.engine == RP_ENGINE_WAVEFRONT
-              ? rpk::launch_wavefront(ks, kp, d_rgb, d_fg, ctr, w->d_queue, w->wf, (int)resident, stream)
-              : rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
-  if (e != 0) return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+  int e = rpk::launch_render(ks, kp, d_rgb, d_fg, ctr, w->d_queue, grid_for(kp.n_queue), stream);
+  if (e != 0) {
+    w->ucost_valid = false;  // the durations may be partly overwritten
+    return fail(RP_EHIP, std::string("render launch: ") + hipGetErrorString((hipError_t)e));
+  }
+  if (uorder) w->frame_flags |= RP_FRAME_UNIT_ORDER;
+  w->ucost_valid = ufit;
+  if (ufit) std::memcpy(w->ucost_geom, ugeom, sizeof ugeom);
   if (kp.nbatch > 1) {
     for (uint32_t f = 0; f < n_frames; f++) {  // each frame's batch sums, added in batch order
       rpk::KParams kf = kp;
@@ -1256,6 +1186,19 @@ int rp_workspace_frame_info(const rp_scene* s, const rp_workspace* w, uint32_t* 
   if (!w) w = &s->ws0;
   if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
   *flags = w->frame_flags;
+  return RP_OK;
+}
+
+int rp_workspace_unit_order(rp_scene* s, rp_workspace* w, uint32_t* durations, uint32_t* order, uint64_t n) {
+  if (!s) return fail(RP_EINVAL, "scene is NULL");
+  if (!w) w = &s->ws0;
+  if (w->scene != s) return fail(RP_EINVAL, "workspace belongs to another scene");
+  if (n > w->ucost_cap) return fail(RP_EINVAL, "n exceeds the workspace's per-unit reservation");
+  if (n == 0) return RP_OK;
+  DeviceGuard g(s->device);
+  RP_HIP(hipDeviceSynchronize());
+  if (durations) RP_HIP(hipMemcpy(durations, w->d_ucost, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+  if (order) RP_HIP(hipMemcpy(order, w->d_uorder, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
   return RP_OK;
 }
 

@@ -1,5 +1,5 @@
-// rp_device.h -- device code shared by the gfx950 kernels (rp_kernel.hip: the persistent megakernel;
-// rp_wavefront.hip: the stage-split engine): the rand 0.8 StdRng keystream, f64 vector math, the
+// rp_device.h -- device code of the gfx950 kernels (rp_kernel.hip: the persistent megakernel and the closest-hit
+// query kernel): the rand 0.8 StdRng keystream, f64 vector math, the
 // conservative-f32 wide-BVH traversal with exact f64 primitive tests, and the materials/textures.
 //
 // Arithmetic is IEEE binary64 in the reference's exact operation order (no contraction: the kernels are
@@ -462,7 +462,7 @@ RPK_INLINE double noise_real(int64_t x, int64_t y, int64_t z, int64_t seed) {
 // The closest hit's primitive kind and material travel with it from the accepting test (bit 31 = triangle,
 // bits 0-30 = material; scene_create caps materials below 2^31 - 1): the shading of a triangle hit then
 // starts at the material and vertex loads instead of re-reading the primitive record first (one dependent
-// L2 round trip less).  KM_UNKNOWN: read them from the record (the stage-split engine does not keep them).
+// L2 round trip less).  KM_UNKNOWN: read them from the record (the q8-node kernel, whose traversal would pay the register).
 constexpr uint32_t KM_TRIANGLE = 0x80000000u, KM_UNKNOWN = 0xFFFFFFFFu;
 struct HitRec {
   double t, u, v;  // u, v: barycentrics of hittable.rs:89-95 (triangles)
@@ -596,7 +596,7 @@ struct TravState {
   uint32_t bestm;  // the closest hit's kind and material (HitRec::km)
   uint32_t cur, sp;
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
-  uint32_t gy, py;  // Node8Q only (0 otherwise)
+  uint32_t gy, py;  // Node8Q: the node group's rank word and the parked primitive group; 4-wide: gy = cur's t_near (f32 bits)
 };
 static constexpr uint32_t W8_GROUP = 0x80000000u;  // cur: a node group (prim groups: first primitive < 2^31)
 
@@ -844,6 +844,13 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
   ts.py = py;
 }
 
+// 4-wide step.  Stack entries carry their entry distance: entry i of a lane is the two words 2i (the child entry) and
+// 2i + 1 (its conservative t_near, f32 bits) of the lane's stack column, and TravState::gy holds the current entry's.
+// An entry is popped for nothing once a primitive closer than its box was accepted after it was pushed: `cull` drops
+// such entries without fetching the node (its box test `fma(tnear, 1 - 2^-19, -2^-100) <= best32` is the one that
+// pushed it, section 4.2 of DESIGN.md, with the closest hit found since; a box whose exact interval meets
+// [t_min, best] never fails it).  The CPU traversal model counted 20 % fewer node visits on C3 camera rays, 6 % on
+// interior rays, 4-6 % on C5.
 template <bool SPILL, uint32_t NF, bool COUNT = false>
 RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr,
@@ -853,11 +860,40 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     return;
   }
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
+  float ct = __uint_as_float(ts.gy);  // the current entry's t_near (0 for the root)
   double best = ts.best;
   float best32 = f32_up(best);
-  const uint32_t cap = S.stack_depth - STACK_SLACK;
+  const uint32_t cap = S.stack_depth / 2u - STACK_SLACK;  // entries of two words
+  const auto dead = [&](float t) { return fmaf(t, 1.0f - 0x1p-19f, -0x1p-100f) > best32; };
+  const auto pop = [&]() {
+    --sp;
+    cur = stk_get<SPILL>(S, stk, stride, spl, 2u * sp);
+    ct = __uint_as_float(stk_get<SPILL>(S, stk, stride, spl, 2u * sp + 1u));
+  };
+  // drop the current entry and the entries under it while they lie beyond the closest hit (no node fetch)
+  const auto cull = [&]() {
+    while (cur != rpl::ENTRY_EMPTY && dead(ct)) {
+      if (sp == 0u) cur = rpl::ENTRY_EMPTY;
+      else pop();
+    }
+  };
+  DCYC_BEGIN(cnode)
   // ---- inner nodes
-  while (!(cur & rpl::ENTRY_LEAF)) {
+  for (;;) {
+    cull();
+    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps descending, so lanes do
+    // not idle in this loop until every lane of the wave holds a leaf.  (Not in the cost probe, COUNT: there a lane's
+    // node visits and primitive tests must not depend on its wave-mates, so every rank of a balanced multi-GPU frame
+    // computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
+    if constexpr (!COUNT) {
+      if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+        leaf = cur;
+        if (sp == 0u) cur = rpl::ENTRY_EMPTY;
+        else pop();
+        cull();
+      }
+    }
+    if (cur & rpl::ENTRY_LEAF) break;
     DIAG(if (td) td->visits++;)
     if constexpr (COUNT) *work += WORK_VISIT;
     DREG(DREG_NODE)
@@ -949,111 +985,97 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
 }
     RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
 #undef RPK_CSWAP
-    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1
-    // farther ones far-to-near without branches: slots sp..sp+2 are written unconditionally (the stack
-    // has STACK_SLACK spare entries; slots past the new top are garbage) and sp advances by k.
+    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1 farther ones
+    // far-to-near, each with its t_near, without branches: entries sp..sp+2 are written unconditionally (the stack has
+    // STACK_SLACK spare entries; entries past the new top are garbage) and sp advances by k.
     const float INFF = __builtin_huge_valf();
     const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
                            (uint32_t)(tn[3] != INFF);
     const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
     const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
-    // Whether every lane's pushes and pops of this visit stay in the LDS part of its stack: a wave-uniform branch
-    // (SPILL kernels), so the common case runs no per-lane exec-mask juggling for the spill path.
-    const bool lds_only = !SPILL || __ballot(sp + 2u >= S.lds_depth) == 0;
+    const float t0 = k == 3u ? tn[3] : (k == 2u ? tn[2] : tn[1]), t1 = k == 3u ? tn[2] : tn[1];
+    // Whether every lane's pushes stay in the LDS part of its stack: a wave-uniform branch (SPILL kernels), so the
+    // common case runs no per-lane exec-mask juggling for the spill path.
+    const bool lds_only = !SPILL || __ballot(2u * sp + 6u > S.lds_depth) == 0;
     if (lds_only) {
-      stk[sp * stride] = e0;
-      stk[(sp + 1u) * stride] = e1;
-      stk[(sp + 2u) * stride] = cc[1];
+      stk[2u * sp * stride] = e0;
+      stk[(2u * sp + 1u) * stride] = __float_as_uint(t0);
+      stk[(2u * sp + 2u) * stride] = e1;
+      stk[(2u * sp + 3u) * stride] = __float_as_uint(t1);
+      stk[(2u * sp + 4u) * stride] = cc[1];
+      stk[(2u * sp + 5u) * stride] = __float_as_uint(tn[1]);
     } else {
-      stk_put<SPILL>(S, stk, stride, spl, sp, e0);
-      stk_put<SPILL>(S, stk, stride, spl, sp + 1u, e1);
-      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, cc[1]);
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp, e0);
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 1u, __float_as_uint(t0));
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 2u, e1);
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 3u, __float_as_uint(t1));
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 4u, cc[1]);
+      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 5u, __float_as_uint(tn[1]));
     }
     sp += k;
     if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
       overflow = true;
       sp = cap;
     }
-    // pops below read entries < the pushes' top (sp + 2 before the push), so an LDS-only visit pops from LDS
-    const auto pop = [&]() -> uint32_t {
+    // next: the nearest hit child, else the top of the stack (culled at the top of the loop)
+    if (n_hit) {
+      cur = cc[0];
+      ct = tn[0];
+    } else if (sp == 0u) {
+      cur = rpl::ENTRY_EMPTY;
+    } else if (lds_only) {
       --sp;
-      return lds_only ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
-    };
-    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
-    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
-    // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
-    // every rank of a balanced multi-GPU frame computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
-    if (lds_only) {
-      // the next entry without a branch: the two entries under the top are read at once (indices clamped into the
-      // column; an entry below the stack's bottom is read but never taken), then the pop for a visit that hit no
-      // child and the pop behind a parked leaf are selects
-      const uint32_t t1 = stk[min(sp - 1u, sp) * stride], t2 = stk[min(sp - 2u, sp) * stride];
-      uint32_t npop = (!n_hit && sp) ? 1u : 0u;
-      uint32_t c = n_hit ? cc[0] : (sp ? t1 : rpl::ENTRY_EMPTY);
-      if constexpr (!COUNT) {
-        const bool park = (c & rpl::ENTRY_LEAF) && c != rpl::ENTRY_EMPTY && leaf == 0u;
-        const uint32_t left = sp - npop;
-        leaf = park ? c : leaf;
-        const uint32_t c2 = left ? (npop ? t2 : t1) : rpl::ENTRY_EMPTY;
-        npop += (park && left) ? 1u : 0u;
-        c = park ? c2 : c;
-      }
-      cur = c;
-      sp -= npop;
+      cur = stk[2u * sp * stride];
+      ct = __uint_as_float(stk[(2u * sp + 1u) * stride]);
     } else {
-      if (n_hit) cur = cc[0];
-      else cur = sp ? pop() : rpl::ENTRY_EMPTY;
-      if constexpr (!COUNT) {
-        if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
-          leaf = cur;
-          cur = sp ? pop() : rpl::ENTRY_EMPTY;
-        }
-      }
+      pop();
     }
     if constexpr (!COUNT) {
-      // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
+      // ... and once at most S.leaf_break lanes still look for a leaf, the wave moves on to the leaves: the
       // last few descents ran with most of the wave idle (those lanes resume their descent next step)
       if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
     }
   }
-  // the pops from here on only shrink sp: when no lane's stack reaches into its spill run, they all read LDS (a
-  // wave-uniform branch, as in the node loop)
-  const bool lds_pop = !SPILL || __ballot(sp > S.lds_depth) == 0;
-  const auto pop = [&]() -> uint32_t {
-    --sp;
-    return lds_pop ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
-  };
+  DCYC_END(DCYC_NODE_LOOP, cnode)
+  DCYC_BEGIN(cprim)
+  cull();
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
-    cur = sp ? pop() : rpl::ENTRY_EMPTY;
+    if (sp == 0u) cur = rpl::ENTRY_EMPTY;
+    else pop();
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
-  // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
+  // entry while it is a live leaf as well.  One primitive per lane per iteration across those leaves, so
   // lanes with different leaf sizes advance together instead of the wave running every leaf's count.
-  uint32_t k = leaf & rpl::LEAF_FIRST_MASK;
-  uint32_t kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+  uint32_t kp = leaf & rpl::LEAF_FIRST_MASK;
+  uint32_t kend = kp + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
   while (leaf != 0u) {
     DIAG(if (td) td->tests++;)
     if constexpr (COUNT) *work += WORK_TEST;
     DREG(DREG_PRIM)
-    prim_test(S, k, o, d, tmin, best, ts);
-    if (++k == kend) {
+    prim_test(S, kp, o, d, tmin, best, ts);
+    if (++kp == kend) {
+      best32 = f32_up(best);
+      cull();
       if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
         leaf = cur;
-        cur = sp ? pop() : rpl::ENTRY_EMPTY;
-        k = leaf & rpl::LEAF_FIRST_MASK;
-        kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+        if (sp == 0u) cur = rpl::ENTRY_EMPTY;
+        else pop();
+        kp = leaf & rpl::LEAF_FIRST_MASK;
+        kend = kp + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
       } else {
         leaf = 0u;
       }
     }
     if (!COUNT && PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= PRIM_BREAK) {
-      // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
-      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
+      // park the rest of the current run [kp, kend) as a leaf entry; the next step tests it first
+      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - kp - 1u) << rpl::LEAF_SHIFT) | kp;
       break;
     }
   }
+  DCYC_END(DCYC_PRIM_LOOP, cprim)
   ts.cur = cur;
+  ts.gy = __float_as_uint(ct);
   ts.sp = sp;
   ts.best = best;
   ts.leaf = leaf;
@@ -1072,152 +1094,6 @@ RPK_INLINE void traverse(const KScene& S, lds_u32* stk, uint32_t stride, V3 o, V
   hr.v = t.bv;
   hr.prim = t.bestp;
   hr.km = t.bestm;
-}
-
-// Packet traversal of a coherent wave (the primary pass, rp_kernel.hip primary_kernel; Node4 / Node4Q trees).  The 64
-// lanes' rays leave one pixel quad within a sample's jitter, so the wave walks ONE stack of (entry, lane mask) pairs:
-// at an inner node (a wave-uniform address: one fetch for the wave) each lane of the entry's mask tests the four child
-// boxes with its own conservative slab test and closest hit so far, a child is taken with the mask of the lanes that
-// hit it, nearest first in the order of the mask's first lane; at a leaf the mask's lanes run the exact f64 tests.  A
-// lane tests every subtree its own test accepts (the visit order only changes which exact-t tie wins), so each lane
-// gets its closest hit as in trav_step.  The stack lives in LDS (entries at stk_e, masks at stk_m, `cap` entries),
-// written by lane 0 and read by the wave.
-typedef __attribute__((address_space(3))) unsigned long long lds_u64;
-template <uint32_t NF>
-RPK_INLINE void packet_traverse(const KScene& S, lds_u32* stk_e, lds_u64* stk_m, uint32_t cap,
-                                uint64_t live, const Ray32& r, V3 o, V3 d, double tmin, TravState& ts,
-                                bool& overflow, TravDiag* td = nullptr) {
-  static_assert(NF == rpl::NODES_F32 || NF == rpl::NODES_Q8, "packet traversal: 4-wide trees");
-  const uint32_t lane = __lane_id();
-  uint32_t cur = S.root, sp = 0;
-  uint64_t m = live;
-  double best = ts.best;
-  float best32 = f32_up(best);
-  const char* nb = reinterpret_cast<const char*>(S.nodes);
-  for (;;) {
-    const bool in = (m >> lane) & 1ull;
-    if (m != 0 && !(cur & rpl::ENTRY_LEAF)) {
-      DIAG(if (td && in) td->visits++;)
-      f2 NX[2], FX[2], NY[2], FY[2], NZ[2], FZ[2];
-      uint4 ch;
-      if constexpr (NF == rpl::NODES_Q8) {
-        const uint32_t no = cur << 6;
-        const float4 c0 = *reinterpret_cast<const float4*>(nb + no);
-        const uint4 c1 = *reinterpret_cast<const uint4*>(nb + (no + 16u));
-        const uint4 c2 = *reinterpret_cast<const uint4*>(nb + (no + 32u));
-        ch = *reinterpret_cast<const uint4*>(nb + (no + 48u));
-        const float Ax = c0.w * r.ix, Ay = __uint_as_float(c1.x) * r.iy, Az = __uint_as_float(c1.y) * r.iz;
-        const float Bnx = fmaf(c0.x, r.ix, r.nbx), Bny = fmaf(c0.y, r.iy, r.nby), Bnz = fmaf(c0.z, r.iz, r.nbz);
-        const float Bfx = fmaf(c0.x, r.ix, r.fbx), Bfy = fmaf(c0.y, r.iy, r.fby), Bfz = fmaf(c0.z, r.iz, r.fbz);
-        const uint32_t qnx = __builtin_amdgcn_perm(c1.w, c1.z, r.sx), qfx = __builtin_amdgcn_perm(c1.z, c1.w, r.sx);
-        const uint32_t qny = __builtin_amdgcn_perm(c2.y, c2.x, r.sy), qfy = __builtin_amdgcn_perm(c2.x, c2.y, r.sy);
-        const uint32_t qnz = __builtin_amdgcn_perm(c2.w, c2.z, r.sz), qfz = __builtin_amdgcn_perm(c2.z, c2.w, r.sz);
-        const f2 ax = {Ax, Ax}, ay = {Ay, Ay}, az = {Az, Az};
-        const f2 bnx = {Bnx, Bnx}, bny = {Bny, Bny}, bnz = {Bnz, Bnz}, bfx = {Bfx, Bfx}, bfy = {Bfy, Bfy}, bfz = {Bfz, Bfz};
-#define RPK_Q2(w, h) f2{(float)(((w) >> (16 * (h))) & 0xffu), (float)(((w) >> (16 * (h) + 8)) & 0xffu)}
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-          NX[q] = pk_fma(RPK_Q2(qnx, q), ax, bnx);
-          FX[q] = pk_fma(RPK_Q2(qfx, q), ax, bfx);
-          NY[q] = pk_fma(RPK_Q2(qny, q), ay, bny);
-          FY[q] = pk_fma(RPK_Q2(qfy, q), ay, bfy);
-          NZ[q] = pk_fma(RPK_Q2(qnz, q), az, bnz);
-          FZ[q] = pk_fma(RPK_Q2(qfz, q), az, bfz);
-        }
-#undef RPK_Q2
-      } else {
-        const uint32_t no = cur << 7;
-        const float4 nx = *reinterpret_cast<const float4*>(nb + (no + r.sx));
-        const float4 fx = *reinterpret_cast<const float4*>(nb + (no + (r.sx ^ 16u)));
-        const float4 ny = *reinterpret_cast<const float4*>(nb + (no + r.sy));
-        const float4 fy = *reinterpret_cast<const float4*>(nb + (no + (r.sy ^ 16u)));
-        const float4 nz = *reinterpret_cast<const float4*>(nb + (no + r.sz));
-        const float4 fz = *reinterpret_cast<const float4*>(nb + (no + (r.sz ^ 16u)));
-        ch = *reinterpret_cast<const uint4*>(nb + (no + 96u));
-        const f2 ix = {r.ix, r.ix}, iy = {r.iy, r.iy}, iz = {r.iz, r.iz};
-        const f2 nbx = {r.nbx, r.nbx}, nby = {r.nby, r.nby}, nbz = {r.nbz, r.nbz};
-        const f2 fbx = {r.fbx, r.fbx}, fby = {r.fby, r.fby}, fbz = {r.fbz, r.fbz};
-        NX[0] = pk_fma(f2{nx.x, nx.y}, ix, nbx); NX[1] = pk_fma(f2{nx.z, nx.w}, ix, nbx);
-        FX[0] = pk_fma(f2{fx.x, fx.y}, ix, fbx); FX[1] = pk_fma(f2{fx.z, fx.w}, ix, fbx);
-        NY[0] = pk_fma(f2{ny.x, ny.y}, iy, nby); NY[1] = pk_fma(f2{ny.z, ny.w}, iy, nby);
-        FY[0] = pk_fma(f2{fy.x, fy.y}, iy, fby); FY[1] = pk_fma(f2{fy.z, fy.w}, iy, fby);
-        NZ[0] = pk_fma(f2{nz.x, nz.y}, iz, nbz); NZ[1] = pk_fma(f2{nz.z, nz.w}, iz, nbz);
-        FZ[0] = pk_fma(f2{fz.x, fz.y}, iz, fbz); FZ[1] = pk_fma(f2{fz.z, fz.w}, iz, fbz);
-      }
-      const uint32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
-      float tn[4];
-      uint64_t cm[4];
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-          const int c = 2 * q + e;
-          const float TN = fmaxf(fmaxf(NX[q][e], NY[q][e]), fmaxf(NZ[q][e], r.tmin));
-          const float TF = fminf(fminf(FX[q][e], FY[q][e]), fminf(FZ[q][e], best32));
-          const bool hit = in && fmaf(TN, 1.0f - 0x1p-19f, -0x1p-100f) <= TF && cc[c] != rpl::ENTRY_EMPTY;
-          tn[c] = hit ? TN : __builtin_huge_valf();
-          cm[c] = __ballot(hit);
-        }
-      }
-      // nearest first in the order of the mask's first lane (children it misses after the ones it hits)
-      const int lead = __builtin_ctzll(m);
-      float lt[4];
-      uint32_t ce[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const float v = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tn[c]), lead));
-        lt[c] = !cm[c] ? __builtin_inff() : (v == __builtin_inff() ? 0x1.fffffep127f : v);  // others' hits after the lead's
-        ce[c] = __builtin_amdgcn_readfirstlane(cc[c]);
-      }
-#define RPK_PSWAP(a, b)                                                                 \
-      if (lt[b] < lt[a]) {                                                              \
-        const float t_ = lt[a]; lt[a] = lt[b]; lt[b] = t_;                              \
-        const uint32_t e_ = ce[a]; ce[a] = ce[b]; ce[b] = e_;                           \
-        const uint64_t m_ = cm[a]; cm[a] = cm[b]; cm[b] = m_;                           \
-      }
-      RPK_PSWAP(0, 1) RPK_PSWAP(2, 3) RPK_PSWAP(0, 2) RPK_PSWAP(1, 3) RPK_PSWAP(1, 2)
-#undef RPK_PSWAP
-      // push the farther children with lanes, far first; take the nearest
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        if (cm[c]) {
-          if (sp < cap) {
-            if (lane == 0) {
-              stk_e[sp] = ce[c];
-              stk_m[sp] = cm[c];
-            }
-            sp++;
-          } else {
-            overflow = true;
-          }
-        }
-      }
-      if (cm[0]) {
-        cur = ce[0];
-        m = cm[0];
-        continue;
-      }
-    } else if (m != 0) {
-      // a leaf: the exact f64 tests of its primitives by the mask's lanes
-      const uint32_t k0 = cur & rpl::LEAF_FIRST_MASK, n = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
-      for (uint32_t k = k0; k < k0 + n; k++) {
-        if (in) {
-          DIAG(if (td) td->tests++;)
-          prim_test(S, k, o, d, tmin, best, ts);
-        }
-      }
-      best32 = f32_up(best);
-    }
-    if (sp == 0) break;
-    --sp;
-    cur = __builtin_amdgcn_readfirstlane(stk_e[sp]);
-    const uint64_t mm = stk_m[sp];
-    m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(mm >> 32)) << 32) |
-        (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)mm);
-  }
-  ts.best = best;
-  ts.cur = rpl::ENTRY_EMPTY;
-  ts.leaf = 0u;
 }
 
 // Hit record of the closest primitive (hittable.rs:59-62, 103-107).

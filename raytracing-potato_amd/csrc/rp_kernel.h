@@ -21,11 +21,11 @@ struct KScene {
   double qbound;         // Node4Q: bound on every node frame's |o| and 255 s (rp_layout.h qbound): the slab slack
   uint32_t node_format;  // rpl::NODES_F32 / NODES_Q8: picks the kernel instantiation
   uint32_t leaf_break;   // trav_step leaves the inner-node loop once at most this many lanes still seek a leaf
-  uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
-  uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
+  uint32_t stack_depth;  // traversal stack words per lane (4-wide: 2 x (3 x max_depth + 7), an entry is two words)
+  uint32_t lds_depth;    // words of it in LDS; words [lds_depth, stack_depth) spill to `spill`
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
   uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
-  uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) entries
+  uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) words
   uint32_t* unit_t0;     // per-lane start time of the lane's measured unit (tile costs), render_lanes words
 };
 
@@ -39,15 +39,12 @@ enum { RENDER_BLOCK = 64 };
 // lane primitive tests.
 // [352 + b] units whose duration (100 MHz ticks) has floor(log2) = b + DIAG_DUR_LOG0 (clamped to 0..23), [376 + b]
 // their rays summed.
-// [400 + i] the coherent primary pass (primary_kernel): items, rays, lane node visits, lane primitive tests, wave
-// trav_step calls, wave-cycles in ray setup (key, ChaCha, camera), in traversal and in fetch + store, and the summed
-// per-item maximum of a lane's node visits.
-enum { DIAG_N = 416, DIAG_DUR = 352, DIAG_DUR_N = 24, DIAG_DUR_LOG0 = 10, DIAG_PRIM = 400 };
+enum { DIAG_N = 416, DIAG_DUR = 352, DIAG_DUR_N = 24, DIAG_DUR_LOG0 = 10 };
 // Cycle regions (RPK_DIAG builds), from DIAG_N index DIAG_CYC: wave-cycles spent executing each code region
 enum { DIAG_CYC = 320 };
 enum {
   DCYC_SURF, DCYC_SPHUV, DCYC_TEXISSUE, DCYC_SCATTER, DCYC_TEXVAL, DCYC_EMIT, DCYC_START_SAMPLE, DCYC_END_SAMPLE,
-  DCYC_NEWRAY, DCYC_REFILL, DCYC_NEXT_BOUNCE, DCYC_N
+  DCYC_NEWRAY, DCYC_REFILL, DCYC_NEXT_BOUNCE, DCYC_NODE_LOOP, DCYC_PRIM_LOOP, DCYC_N
 };
 // Timeline histograms (RPK_DIAG builds), 64 bins of DIAG_BIN_TICKS (100 MHz real-time clock) from the
 // block's start: [64 + b] lanes retiring in bin b, [128 + b] rays of the pixels fetched in bin b,
@@ -61,8 +58,7 @@ enum { DIAG_HIST = 64, DIAG_BIN_TICKS = RPK_DIAG_BIN_TICKS };
 enum {
   DREG_NODE, DREG_PRIM, DREG_STEP, DREG_SHADE, DREG_SURF, DREG_SPHUV, DREG_TEX, DREG_LAMBERT, DREG_METAL,
   DREG_DIELEC, DREG_LOOP_LAMBERT, DREG_LOOP_METAL, DREG_END_SAMPLE, DREG_END_PIXEL, DREG_START_SAMPLE,
-  DREG_REFILL, DREG_RNG_FALLBACK, DREG_JIT_FALLBACK, DREG_BEGIN_PIXEL, DREG_RING_LOAD, DREG_ROUND, DREG_MISS,
-  DREG_HINT_FALLBACK, DREG_N
+  DREG_REFILL, DREG_RNG_FALLBACK, DREG_JIT_FALLBACK, DREG_BEGIN_PIXEL, DREG_RING_LOAD, DREG_ROUND, DREG_MISS, DREG_N
 };
 
 // Division by a launch constant d >= 1 of numerators n < 2^31 (Granlund & Montgomery 1994, Thm 4.2 with N = 31):
@@ -109,14 +105,6 @@ struct KParams {
   uint32_t* tile_cost;         // probe: [k] cost (rp_device.h WORK_*: node visits, primitive tests, rays)
                                // summed over the tile's probed samples, [TILE_SORT_MAX + k] the costliest
                                // probed sample (zeroed by the caller)
-  // Coherent primary pass (launch_primary; camera lens_radius == 0 only): per shard slot and sample (slot * spp + the
-  // sample's index in the pixel) the camera ray's closest primitive, -1 = none.  The render kernel reads it at every
-  // camera sample instead of traversing (NULL = off: camera rays traverse in the path loop).
-  int32_t* prim_hint;
-  uint32_t prim_quads_x;       // primary pass: 2 x 2 pixel quads per tile row, ceil(tw / 2)
-  uint32_t prim_items_tile;    // primary pass: work items (64 camera rays: a quad x 16 samples) per tile
-  uint32_t prim_sgroups;       // primary pass: 16-sample groups per pixel, ceil(spp / 16)
-  Div32 dv_sps;                // primary pass: make_div32(spp_batch)
   // Learned per-unit order (launch_unit_order): render -- every unit's duration (100 MHz ticks) is stored at
   // unit_cost[slot * nbatch + batch] (NULL = off); and when unit_order is set the queues hand out units in its order
   // (position p -> unit unit_order[p]; queue g serves the chunks g, g + G, ... of order_chunk positions) instead of
@@ -164,14 +152,8 @@ int launch_learn_costs(const uint32_t* sum, const uint32_t* max, uint32_t rank_s
 enum { SPP_BATCH = 32 };
 
 // Unit-queue words of a workspace: group g's counter at g * QUEUE_STRIDE (own 128 B line), the probe's at
-// QUEUE_PROBE, the primary pass's group g at QUEUE_PRIM + g * QUEUE_STRIDE.
-enum {
-  QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_STRIDE, QUEUE_PRIM = QUEUE_PROBE + QUEUE_STRIDE,
-  QUEUE_WORDS = QUEUE_PRIM + QUEUE_GROUPS * QUEUE_STRIDE
-};
-// Coherent primary pass: a work item is 64 camera rays -- a 2 x 2 pixel quad of one shard tile x PRIM_SAMPLES
-// consecutive samples of each pixel (lane = 16 x quad pixel + sample); items of shard tile k go to queue k mod 8.
-enum { PRIM_SAMPLES = 16 };
+// QUEUE_PROBE.
+enum { QUEUE_GROUPS = 8, QUEUE_STRIDE = 32, QUEUE_PROBE = QUEUE_GROUPS * QUEUE_STRIDE, QUEUE_WORDS = QUEUE_PROBE + QUEUE_STRIDE };
 
 // Counter block layout (RP_COUNTERS_LEN x uint64 in device memory), see rp.h rp_render_device.
 enum { CTR_RAYS = 0, CTR_SAMPLES = 1, CTR_PIXELS = 2, CTR_STATUS = 3, CTR_N = 4 };
@@ -186,17 +168,12 @@ int launch_render(const KScene& s, const KParams& p, double* out_rgb, float* out
                   uint32_t* queue, int grid, void* stream);
 
 // Learned per-unit order (rp_sched.hip): the n units sorted by the previous frame's durations `cost`, longest first, in
-// log-spaced buckets (UNIT_ORDER_Q per octave) that keep shard order inside -> order[0, n).  keys, keys2: n u64 each;
-// scratch: unit_order_scratch_bytes(n) bytes (hipCUB radix sort).  n < 2^31.
-enum { UNIT_ORDER_Q = 4, UNIT_ORDER_CHUNK = 256 };
+// log-spaced buckets (UNIT_ORDER_Q per octave, unit_bucket) that keep shard order inside -> order[0, n).  keys, keys2: n
+// u64 each; scratch: unit_order_scratch_bytes(n) bytes (hipCUB radix sort of UNIT_KEY_BITS bits).  n < 2^31.
+enum { UNIT_ORDER_Q = 4, UNIT_ORDER_CHUNK = 256, UNIT_KEY_BITS = 40 };
 size_t unit_order_scratch_bytes(uint64_t n);
 int launch_unit_order(const uint32_t* cost, uint64_t n, uint64_t* keys, uint64_t* keys2, void* scratch,
                       size_t scratch_bytes, uint32_t* order, void* stream);
-
-// Coherent primary pass over the shard (KParams::prim_hint, lens_radius == 0): every camera ray of the frame traced in
-// waves of 64 neighbouring rays (a 2 x 2 pixel quad x 16 jittered samples), its closest primitive written to prim_hint.
-// `queue` = the workspace's QUEUE_PRIM counters, zeroed on the same stream; grid <= the render grid (the spill runs).
-int launch_primary(const KScene& s, const KParams& p, uint64_t* counters, uint32_t* queue, int grid, void* stream);
 
 // Sort the n (<= TILE_SORT_MAX) probed shard tiles by descending (costliest sample, mean cost per probed
 // pixel), log-quantized, ties by tile index, into order[] (shard tile indices).  One block.
@@ -262,20 +239,6 @@ int launch_frame_assemble(const FrameGeom& g, const uint32_t* gathered, uint32_t
 
 // Blocks of 256 threads resident per CU for the render kernel with this stack depth (occupancy query).
 int render_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t node_format, int* blocks);
-
-// Stage-split engine (rp_wavefront.hip): the path-slot pool of a workspace, structure-of-arrays in device
-// memory, and the host loop of trace / shade passes (synchronous: it polls the ray-queue length every
-// `poll` iterations through the pinned word host_count).
-struct WfBuffers {
-  double *ray, *tp, *sum, *hit;  // two state buffers of 6, 3, 3 doubles per path; hits 3 doubles per path
-  int32_t* prim;                 // 1 per path
-  uint32_t *st, *wc;             // two state buffers of 7 words per path, 4 counters
-  uint32_t* host_count;          // pinned host word
-  uint32_t P, poll;
-};
-int launch_wavefront(const KScene& s, const KParams& p, double* out_rgb, float* out_fg, uint64_t* counters,
-                     uint32_t* queue, const WfBuffers& b, int trace_grid, void* stream);
-int wavefront_trace_blocks_per_cu(uint32_t lds_depth, bool spill, uint32_t node_format, int* blocks);
 
 // Closest-hit query kernel (one ray per thread).
 int launch_intersect(const KScene& s, const double* rays, uint64_t n, double* out_hit, uint32_t* out_mat,

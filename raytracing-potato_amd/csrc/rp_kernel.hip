@@ -141,28 +141,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
       trav_init<NF>(load_scene(A), INF, ts, d);
       tdone = false;
       newray = true;
-      if constexpr (!PROBE) {
-        // the coherent primary pass traced this camera ray already (launch_primary): its closest primitive, re-tested
-        // here with this ray for the exact hit record (t, u, v, material) -- the path starts at shading.  A hint the
-        // test does not accept (never expected: the pass traced the same ray) falls back to traversal.
-        const int32_t* hint = A->P.prim_hint;
-        if (hint) {
-          const int32_t h = hint[(uint64_t)slot * A->P.spp + batch * A->P.spp_batch + s];
-          bool ok = h < 0;
-          if (!ok) {
-            double best = INF;
-            prim_test(load_scene(A), (uint32_t)h, o, d, RAY_EPSILON, best, ts);
-            ts.best = best;
-            ok = ts.bestp == h;
-          }
-          if (ok) {
-            ts.cur = rpl::ENTRY_EMPTY;
-            tdone = true;
-            newray = false;
-          }
-          DIAG(if (!ok) DREG(DREG_HINT_FALLBACK))
-        }
-      }
       start = fresh = false;
     }
     DIAG({ uint64_t t = stamp(); ph[1] += t - t_prev; t_prev = t; })
@@ -276,8 +254,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
             A->P.partial_hits[u] = hits;
           }
           // the unit's duration: its tile's measured cost (rp_kernel.h tile_meas), from one unit in eight (pixel and
-          // batch hashed: every tile's sample spread over its pixels and batches) -- timing all units cost 0.9 %
-          // every unit's duration for the next frame's per-unit order (unit_cost, rp_sched.hip)
+          // batch hashed: every tile's sample spread over its pixels and batches) -- timing all units cost 0.9 % --
+          // and every unit's duration for the next frame's per-unit order (unit_cost, rp_sched.hip)
           const bool mt = !PROBE && A->P.tile_meas && meas_unit(pipj, batch);
           if (!PROBE && (mt || A->P.unit_cost)) {
             const uint32_t dur = (uint32_t)__builtin_amdgcn_s_memrealtime() - A->S.unit_t0[blockIdx.x * BLOCK + tid];
@@ -391,155 +369,6 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
   if (overflow) atomicOr(&ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
   __syncthreads();
   if (threadIdx.x < 3) atomicAdd(&ctr[CTR_RAYS + threadIdx.x], blk_ctr[threadIdx.x]);
-}
-
-// Coherent primary pass (rp_kernel.h launch_primary).  Persistent one-wave blocks; a wave takes a work item -- 64 camera
-// rays: a 2 x 2 pixel quad of one shard tile x PRIM_SAMPLES consecutive samples of each pixel, lane = 16 x quad pixel +
-// sample -- from its XCD group's queue (shard tiles k = g, g + 8, ...), makes the rays' jitter (the samples' keystream
-// words 4 s .. 4 s + 3 of their unit streams, render.rs:74-82; a quad of lanes makes one ChaCha block together), shoots
-// them (Camera::shoot, lens 0) and traverses them with the path loop's own traversal (trav_begin + trav_step), then
-// stores each ray's closest primitive.  The 64 rays leave a pixel quad within a sample's jitter of each other, so the
-// lanes visit nearly the same nodes and leaves: the loads of a visit touch one or two lines instead of 64.
-template <bool SPILL, uint32_t NF>
-__global__ void __launch_bounds__(BLOCK) primary_kernel(const KArgs args) {
-  extern __shared__ uint32_t lds_stack[];
-  lds_u32* stk = (lds_u32*)(lds_stack + threadIdx.x);
-  const uint32_t lane = threadIdx.x;  // BLOCK = one wave
-  bool overflow = false;
-  const uint32_t G = QUEUE_GROUPS, home = blockIdx.x % G;
-  uint32_t tries = 0;
-  DIAG(uint64_t d_items = 0, d_rays = 0, d_steps = 0, d_maxv = 0, c_setup = 0, c_trav = 0, c_rest = 0;
-       TravDiag td; uint64_t t_prev = stamp();)
-  for (;;) {
-    KArgsPtr A = kargs();
-    uint32_t g = home + tries;
-    if (g >= G) g -= G;
-    const uint32_t K = A->P.n_shard_tiles, per = A->P.prim_items_tile;
-    const uint32_t nk = K / G + (g < K % G ? 1u : 0u);  // queue g serves the shard tiles g, g + G, ...
-    uint32_t q = 0;
-    if (lane == 0) q = atomicAdd(A->queue + g * QUEUE_STRIDE, 1u);
-    q = __builtin_amdgcn_readfirstlane(q);
-    if ((uint64_t)q >= (uint64_t)nk * per) {
-      if (++tries >= G) break;  // every queue drained
-      continue;
-    }
-    // (wave-uniform decode, once per 64 rays)
-    const uint32_t i = q / per, rem = q - i * per;
-    const uint32_t k = i * G + g;
-    const uint32_t quad = rem / A->P.prim_sgroups, sg = rem - quad * A->P.prim_sgroups;
-    const uint32_t qy = quad / A->P.prim_quads_x, qx = quad - qy * A->P.prim_quads_x;
-    const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;
-    const uint32_t ty = t / A->P.tiles_x, tx = t - ty * A->P.tiles_x;
-    const uint32_t tw = A->P.tw, th = A->P.th;
-    const uint32_t p = lane >> 4;
-    const uint32_t li = 2u * qx + (p & 1u), lj = 2u * qy + (p >> 1);
-    const uint32_t s = sg * PRIM_SAMPLES + (lane & 15u);
-    const uint32_t pi = tx * tw + li, pj = ty * th + lj;
-    const bool valid = li < tw && lj < th && pi < A->P.W && pj < A->P.H && s < A->P.spp;
-    // the sample's unit stream (RNG contract) and its jitter words 4 sl .. 4 sl + 3 (block sl / 4)
-    const uint32_t batch = udiv(s, A->P.dv_sps.m, A->P.dv_sps.s), sl = s - batch * A->P.spp_batch;
-    uint32_t key[8];
-    seed_key(unit_seed(A, pi, pj, batch), key);
-    uint4 jw;
-    if (A->P.spp_batch % 4u == 0u) {
-      // the quad's four lanes are samples 4 m .. 4 m + 3 of one unit (sl = 4 m + lane % 4): one block, made together
-      jw = quad_row(chacha12_quad(key, sl >> 2), lane & 3u);
-    } else {
-      uint32_t w[16];
-      chacha12(key, sl >> 2, w);
-      const uint32_t r = sl & 3u;
-      jw = r == 0 ? make_uint4(w[0], w[1], w[2], w[3]) : r == 1 ? make_uint4(w[4], w[5], w[6], w[7])
-         : r == 2 ? make_uint4(w[8], w[9], w[10], w[11]) : make_uint4(w[12], w[13], w[14], w[15]);
-    }
-    const double ju = ((double)pi + words_f64(jw.x, jw.y)) / (double)A->P.W;
-    const double jv = ((double)pj + words_f64(jw.z, jw.w)) / (double)A->P.H;
-    V3 o, d;
-    camera_dir(A, ju, jv, 0.0, 0.0, o, d);
-    DIAG(const uint32_t v0 = td.visits;)
-    DIAG({ const uint64_t t = stamp(); c_setup += t - t_prev; t_prev = t; })
-    const KScene S = load_scene(A);
-    TravState ts;
-    trav_begin<NF>(S, o, d, RAY_EPSILON, INF, ts);
-    Ray32 r;
-    setup_ray32<NF>(o, d, RAY_EPSILON, S.qbound, r);
-    if constexpr (NF != rpl::NODES_W8) {
-      // 4-wide trees: one packet traversal for the wave (a stack of entry + lane-mask pairs at the front of the LDS)
-      lds_u32* se = (lds_u32*)lds_stack;
-      lds_u64* sm = (lds_u64*)(lds_stack + ((S.stack_depth + 1u) & ~1u));
-      DIAG(d_steps++;)
-      packet_traverse<NF>(S, se, sm, S.stack_depth, __ballot(valid), r, o, d, RAY_EPSILON, ts, overflow DIAG(, &td));
-    } else {
-      const uint32_t spl = SPILL ? (blockIdx.x * BLOCK + lane) * (S.stack_depth - S.lds_depth) : 0u;
-      bool done = !valid || trav_done(ts);
-      while (__ballot(!done) != 0) {
-        if (!done) {
-          DIAG(d_steps += lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()) ? 1u : 0u;)
-#ifdef RPK_DIAG
-          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow, &td);
-#else
-          trav_step<SPILL, NF>(S, stk, BLOCK, spl, r, o, d, RAY_EPSILON, ts, overflow);
-#endif
-          done = trav_done(ts);
-        }
-      }
-    }
-    DIAG({ const uint64_t t = stamp(); c_trav += t - t_prev; t_prev = t; })
-    DIAG(d_items++; d_rays += valid ? 1u : 0u;
-         uint32_t mv = td.visits - v0;
-         for (int off = 32; off >= 1; off >>= 1) mv = max(mv, (uint32_t)__shfl_xor(mv, off));
-         d_maxv += mv;)
-    if (valid) {
-      const uint64_t slot = (uint64_t)k * tw * th + (uint64_t)lj * tw + li;
-      A->P.prim_hint[slot * A->P.spp + s] = ts.bestp;
-    }
-  }
-  if (overflow) atomicOr(&kargs()->ctr[CTR_STATUS], (unsigned long long)STATUS_STACK_OVERFLOW);
-#ifdef RPK_DIAG
-  {
-    const uint64_t t = stamp();
-    c_rest += t - t_prev;
-    unsigned long long* dg = kargs()->diag + DIAG_PRIM;
-    atomicAdd(&dg[1], (unsigned long long)d_rays);
-    atomicAdd(&dg[2], (unsigned long long)td.visits);
-    atomicAdd(&dg[3], (unsigned long long)td.tests);
-    atomicAdd(&dg[4], (unsigned long long)d_steps);
-    if (lane == 0) {
-      atomicAdd(&dg[0], (unsigned long long)d_items);
-      atomicAdd(&dg[5], (unsigned long long)c_setup);
-      atomicAdd(&dg[6], (unsigned long long)c_trav);
-      atomicAdd(&dg[7], (unsigned long long)c_rest);
-      atomicAdd(&dg[8], (unsigned long long)d_maxv);
-    }
-  }
-#endif
-}
-
-int launch_primary(const KScene& s, const KParams& p, uint64_t* counters, uint32_t* queue, int grid, void* stream) {
-  // the per-lane stack (8-wide trees) or the packet stack: stack_depth entries of 4 + 8 bytes
-  const size_t lds = std::max((size_t)s.lds_depth * BLOCK * sizeof(uint32_t), (size_t)(s.stack_depth + 2) * 12);
-  const bool spill = s.lds_depth < s.stack_depth;
-  KArgs a;
-  a.S = s;
-  a.P = p;
-  a.out = nullptr;
-  a.out_fg = nullptr;
-  a.ctr = reinterpret_cast<unsigned long long*>(counters);
-  a.queue = queue;
-  a.diag = reinterpret_cast<unsigned long long*>(s.diag);
-  const hipStream_t st = (hipStream_t)stream;
-#define RPK_LAUNCH(S_)                                                                                    \
-  do {                                                                                                    \
-    if (s.node_format == rpl::NODES_W8)                                                                   \
-      hipLaunchKernelGGL((primary_kernel<S_, rpl::NODES_W8>), dim3(grid), dim3(BLOCK), lds, st, a);       \
-    else if (s.node_format == rpl::NODES_Q8)                                                              \
-      hipLaunchKernelGGL((primary_kernel<S_, rpl::NODES_Q8>), dim3(grid), dim3(BLOCK), lds, st, a);       \
-    else                                                                                                  \
-      hipLaunchKernelGGL((primary_kernel<S_, rpl::NODES_F32>), dim3(grid), dim3(BLOCK), lds, st, a);      \
-  } while (0)
-  if (spill) RPK_LAUNCH(true);
-  else RPK_LAUNCH(false);
-#undef RPK_LAUNCH
-  return (int)hipGetLastError();
 }
 
 template <uint32_t NF>

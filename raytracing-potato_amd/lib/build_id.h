@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "8bb994a1752f1509"
+#define RP_BUILD_ID "ae375ea43caf0676"

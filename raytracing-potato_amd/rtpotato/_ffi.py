@@ -27,18 +27,16 @@ RP_COUNTERS_LEN = 4  # device counter block: rays, samples, pixels, status (incl
 RP_SAMPLES_PER_STREAM = 32
 RP_COMM_ID_BYTES = 128
 RP_BUILDER_AUTO, RP_BUILDER_HOST, RP_BUILDER_DEVICE, RP_BUILDER_PLOC = 0, 1, 2, 3
-RP_ENGINE_MEGAKERNEL, RP_ENGINE_WAVEFRONT = 0, 1
 RP_NODES_AUTO, RP_NODES_F32, RP_NODES_Q8, RP_NODES_W8 = 0, 1, 2, 3
 RP_TILES_AUTO, RP_TILES_PLAIN, RP_TILES_COST, RP_TILES_MORTON, RP_TILES_PROBE = 0, 1, 2, 3, 4
 RP_QUEUES_AUTO, RP_QUEUES_SINGLE, RP_QUEUES_XCD_TILES, RP_QUEUES_XCD_REGIONS = 0, 1, 2, 3
 RP_COLLAPSE_AUTO, RP_COLLAPSE_GREEDY, RP_COLLAPSE_SAH = 0, 1, 2
 RP_LAYOUT_AUTO, RP_LAYOUT_DFS, RP_LAYOUT_DFS_LINE = 0, 1, 2
-RP_PRIMARY_AUTO, RP_PRIMARY_OFF, RP_PRIMARY_ON = 0, 1, 2
 RP_UNITS_AUTO, RP_UNITS_TILES, RP_UNITS_LEARNED = 0, 1, 2
-RP_FRAME_PRIMARY_PASS, RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED, RP_FRAME_UNIT_ORDER = 1, 2, 4, 8
+RP_FRAME_LEARNED_ORDER, RP_FRAME_PROBED, RP_FRAME_UNIT_ORDER = 2, 4, 8
 RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
-RP_ABI_VERSION = 8
+RP_ABI_VERSION = 9
 RP_MAX_FRAMES = 64
 RP_FRAME_ORDER_AUTO, RP_FRAME_ORDER_SEQUENTIAL, RP_FRAME_ORDER_INTERLEAVED = 0, 1, 2
 
@@ -98,9 +96,9 @@ class rp_scene_options(Structure):
     _fields_ = [("builder", c_uint32), ("max_leaf", c_uint32), ("cost_traverse", c_double),
                 ("always_max", ctypes.c_int32), ("lds_depth", c_uint32), ("self_check", c_uint32),
                 ("trav_threshold", c_uint32), ("tile_order", c_uint32), ("probe_n", c_uint32),
-                ("engine", c_uint32), ("wf_slots", c_uint32), ("node_format", c_uint32), ("leaf_break", c_uint32),
+                ("node_format", c_uint32), ("leaf_break", c_uint32),
                 ("unit_queues", c_uint32), ("queue_chunk", c_uint32), ("debug_stack_depth", c_uint32),
-                ("collapse", c_uint32), ("node_layout", c_uint32), ("primary", c_uint32), ("unit_order", c_uint32)]
+                ("collapse", c_uint32), ("node_layout", c_uint32), ("unit_order", c_uint32)]
 
 
 class rp_stats(Structure):
@@ -137,7 +135,8 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_comm_info", "rp_frame_gather", "rp_gather_stride", "rp_frame_assemble", "rp_render_gather", "rp_multi_create", "rp_multi_destroy",
               "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
               "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times",
-              "rp_workspace_frame_info", "rp_workspace_reserve_frames", "rp_render_frames_device_ws", "rp_frames_gather"]
+              "rp_workspace_frame_info", "rp_workspace_reserve_frames", "rp_render_frames_device_ws", "rp_frames_gather",
+              "rp_workspace_unit_order"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_selfcheck_ex", "rph_bvh_traversal_stats_ex", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64", "rph_make_div32"]
@@ -214,6 +213,7 @@ def rp() -> ctypes.CDLL:
     lib.rp_scene_build_times.argtypes = [c_void_p, c_void_p, c_uint32]
     lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_workspace_frame_info.argtypes = [c_void_p, c_void_p, POINTER(c_uint32)]
+    lib.rp_workspace_unit_order.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]
     lib.rp_workspace_reserve_frames.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32]
     lib.rp_frames_gather.argtypes = [c_void_p, c_void_p, c_void_p, POINTER(rp_render_params), c_uint32, c_void_p, c_void_p,
                                      c_void_p, c_void_p]

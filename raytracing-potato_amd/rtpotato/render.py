@@ -16,19 +16,17 @@ from .scene import RenderParams, Scene, shard_slot_count
 def scene_options(**kw) -> F.rp_scene_options:
     """rp_scene_options with the library defaults (rp_scene_options_init), fields overridden by keyword:
     builder ("auto" | "host" | "gpu" (LBVH) | "ploc" or RP_BUILDER_*), max_leaf, cost_traverse, always_max, lds_depth,
-    self_check, trav_threshold, tile_order, probe_n, engine ("megakernel" | "wavefront"), wf_slots,
+    self_check, trav_threshold, tile_order, probe_n,
     node_format ("auto" | "f32" | "q8" | "w8" or RP_NODES_*), tile_order ("auto" | "plain" | "cost" | "morton" | "probe"), leaf_break,
     unit_queues ("auto" | "single" | "xcd_tiles" | "xcd_regions" or RP_QUEUES_*), collapse ("auto" | "greedy" | "sah" or
-    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), primary ("auto" | "off" | "on" or RP_PRIMARY_*),
-    unit_order ("auto" | "tiles" | "learned" or RP_UNITS_*)."""
+    RP_COLLAPSE_*), node_layout ("auto" | "dfs" | "dfs_line" or RP_LAYOUT_*), unit_order ("auto" | "tiles" | "learned" or
+    RP_UNITS_*)."""
     o = F.rp_scene_options()
     F.check(F.rp().rp_scene_options_init(ctypes.byref(o)))
     for k, v in kw.items():
         if k == "builder" and isinstance(v, str):
             v = {"auto": F.RP_BUILDER_AUTO, "host": F.RP_BUILDER_HOST, "gpu": F.RP_BUILDER_DEVICE,
                  "ploc": F.RP_BUILDER_PLOC}[v]
-        if k == "engine" and isinstance(v, str):
-            v = {"megakernel": F.RP_ENGINE_MEGAKERNEL, "wavefront": F.RP_ENGINE_WAVEFRONT}[v]
         if k == "tile_order" and isinstance(v, str):
             v = {"auto": F.RP_TILES_AUTO, "plain": F.RP_TILES_PLAIN, "cost": F.RP_TILES_COST,
                  "morton": F.RP_TILES_MORTON, "probe": F.RP_TILES_PROBE}[v]
@@ -43,8 +41,6 @@ def scene_options(**kw) -> F.rp_scene_options:
             v = {"auto": F.RP_LAYOUT_AUTO, "dfs": F.RP_LAYOUT_DFS, "dfs_line": F.RP_LAYOUT_DFS_LINE}[v]
         if k == "unit_order" and isinstance(v, str):
             v = {"auto": F.RP_UNITS_AUTO, "tiles": F.RP_UNITS_TILES, "learned": F.RP_UNITS_LEARNED}[v]
-        if k == "primary" and isinstance(v, str):
-            v = {"auto": F.RP_PRIMARY_AUTO, "off": F.RP_PRIMARY_OFF, "on": F.RP_PRIMARY_ON}[v]
         if not hasattr(o, k):
             raise KeyError(f"unknown scene option {k!r}")
         setattr(o, k, v)
@@ -143,6 +139,15 @@ class DeviceScene:
         f = ctypes.c_uint32()
         F.check(F.rp().rp_workspace_frame_info(self.handle, workspace.handle if workspace else None, ctypes.byref(f)))
         return f.value
+
+    def unit_order(self, n: int, workspace: "Workspace | None" = None) -> tuple:
+        """rp_workspace_unit_order: (durations, order) of the last render's n units (uint32 arrays; order valid when
+        frame_info has RP_FRAME_UNIT_ORDER)."""
+        dur = np.zeros(n, dtype=np.uint32)
+        order = np.zeros(n, dtype=np.uint32)
+        F.check(F.rp().rp_workspace_unit_order(self.handle, workspace.handle if workspace else None, dur.ctypes.data,
+                                               order.ctypes.data, n))
+        return dur, order
 
     def set_tile_costs(self, params: RenderParams, costs: np.ndarray, ranks: int,
                        workspace: "Workspace | None" = None) -> None:

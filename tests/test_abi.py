@@ -42,7 +42,7 @@ def test_librp_host_exports_all_rp_host_h_symbols():
 def test_librp_loads_and_reports_without_gpu():
     from rtpotato import _ffi as F
     L = F.rp()
-    assert L.rp_abi_version() == F.RP_ABI_VERSION == 8
+    assert L.rp_abi_version() == F.RP_ABI_VERSION == 9
     n = ctypes.c_int(-1)
     rc = L.rp_device_count(ctypes.byref(n))
     assert rc in (F.RP_OK, F.RP_ENODEV) and n.value >= 0
@@ -139,7 +139,7 @@ def test_product_kernel_has_no_experiment_switches():
     no #if on an experiment macro, and the switches of earlier rounds are refused by #error."""
     import subprocess
     allowed = {"RPK_DIAG", "RPK_DIAG_NOSTAMP", "RPK_DIAG_BIN_TICKS"}
-    for f in ("rp_device.h", "rp_kernel.hip", "rp_kernel.h", "rp_wavefront.hip", "rp_layout.h"):
+    for f in ("rp_device.h", "rp_kernel.hip", "rp_kernel.h", "rp_layout.h"):
         src = open(os.path.join(PKG, "csrc", f)).read()
         conds = re.findall(r"^\s*#\s*(?:if|ifdef|ifndef|elif)\b(.*)$", src, flags=re.M)
         used = set()
@@ -258,3 +258,39 @@ def test_bench_frames_per_launch_cap():
     c5 = 128 * 128 * 1024
     assert b.frames_per_launch_cap(16, c5, 8) == 15 and b.frames_per_launch_cap(16, c5, 8) * c5 * 8 < 1 << 31
     assert b.frames_per_launch_cap(1, 0, 0) == 1 and b.frames_per_launch_cap(8, 1 << 31, 1) == 1
+    # the library's per-XCD queue bound, 2 n + lanes < 2^32 - 1, is the binding one (it is below 2^31)
+    for slots, batches in ((c3, 1), (c3, 8), (c5, 8), (1 << 20, 3), ((1 << 31) // 2 - 1000, 1)):
+        for lanes in (262_144, b.LANES_MAX):
+            L = b.frames_per_launch_cap(64, slots, batches, lanes)
+            n = slots * batches * L
+            assert L == 1 or (n < 1 << 31 and 2 * n + lanes < 0xFFFFFFFF), (slots, batches, lanes, L)
+            assert L == 64 or 2 * (n + slots * batches) + lanes >= 0xFFFFFFFF - 1 or (n + slots * batches) >= 1 << 31
+
+
+def test_bench_frame_sequence_seeds():
+    """bench.py's launches take consecutive frames of one sequence, so the warm-up's frames and the timed
+    frames (and the single-frame and side-leg frames after them) have disjoint seeds -- for every per-pixel stream, since
+    frame f's stream of (pixel, batch) is seed + f B W H + b W H + j W + i."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    W, H, seed = 1920, 1080, 1592590337
+    for nb, warm, steps, L in ((1, 5, 20, 32), (8, 5, 20, 32), (8, 8, 16, 8), (1, 3, 7, 1)):
+        seq = b.FrameSeq()
+        phases = []
+        for sizes in (b.launch_sizes(warm, L), b.launch_sizes(steps, L), [1, 1, 1]):
+            streams = set()
+            for n in sizes:
+                f0, s0 = seq.launch(seed, nb, W, H, n)
+                assert s0 == b.frame_seed(seed, nb, W, H, f0)
+                for f in range(n):  # frame f of the launch: s0 + f B W H (rp_render_frames_device_ws)
+                    fs = (s0 + f * nb * W * H) & b.U64
+                    streams.add(fs)
+            phases.append(streams)
+        assert len(phases[0]) == warm and len(phases[1]) == steps
+        assert not (phases[0] & phases[1]) and not (phases[1] & phases[2]) and not (phases[0] & phases[2])
+        # a frame's per-pixel streams occupy [fs, fs + B W H): consecutive frames never share one
+        allf = sorted(phases[0] | phases[1] | phases[2])
+        assert all(y - x >= nb * W * H for x, y in zip(allf, allf[1:]))
+    assert b.frame_seed(b.U64, 1, 1, 1, 1) == 0  # u64 wrap, like rp_render_params.seed

@@ -318,35 +318,3 @@ def test_frame_assemble_multi_rank_layout(gpu, world):
     assert np.array_equal(frame8.cpu().numpy().reshape(p.height, p.width, 4), rgba[..., [2, 1, 0, 3]])
 
 
-@pytest.mark.parametrize("name,arg,spp,opts", [
-    ("bunny_full", None, 40, {}), ("three_balls", None, 3, {}), ("variants", None, 6, {}),
-    ("variants_sky", None, 5, {}), ("more_balls_optimized", None, 4, {}), ("glass_bunny", None, 4, {}),
-    ("random_mesh", 200_000, 4, {"lds_depth": 17}), ("bunny_full", None, 9, {"wf_slots": 1}),
-    ("random_mesh", 200_000, 4, {"node_format": "w8"})])
-def test_wavefront_engine_matches_megakernel(gpu, name, arg, spp, opts):
-    """The stage-split engine (rp_scene_options.engine = wavefront: trace / shade passes over a path-slot pool)
-    renders the megakernel's image bit for bit -- same paths, same RNG stream, same accumulation order --
-    with the same ray, sample and pixel counts, and matches the oracle."""
-    from rtpotato import scenes
-    from rtpotato.scene import RenderParams
-    sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 56, 36)
-    p = RenderParams(56, 36, spp, 8, scenes.DEFAULT_SEED, 16, 16)
-    ref, ref_fg, st = gpu.render(sc, p, foreground=True, options=dict(opts))
-    rgb, fg, stw = gpu.render(sc, p, foreground=True, options=dict(opts, engine="wavefront"))
-    assert np.array_equal(rgb, ref) and np.array_equal(fg, ref_fg)
-    assert (stw["rays"], stw["samples"], stw["pixels"]) == (st["rays"], st["samples"], st["pixels"])
-    if name == "variants":
-        orc, _, ctr = oracle_render(sc, p, threads=16)
-        assert_parity(compare(rgb, orc))
-        assert ctr["rays"] == stw["rays"]
-
-
-def test_wavefront_engine_c3_shard(gpu):
-    """The stage-split engine on config C3's scene at full size, shard 3 of 16 (1/16 of the frame, 256 spp):
-    bitwise the megakernel's shard."""
-    from rtpotato import scenes
-    scene, params = scenes.config_scene("C3")
-    p = replace(params, shard=3, num_shards=16)
-    ref, _, st = gpu.render(scene, p)
-    rgb, _, stw = gpu.render(scene, p, options={"engine": "wavefront"})
-    assert np.array_equal(rgb, ref) and stw["rays"] == st["rays"]

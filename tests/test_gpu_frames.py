@@ -152,20 +152,49 @@ def test_frames_spp0_and_errors(gpu):
         ds.reserve(q)  # one frame's batch sums: two frames do not fit
         with pytest.raises(F.RPError, match="rp_workspace_reserve_frames"):
             ds.render_frames_device(q, 2, out, ctr)
-    with gpu.DeviceScene(sc, options={"engine": "wavefront"}) as ds:
+
+
+def test_frame_info_flags(gpu):
+    """rp_workspace_frame_info: a workspace's first frame probes its tile costs (RP_FRAME_PROBED), the next frame of the
+    same geometry schedules from the learned table (RP_FRAME_LEARNED_ORDER) without a probe, and a render that launches
+    nothing -- spp = 0, a refused call -- reports no scheduling at all (the flags are reset before any
+    return)."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.scene import shard_slot_count
+    sc, p = _scene("bunny_full", 64, 48, 4)
+    p = replace(p, tile_w=16, tile_h=16)
+    n = shard_slot_count(p)
+    dev = torch.device("cuda", 0)
+    out = torch.zeros(3 * n, dtype=torch.float64, device=dev)
+    ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+    with gpu.DeviceScene(sc) as ds:
+        w = ds.workspace()
+        ds.render_device(p, out, ctr, workspace=w)
+        assert ds.frame_info(w) == F.RP_FRAME_PROBED
+        ds.render_device(p, out, ctr, workspace=w)
+        assert ds.frame_info(w) == F.RP_FRAME_LEARNED_ORDER
+        ds.render_device(replace(p, spp=0), out, ctr, workspace=w)
+        assert ds.frame_info(w) == 0
+        ds.render_device(p, out, ctr, workspace=w)
+        assert ds.frame_info(w) == F.RP_FRAME_LEARNED_ORDER
         with pytest.raises(F.RPError):
-            ds.render_frames_device(replace(p, spp=2), 2, out, ctr)
+            ds.render_device(replace(p, max_bounce=0), out, ctr, workspace=w)
+        assert ds.frame_info(w) == 0
+        torch.cuda.synchronize()
+        w.close()
 
 
-@pytest.mark.parametrize("shard", [None, 3])
-def test_frames_c3_full_size(gpu, shard):
-    """bench.py's workload at full size: C3 (1920x1080x256, 32-sample streams) rendered 8 frames to a launch in the
-    interleaved order with the default queue chunks -- each of the launch's frames equals its lone render (seed + f B W H)
-    bit for bit, with the summed counts; also shard 3 of an 8-way balanced deal (the N = 8 per-rank work) under an
-    installed cost table (as every rank holds one after its first gathered frame).  The lone renders are themselves
-    oracle-checked at this size (test_gpu_configs.py)."""
+@pytest.mark.parametrize("shard,sps", [(None, 256), (None, 0), (3, 0)])
+def test_frames_c3_full_size(gpu, shard, sps):
+    """bench.py's workloads at full size: C3 (1920x1080x256) rendered 8 frames to a launch in the interleaved order with
+    the default queue chunks, under SURVEY.md 8c's one stream per pixel (the N = 1 headline) and in 32-sample streams --
+    each of the launch's frames equals its lone render (seed + f B W H) bit for bit, with the summed counts; also shard 3
+    of an 8-way balanced deal (the N = 8 per-rank work) under an installed cost table (as every rank holds one after its
+    first gathered frame).  The lone renders are themselves oracle-checked at this size (test_gpu_configs.py)."""
     from rtpotato import scenes
     scene, params = scenes.config_scene("C3")
+    params = replace(params, samples_per_stream=sps)
     table = None
     if shard is not None:
         n_tiles = -(-params.width // params.tile_w) * -(-params.height // params.tile_h)

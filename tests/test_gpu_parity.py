@@ -372,12 +372,12 @@ def test_host_tree_collapse(gpu, collapse, fmt):
 @pytest.mark.parametrize("name,arg", [("bunny_full", None), ("random_mesh", 200_000)])
 def test_spilled_traversal_stack(gpu, name, arg, fmt):
     """Traversal stack entries beyond the LDS part spill to the per-lane global run (the SPILL kernel that
-    deep trees such as C5's use): forced here with options.lds_depth = 17, so nearly every traversal spills
-    -- same image as the oracle."""
+    deep trees such as C5's use): forced here with options.lds_depth = 8 entries (the minimum), so deep traversals
+    spill -- same image as the oracle."""
     from rtpotato import scenes
     from rtpotato.scene import RenderParams
     sc = scenes.configure(scenes.CATALOGUE[name](arg) if arg else scenes.CATALOGUE[name](), 64, 40)
-    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 17, "node_format": fmt})
+    _check(gpu, sc, RenderParams(64, 40, 6, 8, scenes.DEFAULT_SEED), options={"lds_depth": 8, "node_format": fmt})
 
 
 @pytest.mark.parametrize("fmt", ["f32", "q8"])

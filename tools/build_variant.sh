@@ -27,6 +27,6 @@ mkdir -p "$TMP/include" && cp "$HERE"/../include/*.h "$TMP/include/"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -mllvm -disable-machine-licm \
   "$@" -c "$TMP/rp_kernel.hip" -o "$HERE/lib/k_$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$HERE/lib/librp_$NAME.so" "$HERE/lib/k_$NAME.o" \
-  "$HERE/lib/rp_wavefront.o" "$HERE/lib/rp_api.o" "$HERE/lib/rp_bvh_hip.o" "$HERE/lib/rp_bvh_gpu.o" "$HERE/lib/rp_sched.o" \
+  "$HERE/lib/rp_api.o" "$HERE/lib/rp_bvh_hip.o" "$HERE/lib/rp_bvh_gpu.o" "$HERE/lib/rp_sched.o" \
   "$HERE/lib/rp_id.o" -lrccl
 rm -f "$HERE/lib/k_$NAME.o"

@@ -75,8 +75,32 @@ def main():
                "lane_util": round(d[17 + 2 * i] / max(1, 64 * d[16 + 2 * i]), 3)}
         for i, name in enumerate(regions)}
     cyc = ["surface", "sph_uv", "tex_issue", "scatter", "tex_value", "emit_accum", "start_sample", "end_sample",
-           "newray_always", "refill", "next_bounce"]
+           "newray_always", "refill", "next_bounce", "node_loop", "prim_loop"]
     out["cycle_share"] = {name: round(d[320 + i] / tot, 4) for i, name in enumerate(cyc)}
+    # Loss budget: per cycle region, the share of all wave-cycles its idle lanes cost, cycle share x
+    # (1 - lane utilisation of the region's DREG counter).  Scatter pools the per-material regions and their rejection
+    # loops (lanes summed over execs); emission/accumulation takes the shade region's utilisation.
+    reg = {name: (d[16 + 2 * i], d[17 + 2 * i]) for i, name in enumerate(regions)}
+    def util(*names):
+        e = sum(reg[n][0] for n in names)
+        return reg_l / (64 * e) if (e and (reg_l := sum(reg[n][1] for n in names))) else None
+    umap = {"node_loop": ("node",), "prim_loop": ("prim",), "surface": ("surface",), "sph_uv": ("sph_uv",),
+            "tex_issue": ("texture",), "tex_value": ("texture",),
+            "scatter": ("lambert", "metal", "dielectric", "loop_lambert", "loop_metal"), "emit_accum": ("shade",),
+            "start_sample": ("start_sample",), "end_sample": ("end_sample",), "refill": ("refill",)}
+    lb = {}
+    for name, names in umap.items():
+        u = util(*names)
+        share = d[320 + cyc.index(name)] / tot
+        lb[name] = {"cycle_share": round(share, 4), "lane_util": round(u, 3) if u is not None else None,
+                    "idle_share": round(share * (1 - u), 4) if u is not None else None}
+    named = sum(d[320 + i] for i in range(len(cyc))) / tot
+    out["loss_budget"] = {"regions": dict(sorted(lb.items(), key=lambda kv: -(kv[1]["idle_share"] or 0))),
+                          "idle_share_total": round(sum(v["idle_share"] or 0 for v in lb.values()), 4),
+                          "named_cycle_share": round(named, 4),
+                          "note": "share of all wave-cycles spent in each region x (1 - its lane utilisation): the "
+                                  "issue slots idle lanes cost; the rest of the wave-cycles (1 - named_cycle_share) is "
+                                  "the round's control (ballots, ray setup, queue fetch)"}
     # timeline histograms (10 ms bins from each block's start): lanes retiring, pixels fetched and their rays
     last = max([b for b in range(64) if d[64 + b] or d[192 + b]] or [0])
     out["timeline_10ms"] = [{"t_ms": 10 * b, "retired_lanes": d[64 + b], "pixels": d[192 + b],
@@ -86,18 +110,6 @@ def main():
     out["unit_durations"] = [{"ms_from": round(2 ** (10 + b) / 1e5, 3), "ms_to": round(2 ** (11 + b) / 1e5, 3),
                               "units": d[352 + b], "rays_per_unit": round(d[376 + b] / max(1, d[352 + b]), 1)}
                              for b in range(24) if d[352 + b]]
-    pd = d[400:409]  # rp_kernel.h DIAG_PRIM: the coherent primary pass
-    if pd[0]:
-        cyc = pd[5] + pd[6] + pd[7]
-        out["primary_pass"] = {
-            "items": pd[0], "rays": pd[1], "visits_per_ray": round(pd[2] / max(1, pd[1]), 3),
-            "prim_tests_per_ray": round(pd[3] / max(1, pd[1]), 3),
-            "trav_steps_per_item": round(pd[4] / pd[0], 2),
-            "max_lane_visits_per_item": round(pd[8] / pd[0], 2),
-            "visit_lane_util": round(pd[2] / max(1, 64 * pd[8]), 4),
-            "wave_cycles_per_item": round(cyc / pd[0], 1),
-            "cycle_share": {"setup": round(pd[5] / cyc, 4), "traverse": round(pd[6] / cyc, 4),
-                            "fetch_store": round(pd[7] / cyc, 4)}}
     print(json.dumps(out, indent=1))
 
 

@@ -16,10 +16,9 @@
 #   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ diag if present)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
-#   coherence_<CFG>    tools/primary_coherence.py under rocprofv3 --kernel-trace: camera-ray traversal rate by ray order
 #   pmcx_<CFG>         one --pmc pass of the counters in PMCX (output name PMCX_NAME)
 #   ab[_<CFG>]         interleaved A/B timing: RUNS (or RUNS_<CFG>) = "name:lib:opts ..." (lib = suffix of lib/librp_<lib>.so or main,
-#                      opts = bench.py --opt field=value,... or --flag=value), REPS rounds, config CFG, STEPS_AB frames each
+#                      opts = bench.py --opt field=value,... or --flag=value or --flag), REPS rounds, config CFG, STEPS_AB frames each
 #   abpmc[_<CFG>]      per run of RUNS one FETCH_SIZE and one WRITE_SIZE pass over one CFG frame (traffic A/B)
 # Outputs: gpurun_out/${TAG}_*; gpurun_out/${TAG}_manifest.txt lists every output file with the command that made it.
 set -o pipefail
@@ -142,7 +141,7 @@ for s in ${STEPS:-tests}; do
           name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}; opts=${rest#*:}
           args=""
           for o in $(echo $opts | tr ',' ' '); do  # field=value: --opt; --flag=value: a bench.py flag
-            if [[ $o == --* ]]; then args="$args ${o%%=*} ${o#*=}"; else args="$args --opt $o"; fi
+            if [[ $o == --*=* ]]; then args="$args ${o%%=*} ${o#*=}"; elif [[ $o == --* ]]; then args="$args $o"; else args="$args --opt $o"; fi
           done
           out=gpurun_out/${TAG}_${CFG}_${name}_$rep.json
           step "ab $rep $name"
@@ -158,14 +157,6 @@ for s in ${STEPS:-tests}; do
         name=${run%%:*}; rest=${run#*:}; lib=${rest%%:*}
         pmc $(libpath $lib) $CFG ${name}_fetch FETCH_SIZE && pmc $(libpath $lib) $CFG ${name}_write WRITE_SIZE || exit 1
       done ;;
-    coherence_*)  # tools/primary_coherence.py under a kernel trace: camera rays coherent / 8x8 pixels / shuffled
-      cfg=${s#coherence_}
-      out=gpurun_out/${TAG}_${cfg}_coherence
-      step "coherence $cfg"
-      made $out.json "rocprofv3 --kernel-trace -- python3 tools/primary_coherence.py --config $cfg ${COH_ARGS:-}"
-      timeout -k 10 600 rocprofv3 --kernel-trace -d $out -o run --output-format csv -- \
-        python3 tools/primary_coherence.py --config $cfg --meta $out.meta.json ${COH_ARGS:-} > $out.log 2>&1 &&
-      python3 tools/primary_coherence.py --trace $out --meta $out.meta.json > $out.json 2>> $out.log || exit 1 ;;
     ldswait_*)  # tools/gather_lds_wait.py: a kernel of RCCL's all-gather footprint behind frames in flight (LDSW_ARGS)
       cfg=${s#ldswait_}
       out=gpurun_out/${TAG}_${cfg}_ldswait${LDSW_LABEL:+_$LDSW_LABEL}
