@@ -475,6 +475,19 @@ int rp_frame_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, con
 int rp_frames_gather(rp_comm* comm, rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                      uint32_t n_frames, const double* d_shard_rgb, uint8_t* d_frames_bgra, uint64_t* d_counters,
                      void* stream);
+/* rp_frames_gather in two halves around a collective of the caller's own (ABI v9; MPI, a torch.distributed
+ * all-gather, tests): rp_frames_block_words gives the words (uint32) of one rank's packed block for n_frames frames of
+ * params' shape -- the counter block and plan hash, the measured tile costs, then frame f's to_srgb_u8 bytes at a fixed
+ * offset per frame; rp_frames_pack writes this rank's block (params.shard of params.num_shards) into d_send; the caller
+ * all-gathers the num_shards blocks rank by rank into d_recv (rank r's block at r * words); rp_frames_unpack then does
+ * what rp_frames_gather does after its collective: counters reduced into d_counters (sums, status OR-ed, plan hashes
+ * compared), the gathered tile costs learned, and the n_frames frames assembled into d_frames_bgra.  Same workspace
+ * reservation and rules as rp_frames_gather; asynchronous on `stream`. */
+int rp_frames_block_words(const rp_render_params* params, uint32_t n_frames, uint64_t* words);
+int rp_frames_pack(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params, uint32_t n_frames,
+                   const double* d_shard_rgb, const uint64_t* d_counters, uint32_t* d_send, void* stream);
+int rp_frames_unpack(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params, uint32_t n_frames,
+                     const uint32_t* d_recv, uint8_t* d_frames_bgra, uint64_t* d_counters, void* stream);
 /* The frame assembly step alone, for callers that move the shards with their own collective (MPI, a
  * torch.distributed all-gather): d_gathered holds params->num_shards shard buffers of `stride` slots each
  * (rp_gather_stride: the largest shard, shard 0), rank r's at slot r * stride, `words_per_slot` 32-bit words

@@ -1536,6 +1536,51 @@ int rp_frames_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_render_p
   return gather_assemble(s, w, gp, d_frames_bgra, nullptr, d_counters, st);
 }
 
+int rp_frames_block_words(const rp_render_params* p, uint32_t n_frames, uint64_t* words) {
+  if (!words) return fail(RP_EINVAL, "words is NULL");
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
+  Tiling t;
+  int rc = make_tiling(p, t);
+  if (rc) return rc;
+  *words = pack_words(t, true, n_frames);
+  return RP_OK;
+}
+
+// rp_frames_gather's stage (1) and its stages (3a, 3) around the caller's collective: the workspace's own send / receive
+// buffers are the ones rp_frames_gather uses, copied from / to the caller's.
+int rp_frames_pack(rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t n_frames, const double* d_shard_rgb,
+                   const uint64_t* d_counters, uint32_t* d_send, void* stream) {
+  if (!s || !d_shard_rgb || !d_send || !p) return fail(RP_EINVAL, "scene, params, shards and send buffer must be non-NULL");
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
+  if (!w) w = &s->ws0;
+  GatherPlan gp;
+  int rc = gather_plan(s, w, p->num_shards ? (int)p->num_shards : 1, (int)p->shard, p, gp, n_frames);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  DeviceGuard g(s->device);
+  if ((rc = gather_stage(s, w, gp, d_shard_rgb, true, false, d_counters, st))) return rc;
+  RP_HIP(hipMemcpyAsync(d_send, w->d_pack_send, sizeof(uint32_t) * pack_words(gp.t, true, n_frames),
+                        hipMemcpyDeviceToDevice, st));
+  return RP_OK;
+}
+
+int rp_frames_unpack(rp_scene* s, rp_workspace* w, const rp_render_params* p, uint32_t n_frames, const uint32_t* d_recv,
+                     uint8_t* d_frames_bgra, uint64_t* d_counters, void* stream) {
+  if (!s || !d_recv || !d_frames_bgra || !p) return fail(RP_EINVAL, "scene, params and buffers must be non-NULL");
+  if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
+  if (reinterpret_cast<uintptr_t>(d_frames_bgra) % 4 != 0) return fail(RP_EINVAL, "d_frames_bgra must be 4-byte aligned");
+  if (!w) w = &s->ws0;
+  GatherPlan gp;
+  int rc = gather_plan(s, w, p->num_shards ? (int)p->num_shards : 1, (int)p->shard, p, gp, n_frames);
+  if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  DeviceGuard g(s->device);
+  RP_HIP(hipMemcpyAsync(w->d_pack_recv, d_recv, sizeof(uint32_t) * pack_words(gp.t, true, n_frames) * gp.geom.nranks,
+                        hipMemcpyDeviceToDevice, st));
+  if ((rc = gather_learn(s, w, gp, p, true, st))) return rc;
+  return gather_assemble(s, w, gp, d_frames_bgra, nullptr, d_counters, st);
+}
+
 int rp_render_gather(rp_comm* c, rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_render_params* p,
                      uint8_t* d_frame_bgra, double* d_frame_rgb, uint64_t* d_counters, void* stream) {
   if (!c || !s) return fail(RP_EINVAL, "comm and scene must be non-NULL");

@@ -136,7 +136,7 @@ RP_SYMBOLS = ["rp_abi_version", "rp_last_error", "rp_device_count", "rp_scene_cr
               "rp_render_multi", "rp_shard_unpack_map", "rp_workspace_tile_map", "rp_frame_assemble_ws", "rp_build_id",
               "rp_workspace_tile_costs", "rp_workspace_set_tile_costs", "rp_scene_build_times",
               "rp_workspace_frame_info", "rp_workspace_reserve_frames", "rp_render_frames_device_ws", "rp_frames_gather",
-              "rp_workspace_unit_order"]
+              "rp_workspace_unit_order", "rp_frames_block_words", "rp_frames_pack", "rp_frames_unpack"]
 HOST_SYMBOLS = ["rph_obj_load", "rph_mesh_free", "rph_tga_load", "rph_tga_save", "rph_free", "rph_to_srgb_u8",
                 "rph_lookat", "rph_sky_panorama", "rph_bvh_selfcheck", "rph_bvh_traversal_stats", "rph_bvh_selfcheck_ex", "rph_bvh_traversal_stats_ex", "rph_bvh_tree_hash", "rph_last_error",
                 "rph_stdrng_u64", "rph_make_div32"]
@@ -214,6 +214,11 @@ def rp() -> ctypes.CDLL:
     lib.rp_workspace_tile_costs.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_void_p, c_uint32]
     lib.rp_workspace_frame_info.argtypes = [c_void_p, c_void_p, POINTER(c_uint32)]
     lib.rp_workspace_unit_order.argtypes = [c_void_p, c_void_p, c_void_p, c_void_p, c_uint64]
+    lib.rp_frames_block_words.argtypes = [POINTER(rp_render_params), c_uint32, POINTER(c_uint64)]
+    lib.rp_frames_pack.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]
+    lib.rp_frames_unpack.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]
     lib.rp_workspace_reserve_frames.argtypes = [c_void_p, c_void_p, POINTER(rp_render_params), c_uint32]
     lib.rp_frames_gather.argtypes = [c_void_p, c_void_p, c_void_p, POINTER(rp_render_params), c_uint32, c_void_p, c_void_p,
                                      c_void_p, c_void_p]

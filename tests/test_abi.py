@@ -165,11 +165,16 @@ def test_profile_records_are_of_this_build():
     from rtpotato import _ffi as F
     build = F.rp().rp_build_id().decode()
     cur = json.load(open(os.path.join(REPO, "profiles", "current.json")))["roofline"]
-    assert set(cur) >= {"C3", "C5"}
-    for cfg, rel in cur.items():
+    # keys "<config>" or "<config>@<samples_per_stream>" (bench.py kernel_record): the N = 1 headline's C3 record under
+    # the one-stream contract, the 32-sample streams N > 1 runs use, and C5
+    assert "C3" in cur and "C3@32" in cur and any(k.split("@")[0] == "C5" for k in cur)
+    for key, rel in cur.items():
         rec = json.load(open(os.path.join(REPO, rel)))
-        assert rec["build_id"] == build, (cfg, rel, rec["build_id"], build)
+        cfg, _, sps = key.partition("@")
+        assert rec["build_id"] == build, (key, rel, rec["build_id"], build)
         assert rec["config"] == cfg and rec["rays"] > 0 and rec["traffic_bytes_per_ray"] > 0
+        assert not sps or rec["samples_per_stream"] == int(sps), (key, rec.get("samples_per_stream"))
+    assert json.load(open(os.path.join(REPO, cur["C3"])))["samples_per_stream"] == 256
 
 
 def test_build_id_is_path_independent(tmp_path):

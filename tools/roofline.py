@@ -75,7 +75,7 @@ def algorithmic(diag, node_bytes, bench):
     cfg = bench["config"]
     W, H, spp = cfg["width"], cfg["height"], cfg["spp"]
     rays = float(cfg["rays_per_frame"])
-    nbatch = -(-spp // 32)
+    nbatch = -(-spp // cfg.get("samples_per_stream", 32))
     out_bytes = (W * H * nbatch * 28 * (2 if nbatch > 1 else 0) + W * H * 24) / rays
     parts = {
         "nodes": diag["visits_per_ray"] * node_bytes,
@@ -126,6 +126,7 @@ def main():
     rev = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
     build = bench.get("roofline", {}).get("build_id")
     rec = {"kernel": KERNEL, "config": a.config, "git": rev or None, "build_id": build, "rays": rays,
+           "samples_per_stream": bench["config"].get("samples_per_stream", 32),
            "frames_per_launch": sizes, "counters": c,
            "kernel_ns_per_pass": durs, "bench_ms_per_step": bench.get("ms_per_step")}
     if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
