@@ -612,18 +612,16 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   s->ks.n_always = ps.n_always;
   s->ks.qbound = ps.qbound;
   s->ks.node_format = node_format;
-  // Stack sizes are in 32-bit words.  A 4-wide node pushes at most 3 entries (its non-nearest hits) per level below
-  // the root, +3 spare entries for the kernel's branchless push (rp_device.h STACK_SLACK); an entry is two words, the
-  // child and its t_near (rp_device.h trav_step).  Node8Q: groups of two words, per level at most the rest of a node
-  // group and one primitive group, +3 spare words.
-  const uint32_t epw = node_format == rpl::NODES_W8 ? 1u : 2u;  // words per stack entry
-  s->ks.stack_depth = epw * (3 * ps.max_depth + 4 + 3);
+  // a wide node pushes at most 3 entries (its non-nearest hits) per level below the root; +3 spare
+  // entries for the kernel's branchless push (rp_kernel.hip STACK_SLACK)
+  s->ks.stack_depth = 3 * ps.max_depth + 4 + 3;
+  // Node8Q: groups of two words, per level at most the rest of a node group and one primitive group
   if (node_format == rpl::NODES_W8) s->ks.stack_depth = 4 * (ps.max_depth + 1) + 3;
-  // floor of 17 entries: the spill split below never keeps fewer words in LDS than LDS_FLOOR
-  if (s->ks.stack_depth < epw * 17) s->ks.stack_depth = epw * 17;
+  // floor of 17 entries: the spill split below never keeps fewer in LDS (options.lds_depth tests force 17)
+  if (s->ks.stack_depth < 17) s->ks.stack_depth = 17;
   // test-only: a stack too small for the tree (the kernels flag RP_STATUS_STACK_OVERFLOW, never write past it)
   const bool debug_stack = opt.debug_stack_depth != 0;
-  if (debug_stack) s->ks.stack_depth = epw * opt.debug_stack_depth;
+  if (debug_stack) s->ks.stack_depth = opt.debug_stack_depth;
   s->n_nodes = n_tree_nodes;
   s->n_leaves = ps.n_leaves;
   s->n_prims = desc->n_hittables;
@@ -643,24 +641,23 @@ int scene_create(const rp_scene_desc* desc, int device, const rp_scene_options* 
   // lanes still traversing before the finished ones shade: C3 24 (16: +0.2 %, 32: +0.7 %), C5 32 (-1.6 %)
   if (s->opt.trav_threshold == 0) s->opt.trav_threshold = s->device_bytes > (256ull << 20) ? 32u : DEF_TRAV_THRESHOLD;
   // LDS holds the whole stack unless that costs resident blocks: then the deepest entries spill to a
-  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth (whole entries) that still
-  // fits the occupancy of a shallow stack (C3's 31 entries of two words: 9 in LDS for 4 blocks per SIMD).
-  // options.lds_depth forces a depth in entries (>= 8) for tests and tuning.
-  const uint32_t floor_w = node_format == rpl::NODES_W8 ? 17u : 16u;  // LDS words never fewer than this
+  // per-lane global run (rp_kernel.hip stk_put/stk_get) and LDS keeps the largest depth that still fits
+  // the occupancy of a shallow stack (C5's 43-entry stack: 3 -> 4 blocks per CU).  options.lds_depth
+  // forces a depth (>= 17) for tests and tuning.
   s->ks.lds_depth = s->ks.stack_depth;
   int bpc = 0;
   if (rpk::render_blocks_per_cu(s->ks.stack_depth, false, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   int bpc_spill = 0;
-  if (!debug_stack && rpk::render_blocks_per_cu(floor_w, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
+  if (!debug_stack && rpk::render_blocks_per_cu(17, true, node_format, &bpc_spill) == 0 && bpc_spill > bpc) {
     uint32_t L = s->ks.stack_depth - 1;
     int b = 0;
-    while (L > floor_w && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
-    s->ks.lds_depth = std::max(floor_w, L - L % epw);
+    while (L > 17 && (rpk::render_blocks_per_cu(L, true, node_format, &b) != 0 || b < bpc_spill)) L--;
+    s->ks.lds_depth = L;
     bpc = bpc_spill;
   }
-  if (!debug_stack && opt.lds_depth && epw * opt.lds_depth < s->ks.stack_depth) {
-    s->ks.lds_depth = epw * opt.lds_depth;
-    if (rpk::render_blocks_per_cu(s->ks.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
+  if (!debug_stack && opt.lds_depth && opt.lds_depth < s->ks.stack_depth) {
+    s->ks.lds_depth = opt.lds_depth;
+    if (rpk::render_blocks_per_cu(opt.lds_depth, true, node_format, &bpc) != 0 || bpc < 1) bpc = 1;
   }
   s->blocks_per_cu = bpc;
   phase[4] = lap();

@@ -596,7 +596,7 @@ struct TravState {
   uint32_t bestm;  // the closest hit's kind and material (HitRec::km)
   uint32_t cur, sp;
   uint32_t leaf;  // parked leaf entry (speculative traversal), 0 = none (entry 0 is an inner node)
-  uint32_t gy, py;  // Node8Q: the node group's rank word and the parked primitive group; 4-wide: gy = cur's t_near (f32 bits)
+  uint32_t gy, py;  // Node8Q only (0 otherwise)
 };
 static constexpr uint32_t W8_GROUP = 0x80000000u;  // cur: a node group (prim groups: first primitive < 2^31)
 
@@ -844,13 +844,6 @@ RPK_INLINE void trav_step_w8(const KScene& S, lds_u32* stk, uint32_t stride, uin
   ts.py = py;
 }
 
-// 4-wide step.  Stack entries carry their entry distance: entry i of a lane is the two words 2i (the child entry) and
-// 2i + 1 (its conservative t_near, f32 bits) of the lane's stack column, and TravState::gy holds the current entry's.
-// An entry is popped for nothing once a primitive closer than its box was accepted after it was pushed: `cull` drops
-// such entries without fetching the node (its box test `fma(tnear, 1 - 2^-19, -2^-100) <= best32` is the one that
-// pushed it, section 4.2 of DESIGN.md, with the closest hit found since; a box whose exact interval meets
-// [t_min, best] never fails it).  The CPU traversal model counted 20 % fewer node visits on C3 camera rays, 6 % on
-// interior rays, 4-6 % on C5.
 template <bool SPILL, uint32_t NF, bool COUNT = false>
 RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32_t spl, const Ray32& r, V3 o, V3 d,
                           double tmin, TravState& ts, bool& overflow, TravDiag* td = nullptr,
@@ -860,40 +853,12 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
     return;
   }
   uint32_t cur = ts.cur, sp = ts.sp, leaf = ts.leaf;
-  float ct = __uint_as_float(ts.gy);  // the current entry's t_near (0 for the root)
   double best = ts.best;
   float best32 = f32_up(best);
-  const uint32_t cap = S.stack_depth / 2u - STACK_SLACK;  // entries of two words
-  const auto dead = [&](float t) { return fmaf(t, 1.0f - 0x1p-19f, -0x1p-100f) > best32; };
-  const auto pop = [&]() {
-    --sp;
-    cur = stk_get<SPILL>(S, stk, stride, spl, 2u * sp);
-    ct = __uint_as_float(stk_get<SPILL>(S, stk, stride, spl, 2u * sp + 1u));
-  };
-  // drop the current entry and the entries under it while they lie beyond the closest hit (no node fetch)
-  const auto cull = [&]() {
-    while (cur != rpl::ENTRY_EMPTY && dead(ct)) {
-      if (sp == 0u) cur = rpl::ENTRY_EMPTY;
-      else pop();
-    }
-  };
+  const uint32_t cap = S.stack_depth - STACK_SLACK;
   DCYC_BEGIN(cnode)
   // ---- inner nodes
-  for (;;) {
-    cull();
-    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps descending, so lanes do
-    // not idle in this loop until every lane of the wave holds a leaf.  (Not in the cost probe, COUNT: there a lane's
-    // node visits and primitive tests must not depend on its wave-mates, so every rank of a balanced multi-GPU frame
-    // computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
-    if constexpr (!COUNT) {
-      if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
-        leaf = cur;
-        if (sp == 0u) cur = rpl::ENTRY_EMPTY;
-        else pop();
-        cull();
-      }
-    }
-    if (cur & rpl::ENTRY_LEAF) break;
+  while (!(cur & rpl::ENTRY_LEAF)) {
     DIAG(if (td) td->visits++;)
     if constexpr (COUNT) *work += WORK_VISIT;
     DREG(DREG_NODE)
@@ -985,97 +950,114 @@ RPK_INLINE void trav_step(const KScene& S, lds_u32* stk, uint32_t stride, uint32
 }
     RPK_CSWAP(0, 1) RPK_CSWAP(2, 3) RPK_CSWAP(0, 2) RPK_CSWAP(1, 3) RPK_CSWAP(1, 2)
 #undef RPK_CSWAP
-    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1 farther ones
-    // far-to-near, each with its t_near, without branches: entries sp..sp+2 are written unconditionally (the stack has
-    // STACK_SLACK spare entries; entries past the new top are garbage) and sp advances by k.
+    // The hits are a prefix of the sorted entries (misses sort last as +inf).  Push the k = hits - 1
+    // farther ones far-to-near without branches: slots sp..sp+2 are written unconditionally (the stack
+    // has STACK_SLACK spare entries; slots past the new top are garbage) and sp advances by k.
     const float INFF = __builtin_huge_valf();
     const uint32_t n_hit = (uint32_t)(tn[0] != INFF) + (uint32_t)(tn[1] != INFF) + (uint32_t)(tn[2] != INFF) +
                            (uint32_t)(tn[3] != INFF);
     const uint32_t k = n_hit > 1u ? n_hit - 1u : 0u;
     const uint32_t e0 = k == 3u ? cc[3] : (k == 2u ? cc[2] : cc[1]), e1 = k == 3u ? cc[2] : cc[1];
-    const float t0 = k == 3u ? tn[3] : (k == 2u ? tn[2] : tn[1]), t1 = k == 3u ? tn[2] : tn[1];
-    // Whether every lane's pushes stay in the LDS part of its stack: a wave-uniform branch (SPILL kernels), so the
-    // common case runs no per-lane exec-mask juggling for the spill path.
-    const bool lds_only = !SPILL || __ballot(2u * sp + 6u > S.lds_depth) == 0;
+    // Whether every lane's pushes and pops of this visit stay in the LDS part of its stack: a wave-uniform branch
+    // (SPILL kernels), so the common case runs no per-lane exec-mask juggling for the spill path.
+    const bool lds_only = !SPILL || __ballot(sp + 2u >= S.lds_depth) == 0;
     if (lds_only) {
-      stk[2u * sp * stride] = e0;
-      stk[(2u * sp + 1u) * stride] = __float_as_uint(t0);
-      stk[(2u * sp + 2u) * stride] = e1;
-      stk[(2u * sp + 3u) * stride] = __float_as_uint(t1);
-      stk[(2u * sp + 4u) * stride] = cc[1];
-      stk[(2u * sp + 5u) * stride] = __float_as_uint(tn[1]);
+      stk[sp * stride] = e0;
+      stk[(sp + 1u) * stride] = e1;
+      stk[(sp + 2u) * stride] = cc[1];
     } else {
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp, e0);
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 1u, __float_as_uint(t0));
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 2u, e1);
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 3u, __float_as_uint(t1));
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 4u, cc[1]);
-      stk_put<SPILL>(S, stk, stride, spl, 2u * sp + 5u, __float_as_uint(tn[1]));
+      stk_put<SPILL>(S, stk, stride, spl, sp, e0);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 1u, e1);
+      stk_put<SPILL>(S, stk, stride, spl, sp + 2u, cc[1]);
     }
     sp += k;
     if (sp > cap) {  // cannot happen for a stack sized from the tree depth; flagged, never written past
       overflow = true;
       sp = cap;
     }
-    // next: the nearest hit child, else the top of the stack (culled at the top of the loop)
-    if (n_hit) {
-      cur = cc[0];
-      ct = tn[0];
-    } else if (sp == 0u) {
-      cur = rpl::ENTRY_EMPTY;
-    } else if (lds_only) {
+    // pops below read entries < the pushes' top (sp + 2 before the push), so an LDS-only visit pops from LDS
+    const auto pop = [&]() -> uint32_t {
       --sp;
-      cur = stk[2u * sp * stride];
-      ct = __uint_as_float(stk[(2u * sp + 1u) * stride]);
+      return lds_only ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
+    };
+    // Speculative traversal (Aila & Laine 2009): a lane that reaches a leaf parks it and keeps
+    // descending, so lanes do not idle in this loop until every lane of the wave holds a leaf.  (Not in the
+    // cost probe, COUNT: there a lane's node visits and primitive tests must not depend on its wave-mates, so
+    // every rank of a balanced multi-GPU frame computes the same costs -- include/rp.h RP_SHARD_BALANCED.)
+    if (lds_only) {
+      // the next entry without a branch: the two entries under the top are read at once (indices clamped into the
+      // column; an entry below the stack's bottom is read but never taken), then the pop for a visit that hit no
+      // child and the pop behind a parked leaf are selects
+      const uint32_t t1 = stk[min(sp - 1u, sp) * stride], t2 = stk[min(sp - 2u, sp) * stride];
+      uint32_t npop = (!n_hit && sp) ? 1u : 0u;
+      uint32_t c = n_hit ? cc[0] : (sp ? t1 : rpl::ENTRY_EMPTY);
+      if constexpr (!COUNT) {
+        const bool park = (c & rpl::ENTRY_LEAF) && c != rpl::ENTRY_EMPTY && leaf == 0u;
+        const uint32_t left = sp - npop;
+        leaf = park ? c : leaf;
+        const uint32_t c2 = left ? (npop ? t2 : t1) : rpl::ENTRY_EMPTY;
+        npop += (park && left) ? 1u : 0u;
+        c = park ? c2 : c;
+      }
+      cur = c;
+      sp -= npop;
     } else {
-      pop();
+      if (n_hit) cur = cc[0];
+      else cur = sp ? pop() : rpl::ENTRY_EMPTY;
+      if constexpr (!COUNT) {
+        if ((cur & rpl::ENTRY_LEAF) && cur != rpl::ENTRY_EMPTY && leaf == 0u) {
+          leaf = cur;
+          cur = sp ? pop() : rpl::ENTRY_EMPTY;
+        }
+      }
     }
     if constexpr (!COUNT) {
-      // ... and once at most S.leaf_break lanes still look for a leaf, the wave moves on to the leaves: the
+      // ... and once at most S.leaf_break lanes still look for one, the wave moves on to the leaves: the
       // last few descents ran with most of the wave idle (those lanes resume their descent next step)
       if ((uint32_t)__popcll(__ballot(leaf == 0u)) <= S.leaf_break) break;
     }
   }
   DCYC_END(DCYC_NODE_LOOP, cnode)
   DCYC_BEGIN(cprim)
-  cull();
+  // the pops from here on only shrink sp: when no lane's stack reaches into its spill run, they all read LDS (a
+  // wave-uniform branch, as in the node loop)
+  const bool lds_pop = !SPILL || __ballot(sp > S.lds_depth) == 0;
+  const auto pop = [&]() -> uint32_t {
+    --sp;
+    return lds_pop ? stk[sp * stride] : stk_get<SPILL>(S, stk, stride, spl, sp);
+  };
   if (leaf == 0u && cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
     leaf = cur;
-    if (sp == 0u) cur = rpl::ENTRY_EMPTY;
-    else pop();
+    cur = sp ? pop() : rpl::ENTRY_EMPTY;
   }
   // ---- leaves: the reference's exact f64 primitive tests, the parked leaf first, then the current
-  // entry while it is a live leaf as well.  One primitive per lane per iteration across those leaves, so
+  // entry while it is a leaf as well.  One primitive per lane per iteration across those leaves, so
   // lanes with different leaf sizes advance together instead of the wave running every leaf's count.
-  uint32_t kp = leaf & rpl::LEAF_FIRST_MASK;
-  uint32_t kend = kp + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+  uint32_t k = leaf & rpl::LEAF_FIRST_MASK;
+  uint32_t kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
   while (leaf != 0u) {
     DIAG(if (td) td->tests++;)
     if constexpr (COUNT) *work += WORK_TEST;
     DREG(DREG_PRIM)
-    prim_test(S, kp, o, d, tmin, best, ts);
-    if (++kp == kend) {
-      best32 = f32_up(best);
-      cull();
+    prim_test(S, k, o, d, tmin, best, ts);
+    if (++k == kend) {
       if (cur != rpl::ENTRY_EMPTY && (cur & rpl::ENTRY_LEAF)) {
         leaf = cur;
-        if (sp == 0u) cur = rpl::ENTRY_EMPTY;
-        else pop();
-        kp = leaf & rpl::LEAF_FIRST_MASK;
-        kend = kp + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
+        cur = sp ? pop() : rpl::ENTRY_EMPTY;
+        k = leaf & rpl::LEAF_FIRST_MASK;
+        kend = k + ((leaf >> rpl::LEAF_SHIFT) & 7u) + 1u;
       } else {
         leaf = 0u;
       }
     }
     if (!COUNT && PRIM_BREAK > 0 && (uint32_t)__popcll(__ballot(leaf != 0u)) <= PRIM_BREAK) {
-      // park the rest of the current run [kp, kend) as a leaf entry; the next step tests it first
-      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - kp - 1u) << rpl::LEAF_SHIFT) | kp;
+      // park the rest of the current run [k, kend) as a leaf entry; the next step tests it first
+      if (leaf != 0u) leaf = rpl::ENTRY_LEAF | ((kend - k - 1u) << rpl::LEAF_SHIFT) | k;
       break;
     }
   }
   DCYC_END(DCYC_PRIM_LOOP, cprim)
   ts.cur = cur;
-  ts.gy = __float_as_uint(ct);
   ts.sp = sp;
   ts.best = best;
   ts.leaf = leaf;

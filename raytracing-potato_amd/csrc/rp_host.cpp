@@ -422,8 +422,8 @@ int rph_bvh_traversal_stats_ex(const rp_scene_desc* desc, const double* rays, ui
   // CPU model of rp_device.h's traversal over the same packed 4-wide tree: child boxes tested in f32 with
   // per-axis outward bounds (t = fma(P, inv, nb|fb), quantized: fma(q, s inv, fma(o, inv, nb|fb))), rcp
   // emulated by a correctly rounded 1/x, the min/max slab form instead of the device's octant selection
-  // (the same values), near-first order, stack entries that carry their t_near and are dropped unvisited once a
-  // closer primitive was accepted (4-wide trees, rp_device.h trav_step cull), exact f64 primitive tests.  per_ray: n x 3 {wide nodes visited, primitive tests, closest hittable id or
+  // (the same values), near-first order, exact f64
+  // primitive tests.  per_ray: n x 3 {wide nodes visited, primitive tests, closest hittable id or
   // 2^64-1}.  tests/test_bvh.py checks the closest hits against brute force.
   std::string err;
   int rc = rpb::validate(desc, err);
@@ -552,17 +552,8 @@ int rph_bvh_traversal_stats_ex(const rp_scene_desc* desc, const double* rays, ui
       per_ray[3 * r + 2] = bestp < 0 ? ~0ull : (uint64_t)bestp;
       continue;
     }
-    std::vector<std::pair<uint32_t, float>> stack;  // entry, t_near
+    std::vector<uint32_t> stack;
     uint32_t cur = ps.root;
-    // the next entry whose box still reaches the closest hit (rp_device.h trav_step: cull)
-    auto pop = [&]() -> uint32_t {
-      while (!stack.empty()) {
-        const auto e = stack.back();
-        stack.pop_back();
-        if (!(std::fma(e.second, 1.0f - 0x1p-19f, -0x1p-100f) > best32)) return e.first;
-      }
-      return rpl::ENTRY_EMPTY;
-    };
     for (;;) {
       while (!(cur & rpl::ENTRY_LEAF)) {
         visits++;
@@ -616,13 +607,16 @@ int rph_bvh_traversal_stats_ex(const rp_scene_desc* desc, const double* rays, ui
           for (int b = a + 1; b < 4; b++)
             if (tn[b] < tn[a]) { std::swap(tn[a], tn[b]); std::swap(cc[a], cc[b]); }
         for (int c = 3; c >= 1; c--)
-          if (tn[c] != INFINITY) stack.push_back({cc[c], tn[c]});
-        cur = tn[0] != INFINITY ? cc[0] : pop();
+          if (tn[c] != INFINITY) stack.push_back(cc[c]);
+        if (tn[0] != INFINITY) cur = cc[0];
+        else if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+        else { cur = stack.back(); stack.pop_back(); }
       }
       if (cur == rpl::ENTRY_EMPTY) break;
       const uint32_t first = cur & rpl::LEAF_FIRST_MASK, cnt = ((cur >> rpl::LEAF_SHIFT) & 7u) + 1u;
       for (uint32_t k = first; k < first + cnt; k++) test(k);
-      cur = pop();
+      if (stack.empty()) cur = rpl::ENTRY_EMPTY;
+      else { cur = stack.back(); stack.pop_back(); }
     }
     per_ray[3 * r] = visits;
     per_ray[3 * r + 1] = tests;

@@ -21,11 +21,11 @@ struct KScene {
   double qbound;         // Node4Q: bound on every node frame's |o| and 255 s (rp_layout.h qbound): the slab slack
   uint32_t node_format;  // rpl::NODES_F32 / NODES_Q8: picks the kernel instantiation
   uint32_t leaf_break;   // trav_step leaves the inner-node loop once at most this many lanes still seek a leaf
-  uint32_t stack_depth;  // traversal stack words per lane (4-wide: 2 x (3 x max_depth + 7), an entry is two words)
-  uint32_t lds_depth;    // words of it in LDS; words [lds_depth, stack_depth) spill to `spill`
+  uint32_t stack_depth;  // traversal stack entries per lane (3 x max_depth + 7)
+  uint32_t lds_depth;    // entries of it in LDS; entries [lds_depth, stack_depth) spill to `spill`
   uint64_t* diag;        // diagnostic counters (RPK_DIAG builds), DIAG_N x u64
   uint32_t* rng_slab;    // per-lane keystream cache, render_lanes x rng_slab_bytes_per_lane() bytes
-  uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) words
+  uint32_t* spill;       // per-lane stack overflow, render_lanes x (stack_depth - lds_depth) entries
   uint32_t* unit_t0;     // per-lane start time of the lane's measured unit (tile costs), render_lanes words
 };
 

@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "f20d553364ad3996"
+#define RP_BUILD_ID "edeb3da151eb1761"

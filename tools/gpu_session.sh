@@ -13,7 +13,8 @@
 #   trace_<CFG>        rocprofv3 --kernel-trace --stats around bench.py (the kernel's average launch duration: every launch
 #                      of the run renders the bench's frames per launch, no lone-frame or contract launches)
 #   tracedrv_<CFG>     rocprofv3 --kernel-trace --stats around the driver's command (--steps 20 --warmup 5)
-#   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ diag if present)
+#   pmc_<CFG>          six rocprofv3 --pmc passes over one bench launch -> tools/roofline.py record (+ the diag record
+#                      PMC_DIAG, default gpurun_out/${TAG}_<CFG>_diag.json, if present; PMC_LABEL names a labelled run)
 #   units_<CFG>        tools/unit_times.py: the longest measured unit per tile of a whole frame (UNITS_ARGS)
 #   lat_<CFG>          two --pmc passes: L1 TLB hits/misses, L2 read latency seen by the vector L1, DRAM share of L2 fills
 #   pmcx_<CFG>         one --pmc pass of the counters in PMCX (output name PMCX_NAME)
@@ -114,7 +115,7 @@ for s in ${STEPS:-tests}; do
       pre=gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_pmc
       made gpurun_out/${TAG}_${lc}_roofline.json "python3 tools/roofline.py --config $cfg over the six pmc passes above"
       python3 tools/roofline.py --config $cfg --bench ${pre}_sq.json ${PMC_BENCH_ARGS:+--all-dispatches} \
-        $([ -f gpurun_out/${TAG}_${cfg}_diag.json ] && [ -z "${PMC_LABEL:-}" ] && echo --diag gpurun_out/${TAG}_${cfg}_diag.json) \
+        $(d=${PMC_DIAG:-gpurun_out/${TAG}_${cfg}_diag.json}; [ -f $d ] && echo --diag $d) \
         --out gpurun_out/${TAG}_${lc}_roofline.json \
         ${pre}_sq ${pre}_mix64 ${pre}_mix32 ${pre}_fetch ${pre}_write ${pre}_l2 \
         > gpurun_out/${TAG}_${cfg}${PMC_LABEL:+_$PMC_LABEL}_roofline.log 2>&1 || exit 1 ;;
