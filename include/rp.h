@@ -233,7 +233,8 @@ enum { RP_LAYOUT_AUTO = 0, RP_LAYOUT_DFS = 1, RP_LAYOUT_DFS_LINE = 2 };
  * (log-spaced buckets, shard order inside; a frame ends with its longest unit), on one device or interleaved shards (a
  * balanced plan's tiles may move between frames: those frames keep TILES).  AUTO (ABI v9) = LEARNED for one stream per
  * pixel (samples_per_stream >= spp: lone C3 frames 220 vs 261 ms), TILES for several streams per pixel (32-sample streams:
- * +4.4 %).  Launches of several frames always use TILES.  Results never depend on it. */
+ * +4.4 %) and for launches of several frames (their interleaved tile order, rp_render_frames_device_ws);
+ * LEARNED also orders such launches, a unit's frames handed out together.  Results never depend on it. */
 enum { RP_UNITS_AUTO = 0, RP_UNITS_TILES = 1, RP_UNITS_LEARNED = 2 };
 typedef struct rp_scene_options {
   uint32_t builder;         /* RP_BUILDER_*: AUTO = HOST (multi-threaded binned SAH); DEVICE = LBVH (faster

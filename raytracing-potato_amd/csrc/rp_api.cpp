@@ -868,13 +868,15 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
     kp.tile_order = w->d_tile_order;
   }
   // The learned per-unit order (rp.h RP_UNITS_*, units_on): units longest first by the last render's durations on this
-  // workspace -- same frame shape and shard, one frame per launch, and not a balanced plan over several ranks (its tiles
-  // may move) -- and such renders store their units' durations for the next one.  The workspace's durations and order
+  // workspace -- same frame shape and shard, one frame per launch (or any launch under LEARNED: a unit's n_frames frames
+  // are then handed out together), and not a balanced plan over several ranks (its tiles may move) -- and such renders
+  // store their units' durations for the next one.  The workspace's durations and order
   // are committed only once the launch is enqueued.
   const uint64_t n_units = t.n_slots * t.nbatch;
   const uint32_t ugeom[8] = {p->width, p->height, t.tw, t.th, p->spp, t.sps, t.shard, t.shards};
-  const bool ufit = n_frames == 1 && units_on(s, t.nbatch) && w->d_ucost && n_units <= w->ucost_cap &&
-                    (!t.balanced || t.shards == 1);
+  // (launches of several frames: LEARNED only -- AUTO keeps their interleaved tile order)
+  const bool ufit = (n_frames == 1 || s->opt.unit_order == RP_UNITS_LEARNED) && units_on(s, t.nbatch) && w->d_ucost &&
+                    n_units <= w->ucost_cap && (!t.balanced || t.shards == 1);
   bool uorder = false;
   if (ufit && w->ucost_valid && std::memcmp(ugeom, w->ucost_geom, sizeof ugeom) == 0) {
     int e = rpk::launch_unit_order(w->d_ucost, n_units, w->d_ukey, w->d_ukey2, w->d_usort, w->usort_bytes, w->d_uorder,

@@ -1505,7 +1505,9 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
   const uint32_t tile_px = tw * th, tile_units = tile_px * A->P.nbatch;
   if (!PROBE && A->P.unit_order) {
     // the learned per-unit order (rp_sched.hip): queue g serves the chunks g, g + G, ... of C consecutive positions,
-    // position p holds unit unit_order[p] = slot * nbatch + batch; the same drained-queue walk as the tile queues below
+    // position p holds unit unit_order[p] = slot * nbatch + batch -- with several frames per launch, position p is frame
+    // p mod n_frames of unit unit_order[p / n_frames] (a unit's frames consecutive); the same drained-queue walk as the
+    // tile queues below
     const uint32_t G = max(A->P.queue_groups, 1u), C = A->P.order_chunk, GC = G * C;
     const uint32_t home = G > 1 ? blockIdx.x % G : 0u;
     const uint32_t Q = (uint32_t)A->P.n_queue;
@@ -1524,9 +1526,15 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
         }
       }
       const uint32_t i = RPK_UDIV(q, dv_ochunk);
-      const uint32_t u = A->P.unit_order[i * GC + g * C + (q - i * C)];
+      uint32_t pos = i * GC + g * C + (q - i * C), f = 0;
+      if (A->P.n_frames > 1) {
+        const uint32_t r = RPK_UDIV(pos, dv_frames);
+        f = pos - r * A->P.n_frames;
+        pos = r;
+      }
+      const uint32_t u = A->P.unit_order[pos];
       const uint32_t sl = RPK_UDIV(u, dv_nbatch);
-      batch = u - sl * A->P.nbatch;
+      batch = u - sl * A->P.nbatch + f * A->P.nbatch;  // (the unit carries its global batch)
       slot = sl;
       const uint32_t k = RPK_UDIV(sl, dv_tile_px), local = sl - k * tile_px;
       const uint32_t dk = A->P.shard + k * A->P.nshards, t = A->P.tile_map ? A->P.tile_map[dk] : dk;

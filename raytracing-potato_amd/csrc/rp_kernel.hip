@@ -259,7 +259,8 @@ __global__ void __launch_bounds__(BLOCK) RPK_RENDER_ATTR render_kernel(const KAr
           const bool mt = !PROBE && A->P.tile_meas && meas_unit(pipj, batch);
           if (!PROBE && (mt || A->P.unit_cost)) {
             const uint32_t dur = (uint32_t)__builtin_amdgcn_s_memrealtime() - A->S.unit_t0[blockIdx.x * BLOCK + tid];
-            if (A->P.unit_cost) A->P.unit_cost[(uint64_t)slot * A->P.nbatch + batch] = dur;
+            if (A->P.unit_cost)  // (every frame of a launch writes its unit's slot: any of them is the pixel's cost)
+              A->P.unit_cost[(uint64_t)slot * A->P.nbatch + (batch - unit_frame(A, batch) * A->P.nbatch)] = dur;
             if (mt) {
               meas_dur = dur >> MEAS_SHIFT;
               meas_k = slot / (A->P.tw * A->P.th);

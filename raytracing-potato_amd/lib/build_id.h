@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "edeb3da151eb1761"
+#define RP_BUILD_ID "13c06ba3cbadb017"

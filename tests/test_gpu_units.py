@@ -106,3 +106,41 @@ def test_learned_unit_order_is_longest_first(gpu):
     assert b[0] == _bucket(dur).max() and (dur > 0).sum() == 60 * 44
     assert b[-1] == 0 and dur[order[-1]] == 0  # the edge slots outside the 60 x 44 frame never ran
     assert _bucket(dur).max() - np.median(_bucket(dur[dur > 0])) >= 8  # the scene has long and short units (2 octaves)
+
+
+@pytest.mark.parametrize("sps", [0, 48])
+def test_learned_unit_order_frame_launch(gpu, sps):
+    """LEARNED also orders launches of several frames (a unit's frames handed out together, each with its own seeds): the
+    second launch of 3 frames on a workspace uses the order its first launch learned, and every frame of it equals its
+    lone render bit for bit, counters summed."""
+    import torch
+    from rtpotato import _ffi as F
+    from rtpotato.scene import shard_slot_count
+    sc, p = _scene("bunny_full", 64, 40, 48)
+    p = replace(p, samples_per_stream=sps, tile_w=16, tile_h=16)
+    n, nf = shard_slot_count(p), 3
+    B = -(-p.spp // (sps or F.RP_SAMPLES_PER_STREAM))
+    dev = torch.device("cuda", 0)
+    with gpu.DeviceScene(sc, options={"unit_order": "learned"}) as ds:
+        w = ds.workspace()
+        ds.reserve_frames(p, nf, w)
+        out = torch.zeros(nf * 3 * n, dtype=torch.float64, device=dev)
+        ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+        ds.render_frames_device(p, nf, out, ctr, workspace=w)
+        assert not ds.frame_info(w) & F.RP_FRAME_UNIT_ORDER
+        ds.render_frames_device(p, nf, out, ctr, workspace=w)
+        torch.cuda.synchronize()
+        assert ds.frame_info(w) & F.RP_FRAME_UNIT_ORDER
+        multi = out.cpu().numpy().reshape(nf, n, 3)
+        rays = 0
+        with gpu.DeviceScene(sc, options={"unit_order": "tiles"}) as ref:
+            for f in range(nf):
+                o = torch.zeros(3 * n, dtype=torch.float64, device=dev)
+                c = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device=dev)
+                ref.reserve(p)
+                ref.render_device(replace(p, seed=p.seed + f * B * p.width * p.height), o, c)
+                torch.cuda.synchronize()
+                assert np.array_equal(multi[f].view(np.uint64), o.cpu().numpy().reshape(n, 3).view(np.uint64)), f
+                rays += int(c[0])
+        assert int(ctr[0]) == rays and int(ctr[3]) == 0
+        w.close()
