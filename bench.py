@@ -268,7 +268,7 @@ def main():
     ap.add_argument("--frames-per-launch", type=int, default=32,
                     help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
                          "the frame of seed + f * B * W * H); a step is still one frame (K frames in launches of <= L)")
-    ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved"),
+    ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved", "pixel"),
                     help="RP_FRAME_ORDER_* of a launch of several frames")
     ap.add_argument("--no-single-frame", action="store_true",
                     help="skip the single-frame-per-launch timing reported beside a frame-sequence headline")

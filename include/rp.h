@@ -375,9 +375,10 @@ int rp_workspace_set_tile_costs(rp_scene* scene, rp_workspace* workspace, const 
  * frame_order (RP_FRAME_ORDER_*): SEQUENTIAL hands out frame 0's units, then frame 1's, ...; INTERLEAVED hands out the
  * frames' k-th tiles of the cost order together, for k = 0, 1, ... -- the units in flight at any moment come from a
  * narrower band of the cost order (fewer lanes idle in a wave whose neighbours run longer paths), every frame ends near
- * the launch's end.  AUTO = INTERLEAVED.  The frames' pixels do not depend on it. */
+ * the launch's end.  PIXEL (ABI v9) is INTERLEAVED with a tile's units handed out pixel by pixel, each pixel's frames
+ * consecutive (a wave holds a few pixels x their frames).  AUTO = INTERLEAVED.  The frames' pixels do not depend on it. */
 #define RP_MAX_FRAMES 64
-enum { RP_FRAME_ORDER_AUTO = 0, RP_FRAME_ORDER_SEQUENTIAL = 1, RP_FRAME_ORDER_INTERLEAVED = 2 };
+enum { RP_FRAME_ORDER_AUTO = 0, RP_FRAME_ORDER_SEQUENTIAL = 1, RP_FRAME_ORDER_INTERLEAVED = 2, RP_FRAME_ORDER_PIXEL = 3 };
 int rp_workspace_reserve_frames(rp_scene* scene, rp_workspace* workspace, const rp_render_params* params,
                                 uint32_t n_frames);
 int rp_render_frames_device_ws(rp_scene* scene, rp_workspace* workspace, const rp_camera* camera,

@@ -676,7 +676,7 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   if (!w || w->scene != s) return fail(RP_EINVAL, "workspace is NULL or belongs to another scene");
   w->frame_flags = 0;  //  before any return: an spp = 0 or refused render reports no scheduling
   if (n_frames == 0 || n_frames > RP_MAX_FRAMES) return fail(RP_EINVAL, "n_frames must be 1..RP_MAX_FRAMES");
-  if (frame_order > RP_FRAME_ORDER_INTERLEAVED) return fail(RP_EINVAL, "frame_order must be an RP_FRAME_ORDER_* value");
+  if (frame_order > RP_FRAME_ORDER_PIXEL) return fail(RP_EINVAL, "frame_order must be an RP_FRAME_ORDER_* value");
   Tiling t;
   int rc = make_tiling(p, t);
   if (rc) return rc;
@@ -742,6 +742,10 @@ int render_shard(rp_scene* s, rp_workspace* w, const rp_camera* cam, const rp_re
   kp.queue_chunk = qmode == RP_QUEUES_XCD_REGIONS ? (t.n_shard_tiles + kp.queue_groups - 1) / kp.queue_groups
                   : kp.queue_groups > 1 ? (s->opt.queue_chunk ? s->opt.queue_chunk : chunk_auto) : 1u;
   if (kp.queue_chunk == 0) kp.queue_chunk = 1;
+  // RP_FRAME_ORDER_PIXEL needs a queue's runs of n_frames virtual tiles to be one tile of every frame: single queue, or
+  // chunks of whole multiples of n_frames (the default chunk is); otherwise it is INTERLEAVED
+  if (kp.frames_inter && frame_order == RP_FRAME_ORDER_PIXEL && (kp.queue_groups == 1 || kp.queue_chunk % n_frames == 0))
+    kp.frames_inter = 2;
   // a 32-bit queue word takes its units, plus one failed fetch per resident lane after the last unit (single
   // queue) or one per fetch that passes a drained queue on the way to another (per-XCD queues)
   if ((kp.queue_groups > 1 ? 2 * kp.n_queue : kp.n_queue) + s->lanes() >= 0xffffffffull)

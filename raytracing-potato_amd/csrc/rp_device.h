@@ -1572,8 +1572,17 @@ RPK_INLINE bool fetch_pixel(uint32_t& slot, uint32_t& pi, uint32_t& pj, uint32_t
       }
     }
     // (PROBE launches decode with plain divisions: one small launch)
-    const uint32_t i = PROBE ? q / tile_units : RPK_UDIV(q, dv_units);
-    const uint32_t rem = q - i * tile_units;
+    uint32_t i = PROBE ? q / tile_units : RPK_UDIV(q, dv_units);
+    uint32_t rem = q - i * tile_units;
+    if (!PROBE && A->P.frames_inter == 2u) {
+      // RP_FRAME_ORDER_PIXEL: the n_frames consecutive virtual tiles of a queue's sequence (one shard tile of every
+      // frame) as one run of units with a unit's frames consecutive -- a wave holds ~64 / n_frames pixels x their frames
+      const uint32_t grp = RPK_UDIV(i, dv_frames);
+      const uint32_t o = (i - grp * A->P.n_frames) * tile_units + rem;
+      const uint32_t u = RPK_UDIV(o, dv_frames);
+      i = grp * A->P.n_frames + (o - u * A->P.n_frames);
+      rem = u;
+    }
     const uint32_t ic = PROBE ? i / C : RPK_UDIV(i, dv_chunk);
     uint32_t k = ic * GC + g * C + (i - ic * C);
     // a tile's units pixel-major, a pixel's batches consecutive: a wave fetches 64 / nbatch pixels with all

@@ -120,7 +120,7 @@ struct KParams {
   // together) -- a unit carries its global batch f * nbatch + b, and frame f writes out + f * out_stride (out_fg + f *
   // n_slots) or its batch sums at partial + 3 (f * n_slots + slot) * nbatch.
   uint32_t n_frames;            // >= 1
-  uint32_t frames_inter;        // 1: rank by rank
+  uint32_t frames_inter;        // 1: rank by rank; 2: rank by rank, a unit's frames consecutive (RP_FRAME_ORDER_PIXEL)
   Div32 dv_tiles, dv_frames;    // make_div32(n_shard_tiles), make_div32(n_frames)
   uint64_t out_stride;          // doubles between frames' shard buffers (3 * n_slots)
 };

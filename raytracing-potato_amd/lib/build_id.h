@@ -1,1 +1,1 @@
-#define RP_BUILD_ID "13c06ba3cbadb017"
+#define RP_BUILD_ID "ec12f559726a6fda"

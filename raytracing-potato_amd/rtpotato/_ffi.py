@@ -38,7 +38,7 @@ RP_SHARD_INTERLEAVE, RP_SHARD_BALANCED = 0, 1
 RP_STATUS_STACK_OVERFLOW, RP_STATUS_PLAN_MISMATCH = 1, 2
 RP_ABI_VERSION = 9
 RP_MAX_FRAMES = 64
-RP_FRAME_ORDER_AUTO, RP_FRAME_ORDER_SEQUENTIAL, RP_FRAME_ORDER_INTERLEAVED = 0, 1, 2
+RP_FRAME_ORDER_AUTO, RP_FRAME_ORDER_SEQUENTIAL, RP_FRAME_ORDER_INTERLEAVED, RP_FRAME_ORDER_PIXEL = 0, 1, 2, 3
 
 
 class rp_hittable(Structure):

@@ -211,7 +211,8 @@ class DeviceScene:
         F.check(F.rp().rp_render_frames_device_ws(self.handle, workspace.handle if workspace else None,
                                                   ctypes.byref(cam), ctypes.byref(p), n_frames,
                                                   {"auto": F.RP_FRAME_ORDER_AUTO, "sequential": F.RP_FRAME_ORDER_SEQUENTIAL,
-                                                   "interleaved": F.RP_FRAME_ORDER_INTERLEAVED}.get(order, order),
+                                                   "interleaved": F.RP_FRAME_ORDER_INTERLEAVED,
+                                                   "pixel": F.RP_FRAME_ORDER_PIXEL}.get(order, order),
                                                   out.data_ptr(),
                                                   fg.data_ptr() if fg is not None else None, counters.data_ptr(),
                                                   ctypes.c_void_p(s.cuda_stream)))

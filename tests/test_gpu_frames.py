@@ -71,7 +71,7 @@ def _assert_same(multi, single, mfg, sfg, ctr, sctr):
     assert ctr[3] == 0
 
 
-@pytest.mark.parametrize("order", ["sequential", "interleaved"])
+@pytest.mark.parametrize("order", ["sequential", "interleaved", "pixel"])
 @pytest.mark.parametrize("sps", [48, 0, 7, 16])
 @pytest.mark.parametrize("n_frames", [1, 3])
 def test_frames_equal_single_renders(gpu, sps, n_frames, order):
@@ -90,7 +90,7 @@ def test_frames_scenes(gpu, name):
         _assert_same(*_frames_vs_singles(ds, replace(p, samples_per_stream=8), 4))
 
 
-@pytest.mark.parametrize("order", ["sequential", "interleaved"])
+@pytest.mark.parametrize("order", ["sequential", "interleaved", "pixel"])
 @pytest.mark.parametrize("shard_map", [0, 1])
 def test_frames_shards(gpu, shard_map, order):
     """Shard 1 of 3, interleaved and of the balanced plan.  The plan and the tile order are made once per launch, for
@@ -146,7 +146,7 @@ def test_frames_spp0_and_errors(gpu):
         with pytest.raises(F.RPError):
             ds.render_frames_device(q, 0, out, ctr)
         with pytest.raises(F.RPError):
-            ds.render_frames_device(q, 2, out, ctr, order=3)
+            ds.render_frames_device(q, 2, out, ctr, order=4)
         with pytest.raises(F.RPError):
             ds.render_frames_device(q, F.RP_MAX_FRAMES + 1, torch.zeros(3 * n * 65, dtype=torch.float64, device=dev), ctr)
         ds.reserve(q)  # one frame's batch sums: two frames do not fit

@@ -24,7 +24,7 @@ if [ "$P" = all ] || [ "$P" = final ]; then
 fi
 if [ "$P" = all ] || [ "$P" = sweep ]; then
   TAG=${T}s STEPS="ab_C3" STEPS_AB=16 REPS=2 BENCH_ARGS="--no-single-frame --contract-steps 0" \
-    RUNS="main:main: uol:main:unit_order=learned tt20:main:trav_threshold=20 tt28:main:trav_threshold=28 lb6:main:leaf_break=6 lb12:main:leaf_break=12 pb8:pb8: pb16:pb16:" \
+    RUNS="main:main: pix:main:--frame-order=pixel uol:main:unit_order=learned tt20:main:trav_threshold=20 tt28:main:trav_threshold=28 lb6:main:leaf_break=6 lb12:main:leaf_break=12 pb8:pb8: pb16:pb16:" \
     bash $S || exit 1
 fi
 if [ "$P" = all ] || [ "$P" = shards ]; then
