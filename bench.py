@@ -11,7 +11,8 @@ by librp's frame gather (rp_frame_gather): to_srgb_u8 -> B, G, R, A bytes, one R
 pixel over xGMI (one collective per launch for all its frames, rp_frames_gather), and the device-side de-interleave into
 frame order on every rank (the body of the reference's output.tga), counters summed over the ranks by RCCL as well.  torch.distributed (gloo) only bootstraps the RCCL
 communicator and takes the barrier and max-time reduction.  The K frames are a frame sequence rendered in launches of
-at most L = 32 (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order): the process renders
+at most L = 32 (--frames-per-launch; rp_render_frames_device_ws, frames interleaved in cost order, a pixel's frames
+consecutive: RP_FRAME_ORDER_PIXEL): the process renders
 ONE sequence -- warm-up, timed, single-frame and side-leg launches take its next frames, frame f the config's frame of
 seed + f * B * W * H (B sample batches per pixel), so no timed frame repeats a warm-up frame's seeds -- every frame
 traced, shaded and gathered in full.  `value` is that frame-sequence throughput: no frame of a launch is available
@@ -268,8 +269,9 @@ def main():
     ap.add_argument("--frames-per-launch", type=int, default=32,
                     help="frames rendered by one persistent launch (rp_render_frames_device_ws: frame f of a launch is "
                          "the frame of seed + f * B * W * H); a step is still one frame (K frames in launches of <= L)")
-    ap.add_argument("--frame-order", default="interleaved", choices=("sequential", "interleaved", "pixel"),
-                    help="RP_FRAME_ORDER_* of a launch of several frames")
+    ap.add_argument("--frame-order", default="pixel", choices=("sequential", "interleaved", "pixel"),
+                    help="RP_FRAME_ORDER_* of a launch of several frames (pixel: interleaved with a pixel's frames "
+                         "consecutive, C3 -0.66 %% against interleaved, profiles/r6/c3_v58_knob_sweep_ab.json)")
     ap.add_argument("--no-single-frame", action="store_true",
                     help="skip the single-frame-per-launch timing reported beside a frame-sequence headline")
     ap.add_argument("--shard-of", type=int, default=0,

@@ -37,4 +37,18 @@ if [ "$P" = all ] || [ "$P" = shards ]; then
   TAG=${T}y STEPS="shards_C3" SHARD_NS=1,2,4,8 SHARD_REPS=1 \
     SHARD_ARGS="--maps balanced --inflight 3 --per-launch 20 --frames 20" bash $S || exit 1
 fi
+if [ "$P" = s2 ]; then
+  # the PIXEL frame order confirmed on the whole frame and on an 8-way shard (3 reps), then the records and the bench line
+  # under it (bench.py's default since v58); the diag records of session q6 (lone frames: no frame order) are reused
+  TAG=${T}u STEPS="ab_C3" STEPS_AB=16 REPS=3 BENCH_ARGS="--no-single-frame --contract-steps 0" \
+    RUNS="inter:main:--frame-order=interleaved pix:main:" bash $S || exit 1
+  TAG=${T}v STEPS="ab_C3" STEPS_AB=40 REPS=3 BENCH_ARGS="--no-single-frame --contract-steps 0 --frames-per-launch 20" \
+    RUNS="sinter:main:--shard-of=8,--shard=3,--frame-order=interleaved spix:main:--shard-of=8,--shard=3" bash $S || exit 1
+  TAG=${T}w STEPS="bench_C3 tracedrv_C3" BENCH_ARGS="--steps 20 --warmup 5" bash $S || exit 1
+  TAG=${T}w STEPS="pmc_C3" PMC_DIAG=profiles/r6/c3_v58_diag.json bash $S || exit 1
+  TAG=${T}w STEPS="pmc_C3" PMC_LABEL=s32 PMC_DIAG=profiles/r6/c3_v58_s32_diag.json \
+    PMC_BENCH_ARGS="--steps 16 --warmup 0 --no-single-frame --samples-per-stream 32" bash $S || exit 1
+  TAG=${T}w STEPS="pmc_C5" PMC_LABEL=s32 PMC_DIAG=profiles/r6/c5_v58_s32_diag.json \
+    PMC_BENCH_ARGS="--steps 3 --warmup 0 --no-single-frame --samples-per-stream 32" bash $S || exit 1
+fi
 echo "r6_session done $(date +%T)" >> gpurun_out/${T}_done.txt
