@@ -51,4 +51,10 @@ if [ "$P" = s2 ]; then
   TAG=${T}w STEPS="pmc_C5" PMC_LABEL=s32 PMC_DIAG=profiles/r6/c5_v58_s32_diag.json \
     PMC_BENCH_ARGS="--steps 3 --warmup 0 --no-single-frame --samples-per-stream 32" bash $S || exit 1
 fi
+if [ "$P" = s3 ]; then
+  # the final tree's GPU suite, and the projected N-GPU scaling of bench.py's N > 1 loop in its PIXEL frame order
+  TAG=${T}t STEPS="tests" bash $S || exit 1
+  TAG=${T}y STEPS="shards_C3" SHARD_NS=1,2,4,8 SHARD_REPS=1 \
+    SHARD_ARGS="--maps balanced --inflight 3 --per-launch 20 --frames 20 --frame-order pixel" bash $S || exit 1
+fi
 echo "r6_session done $(date +%T)" >> gpurun_out/${T}_done.txt

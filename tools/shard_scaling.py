@@ -46,7 +46,7 @@ def _render_ws(ds, sp, w):
     torch.cuda.synchronize()
 
 
-def inflight_time(ds, sp, F, frames, table=None, per_launch=1):
+def inflight_time(ds, sp, F, frames, table=None, per_launch=1, order="interleaved"):
     """Steady per-frame time of shard sp with F launches in flight (bench.py's loop without the gather): launches of
     per_launch frames (rp_render_frames_device_ws, interleaved) alternate over F streams and workspaces; one warm-up
     round, then `frames` frames (in launches of per_launch) timed together."""
@@ -69,7 +69,7 @@ def inflight_time(ds, sp, F, frames, table=None, per_launch=1):
         if L == 1:
             ds.render_device(sp, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
         else:
-            ds.render_frames_device(sp, L, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i])
+            ds.render_frames_device(sp, L, bufs[i], ctrs[i], stream=streams[i], workspace=wss[i], order=order)
 
     for i in range(F):
         launch(i)
@@ -105,6 +105,8 @@ def main():
                          "its first gathered frame: the measured costs of all shards, combined through the deal order "
                          "and installed with rp_workspace_set_tile_costs); 0: the whole-frame probe every frame")
     ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value (as bench.py --opt)")
+    ap.add_argument("--frame-order", default="pixel", choices=("interleaved", "pixel"),
+                    help="RP_FRAME_ORDER_* of a launch of several frames (bench.py's default: pixel)")
     a = ap.parse_args()
     options = {}
     for kv in a.opt:
@@ -119,7 +121,7 @@ def main():
     ds = DeviceScene(scene, options=options)
     ds.render(replace(params, spp=4))  # warm
     out = {"config": a.config, "tile": [params.tile_w, params.tile_h], "reps": a.reps, "inflight": a.inflight,
-           "per_launch": a.per_launch,
+           "per_launch": a.per_launch, "frame_order": a.frame_order,
            "scene_options": options or "defaults", "per_map": {}}
     import statistics
     for mp in a.maps.split(","):
@@ -133,7 +135,7 @@ def main():
                 if table is not None:
                     ds.set_tile_costs(sp, table, n)
                 if a.inflight > 1 or a.per_launch > 1:
-                    t, r = inflight_time(ds, sp, a.inflight, a.frames, table, a.per_launch)
+                    t, r = inflight_time(ds, sp, a.inflight, a.frames, table, a.per_launch, a.frame_order)
                     times.append(t)
                     rays += r
                     continue
