@@ -23,6 +23,11 @@ def main():
     ap.add_argument("--sps", type=int, default=0, help="samples_per_stream (the RNG contract; 0 = 32, >= spp: one "
                                                        "stream per pixel)")
     ap.add_argument("--opt", action="append", default=[], help="rp_scene_options field=value")
+    ap.add_argument("--frames", type=int, default=1,
+                    help="> 1: one launch of this many frames (rp_render_frames_device_ws, bench.py's loop), measured "
+                         "after a warm launch of the same size on the same workspace; the timeline bins (10 ms, 64 of "
+                         "them) then cover only the launch's first 640 ms")
+    ap.add_argument("--frame-order", default="pixel", choices=("interleaved", "pixel", "sequential"))
     a = ap.parse_args()
     os.environ.setdefault("RP_LIB", os.path.join(REPO, "raytracing-potato_amd", "lib", "librp_diag.so"))
     from dataclasses import replace
@@ -43,8 +48,26 @@ def main():
         ds.set_tile_costs(params, learned_table(ds, params, a.shards), a.shards)
     NDIAG = 416  # rp_kernel.h DIAG_N
     buf = (ctypes.c_uint64 * NDIAG)()
-    F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
-    _, _, st = ds.render(params)
+    if a.frames > 1:
+        import time
+        import torch
+        from rtpotato.scene import shard_slot_count
+        ds.reserve_frames(params, a.frames)
+        n = shard_slot_count(params)
+        out_rgb = torch.zeros(a.frames * 3 * max(1, n), dtype=torch.float64, device="cuda")
+        ctr = torch.zeros(F.RP_COUNTERS_LEN, dtype=torch.int64, device="cuda")
+        ds.render_frames_device(params, a.frames, out_rgb, ctr, order=a.frame_order)  # warm: learns the tile costs
+        torch.cuda.synchronize()
+        ctr.zero_()
+        F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
+        t = time.perf_counter()
+        ds.render_frames_device(params, a.frames, out_rgb, ctr, order=a.frame_order)
+        torch.cuda.synchronize()
+        st = {"rays": int(ctr[0]), "seconds": time.perf_counter() - t}
+        assert int(ctr[3]) == 0, "status bits set"
+    else:
+        F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
+        _, _, st = ds.render(params)
     F.check(F.rp().rp_diagnostics(ds.handle, buf, NDIAG, 1))
     d = list(buf)
     ph = d[:5]
@@ -52,6 +75,7 @@ def main():
     iters, active, trips, visits, tests = d[5], d[6], d[7], d[8], d[9]
     out = {
         "config": a.config, "spp": a.spp, "samples_per_stream": a.sps or 32, "rays": st["rays"], "seconds": st["seconds"],
+        "frames_per_launch": a.frames, **({"frame_order": a.frame_order} if a.frames > 1 else {}),
         "phase_share": {k: round(v / tot, 4) for k, v in zip(["fetch", "rng_refill", "traverse", "shade", "tail"], ph)},
         "wave_iterations": iters, "lanes_active_at_traverse": round(active / max(1, iters) / 64, 4),
         "visits_per_ray": round(visits / st["rays"], 3), "prim_tests_per_ray": round(tests / st["rays"], 3),
