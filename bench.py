@@ -32,7 +32,8 @@ launch's rays, over the launch's duration (HIP events on its stream):
              MI355X_MICROARCH.md; Infinity-Cache hits are counted, so an upper bound of HBM traffic) against the 8 TB/s
              HBM peak -- the HBM roofline fraction; traffic = those bytes per launch (kernel_ms: its mean duration; a
              launch renders frames_per_launch frames);
-  binding_frac = the fraction of its own roof of what binds the kernel: the larger of the VALU-issue fraction and frac;
+  binding_frac = the fraction of its own roof of what binds the kernel: the larger of the VALU pipe's busy fraction
+             (valu_busy: AMD's VALUBusy from SQ_ACTIVE_INST_VALU) and frac;
   l2_level = the kernel's ALGORITHMIC bytes (its node visits x node bytes + primitive tests x 80 B + the closest hit's
              records + texels + keystream, from the diagnostic build's counts) at this rate, against the guide's
              measured L2-shared gather rate (16.8-18.8 TB/s): these bytes are served by L2 and the Infinity Cache;
@@ -59,24 +60,23 @@ METRIC = "Mrays/s at 1920×1080×256spp bunny scene; 1/2/4/8-GPU scaling + %HBM 
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 SIMDS = 1024                 # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9             # MI355X_MICROARCH.md max clock
-# a wave64 VALU instruction occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md "Wave scheduling")
+# a wave64 v_fma_f32 occupies a SIMD-32 for 2 cycles (MI355X_MICROARCH.md "Wave scheduling"): the issue ceiling if every
+# instruction were that fast.  Most are not: tools/valu_rates.hip measured ~4.1 SIMD cycles per wave64 instruction for
+# f64 ops, compares, selects, min/max, conversions, permutes and the packed f32 ops, ~2.3 only for f32 FMA/ADD/MUL, integer
+# add/sub/logic, right shifts and moves (profiles/r6/valu_rates_gfx950.json) -- so the VALU pipe's busy fraction is read
+# from the hardware (SQ_ACTIVE_INST_VALU, AMD's VALUBusy), not priced from instruction counts.
 VALU_ISSUE_PEAK = SIMDS * CLOCK_HZ / 2.0
-# Weighted VALU pipe occupancy: SIMD cycles per wave64 instruction by class.  f32 / integer / conversion:
-# 2 (the row above); f64 add, mul and FMA issue at half the f32 rate (spec): 4; f32 transcendentals take 8 cycles of
-# one wave's issue against 4 for v_fma_f32 (MI355X_MICROARCH.md "vector-instruction ISSUE cost"): 4; f64
-# transcendentals (v_rcp/v_sqrt/v_rsq_f64) are priced at twice that, 8 -- an assumption, the guide lists no f64 row.
-VALU_CYCLES = {"SQ_INSTS_VALU_ADD_F64": 4.0, "SQ_INSTS_VALU_MUL_F64": 4.0, "SQ_INSTS_VALU_FMA_F64": 4.0,
-               "SQ_INSTS_VALU_TRANS_F32": 4.0, "SQ_INSTS_VALU_TRANS_F64": 8.0}
+CUS = SIMDS // 4
 
 
-def valu_cycles_per_ray(rec):
-    """SIMD cycles per ray the record's VALU instructions occupy, weighted by class (VALU_CYCLES, else 2), or None when
-    the record lacks the instruction mix."""
+def valu_busy_per_ray(rec):
+    """SQ_ACTIVE_INST_VALU per ray (quad-cycles summed over the SIMDs: AMD's VALUBusy = it / CUs / cycles) and the VALU
+    lane utilisation (SQ_THREAD_CYCLES_VALU / (it x 64)), or None when the record lacks them."""
     c = rec.get("counters", {})
-    if "SQ_INSTS_VALU" not in c or not all(k in c for k in VALU_CYCLES):
+    if "SQ_ACTIVE_INST_VALU" not in c or not c["SQ_ACTIVE_INST_VALU"]:
         return None
-    other = c["SQ_INSTS_VALU"] - sum(c[k] for k in VALU_CYCLES)
-    return (2.0 * other + sum(w * c[k] for k, w in VALU_CYCLES.items())) / rec["rays"]
+    util = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]) if "SQ_THREAD_CYCLES_VALU" in c else None
+    return c["SQ_ACTIVE_INST_VALU"] / rec["rays"], util
 # SURVEY.md 8d algorithmic bytes per event of the REFERENCE traversal (reference tree, f64 layout)
 BYTES = {"box_tests": 56, "tri_tests": 84, "sphere_tests": 32, "tri_hits": 120, "texels": 4}
 # MI355X_MICROARCH.md "Indexed rows": rows shared by every workgroup, gathered from the XCD's L2: 16.8-18.8 TB/s
@@ -409,9 +409,10 @@ def main():
         freed[i] = torch.cuda.Event()
         freed[i].record(main_stream)
 
-    def run(spx, nframes, events=True):
-        """nframes frames in launches of <= L (max-over-ranks seconds, launch events, rays per frame, samples)."""
-        sizes = launch_sizes(nframes, L)
+    def run(spx, nframes, events=True, per_launch=None):
+        """nframes frames in launches of <= per_launch (default L) frames (max-over-ranks seconds, launch events, rays
+        per frame, samples)."""
+        sizes = launch_sizes(nframes, per_launch or L)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in sizes]
         if world > 1:
             dist.barrier()
@@ -478,19 +479,21 @@ def main():
     # StdRng stream per pixel running the unchanged body of main.rs:70-86 over all spp).
     side, side_key = None, None
     one_stream = params.samples_per_stream >= params.spp
+    side_sps = F.RP_SAMPLES_PER_STREAM if one_stream else params.spp
+    # the side contract's own launch cap: 32-sample streams carry spp / 32 units per pixel (C5: 15 frames a launch)
+    Lc = frames_per_launch_cap(L, nslots, -(-params.spp // side_sps))
     csteps = args.contract_steps if args.contract_steps >= 0 else (
-        (L if L > 1 else 3) if (sps_auto or not args.samples_per_stream) and not (args.shard_of or args.spp or args.tile)
+        (Lc if Lc > 1 else 3) if (sps_auto or not args.samples_per_stream) and not (args.shard_of or args.spp or args.tile)
         else 0)
     if csteps > 0 and params.spp > F.RP_SAMPLES_PER_STREAM:
         side_key = "streams_of_32" if one_stream else "contract_one_stream"
-        side_sps = F.RP_SAMPLES_PER_STREAM if one_stream else params.spp
         spc = shard_params(replace(params, samples_per_stream=side_sps), rank, world)
         for w in wss:
-            ds.reserve_frames(spc, L, w)
+            ds.reserve_frames(spc, Lc, w)
         for _ in range(F_):  # one launch per in-flight workspace: each learns this contract's tile costs
             step(1, spx=spc)
             torch.cuda.synchronize()
-        tcs, _, crays, _, csz = run(spc, csteps, events=False)
+        tcs, _, crays, _, csz = run(spc, csteps, events=False, per_launch=Lc)
         side = {"samples_per_stream": side_sps, "steps": csteps, "warmup": F_, "launches": csz,
                 "ms_per_step": round(tcs / csteps * 1e3, 3),
                 "value": round(crays * csteps / tcs / 1e6, 3), "unit": "Mrays/s",
@@ -558,25 +561,26 @@ def main():
                                      "frac": round(tf / FP64_VALU_PEAK_TFLOPS, 4),
                                      "note": "upper bound: f64 FMA (2 flops), MUL, ADD, transcendental wave-instructions "
                                              "x 64 lanes; peak = half the FP32 vector rate (spec)"}
-            wcyc = valu_cycles_per_ray(rec)
-            pipe = None
-            if wcyc is not None:
-                # the VALU pipes' busy fraction: weighted SIMD cycles of this launch's rays over the SIMD-cycles of the launch
-                pipe = wcyc * local_rays / kernel_s / (SIMDS * CLOCK_HZ)
-                roof["valu_issue"]["weighted"] = {
-                    "frac": round(pipe, 4), "simd_cycles_per_ray": round(wcyc, 2),
-                    "weights": {**{k.replace("SQ_INSTS_VALU_", "").lower(): v for k, v in VALU_CYCLES.items()},
-                                "other": 2.0},
-                    "note": "SIMD cycles per wave64 instruction by class (bench.py VALU_CYCLES): f64 add/mul/fma at half "
-                            "the f32 rate, transcendentals at the guide's 8-cycle single-wave issue (f64 assumed twice "
-                            "that); unweighted frac counts every instruction at 2 cycles"}
-            valu_bind = pipe if pipe is not None else valu_frac
-            binding = (("valu_pipe_weighted" if pipe is not None else "valu_issue"), valu_bind) \
-                if valu_bind >= tr_frac else ("hbm_traffic", tr_frac)
+            vb = valu_busy_per_ray(rec)
+            busy = None
+            if vb is not None:
+                busy = vb[0] * local_rays / kernel_s / (CUS * CLOCK_HZ)
+                roof["valu_busy"] = {
+                    "frac": round(busy, 4), "lane_utilisation": round(vb[1], 4) if vb[1] is not None else None,
+                    "active_quad_cycles_per_ray": round(vb[0], 2),
+                    "basis": "AMD's VALUBusy: SQ_ACTIVE_INST_VALU (quad-cycles, summed over the SIMDs) per ray of the record "
+                             "x this launch's rays / (CUs x clock x launch duration); lane_utilisation = "
+                             "SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)",
+                    "sensitivity": "16 extra VALU instructions per node visit cost 0.45 of their pipe time (v_fma_f32 "
+                                   "+0.96 %, v_max_f32 +1.88 %; profiles/r6/c3_v58_valu_sensitivity_ab.json): VALU work "
+                                   "the kernel sheds pays back about half its issue time"}
+            vbind = busy if busy is not None else valu_frac
+            binding = (("valu_busy" if busy is not None else "valu_issue"), vbind) if vbind >= tr_frac \
+                else ("hbm_traffic", tr_frac)
             roof["binding"] = {"resource": binding[0], "frac": round(binding[1], 4),
                                "unweighted_valu_issue": round(valu_frac, 4),
-                               "note": "the kernel is latency-bound (cycle_budget: waves wait on memory ~45 % of their "
-                                       "cycles at 4 waves/SIMD); the weighted VALU pipe occupancy is the larger share"}
+                               "note": "the VALU pipe is ~0.9 busy at ~0.47 lane utilisation (idle lanes of divergent "
+                                       "traversal and shading); memory-side traffic is ~0.2 of HBM"}
         ref_bpr = reference_equivalent(args.config)
         roof["reference_equivalent"] = {
             "bytes_per_ray": round(ref_bpr, 1), "GBps": round(ref_bpr * local_rays / kernel_s / 1e9, 1),
