@@ -297,6 +297,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # Rehearsal (tests/test_gpu_bench_rehearsal.py): RP_BENCH_REHEARSAL=gloo runs the N-rank loop with every rank on
+    # device 0 and the frames gathered by rp_frames_pack -> a gloo all-gather of the packed blocks -> rp_frames_unpack
+    # (RCCL puts no two ranks on one device).  It exercises this loop's N > 1 code on a one-GPU box; its line is labelled
+    # and is not a measurement.
+    rehearsal = world > 1 and os.environ.get("RP_BENCH_REHEARSAL", "") == "gloo"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -332,8 +339,10 @@ def main():
     smap = args.shard_map if args.shard_map != "auto" else ("balanced" if nsh > 1 else "interleave")
     params = replace(params, shard_map=F.RP_SHARD_BALANCED if smap == "balanced" else F.RP_SHARD_INTERLEAVE)
     sp = shard_params(params, rank, world) if not args.shard_of else shard_params(params, args.shard, args.shard_of)
-    with stdout_to_stderr():
-        comm = bootstrap_comm(rank, world, local)
+    comm = None
+    if not rehearsal:
+        with stdout_to_stderr():
+            comm = bootstrap_comm(rank, world, local)
     # Frames per launch (rp_render_frames_device_ws): one persistent launch renders L frames, frame f of
     # it the frame of seed + f * B * W * H, and hands out the frames' k-th tiles of the cost order together
     # (RP_FRAME_ORDER_INTERLEAVED).  The GPU's 262,144 resident lanes hold 1.6 % of a C3 frame's 16.6 M units and 12.5 %
@@ -400,7 +409,15 @@ def main():
             return
         # the launch's frames: output stage + ONE RCCL all-gather of their BGRA8 shards + de-interleave into n frames
         # (+ the launch's counters summed over the ranks), on the main stream
-        if L == 1:
+        if rehearsal:
+            send = torch.zeros(ds.frames_block_words(spx, n), dtype=torch.int32, device=dev)
+            ds.frames_pack(spx, n, bufs[i], ctrs[i], send, stream=main_stream, workspace=wss[i])
+            main_stream.synchronize()
+            blocks = [torch.zeros(send.numel(), dtype=torch.int32) for _ in range(world)]
+            dist.all_gather(blocks, send.cpu())
+            recv = torch.cat(blocks).to(dev)
+            ds.frames_unpack(spx, n, recv, frames, counters=ctrs[i], stream=main_stream, workspace=wss[i])
+        elif L == 1:
             ds.frame_gather(comm, spx, bufs[i], frame_bgra=frames, counters=ctrs[i], stream=main_stream,
                             workspace=wss[i])
         else:
@@ -600,7 +617,9 @@ def main():
                        "rng_contract": "SURVEY.md 8c: one stream per pixel" if one_stream else
                                        f"streams of {params.samples_per_stream or 32} samples",
                        "tile": [params.tile_w, params.tile_h],
-                       "parallelism": f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
+                       "parallelism": (f"REHEARSAL: {world} ranks on device 0, rp_frames_pack blocks all-gathered over "
+                                       f"gloo (RP_BENCH_REHEARSAL; not a measurement)") if rehearsal else
+                                      f"tile-sharded x{world} + RCCL all-gather (librp)" if world > 1 else "1 GPU",
                        "frames_in_flight": F_, "frames_per_launch": L,
                        "output": "to_srgb_u8 BGRA8 frame (TGA pixel order) assembled on every rank",
                        "rays_per_frame": int(rays_step), "rays_per_sample": rays_step / samples_step,
@@ -608,6 +627,7 @@ def main():
                        "scene_options": options or "defaults", "shard_map": smap,
                        **({"simulated_shard": f"shard {args.shard} of {args.shard_of}, no gather (diagnostic)"}
                           if args.shard_of else {})},
+            **({"rehearsal": True} if rehearsal else {}),
             "roofline": roof,
             "binding_frac": round(binding[1], 4) if binding else None,
             "binding_resource": binding[0] if binding else None,
@@ -624,7 +644,8 @@ def main():
                 ratios["vs_full_host_extrapolated"] = round(value / cb["full_host_extrapolated"]["value"], 1)
             out["gpu_over_cpu"] = ratios
         print(json.dumps(out), flush=True)
-    comm.close()
+    if comm is not None:
+        comm.close()
     ds.close()
     if world > 1:
         dist.destroy_process_group()

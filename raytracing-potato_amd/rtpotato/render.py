@@ -266,6 +266,41 @@ class DeviceScene:
                                         counters.data_ptr() if counters is not None else None,
                                         ctypes.c_void_p(s.cuda_stream)))
 
+    def frames_block_words(self, params: RenderParams, n_frames: int) -> int:
+        """rp_frames_block_words: 32-bit words of one rank's packed block for a launch of n_frames frames (the same on
+        every rank of the job)."""
+        p = params.to_c()
+        w = ctypes.c_uint64()
+        F.check(F.rp().rp_frames_block_words(ctypes.byref(p), n_frames, ctypes.byref(w)))
+        return w.value
+
+    def frames_pack(self, params: RenderParams, n_frames: int, shard_rgb, counters, send, stream=None,
+                    workspace: "Workspace | None" = None) -> None:
+        """rp_frames_pack: this rank's half of rp_frames_gather without the collective -- the launch's n_frames shards
+        (output stage to BGRA8) and its counters into `send` (torch int32, frames_block_words words), for a caller's
+        own all-gather."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(shard_rgb.device)
+        assert send.dtype == torch.int32 and send.is_cuda and send.numel() >= self.frames_block_words(params, n_frames)
+        p = params.to_c()
+        F.check(F.rp().rp_frames_pack(self.handle, workspace.handle if workspace else None, ctypes.byref(p), n_frames,
+                                      shard_rgb.data_ptr(), counters.data_ptr(), send.data_ptr(),
+                                      ctypes.c_void_p(s.cuda_stream)))
+
+    def frames_unpack(self, params: RenderParams, n_frames: int, recv, frames_bgra, counters=None, stream=None,
+                      workspace: "Workspace | None" = None) -> None:
+        """rp_frames_unpack: the all-gathered blocks of every rank (`recv`, rank-major) de-interleaved into the n_frames
+        assembled BGRA8 frames and the counters summed over the ranks."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream(recv.device)
+        n = params.width * params.height
+        assert frames_bgra.is_cuda and frames_bgra.numel() * frames_bgra.element_size() >= 4 * n * n_frames
+        p = params.to_c()
+        F.check(F.rp().rp_frames_unpack(self.handle, workspace.handle if workspace else None, ctypes.byref(p), n_frames,
+                                        recv.data_ptr(), frames_bgra.data_ptr(),
+                                        counters.data_ptr() if counters is not None else None,
+                                        ctypes.c_void_p(s.cuda_stream)))
+
     def render_gather(self, comm: "Comm", params: RenderParams, frame_bgra=None, frame_rgb=None, counters=None,
                       camera=None, stream=None, workspace: "Workspace | None" = None) -> None:
         """rp_render_gather: render this rank's shard and gather the frame (see frame_gather)."""
