@@ -457,6 +457,10 @@ def main():
         torch.cuda.synchronize()
         log(f"[rank {rank}] warmup launch {w} ({n} frames) done")
     elapsed_max, kdur, rays_step, samples_step, sizes = run(sp, args.steps)
+    dump = os.environ.get("RP_BENCH_DUMP")
+    if dump and rank == 0 and not args.shard_of:  # tests only: the timed run's last launch, assembled BGRA8 frames
+        import numpy as np
+        np.save(dump, frames[:sizes[-1] * params.width * params.height * 4].cpu().numpy())
     kernel_s = sum(kdur) / args.steps  # per frame: launch durations over the frames they rendered
     kernel_launch_ms = sum(kdur) / len(kdur) * 1e3
     if F_ > 1:

@@ -5,7 +5,8 @@ puts no two ranks on one device, so here every rank renders its tile shard on de
 gathered by the caller-collective pair of the C-ABI -- rp_frames_pack, a gloo all-gather of the packed blocks,
 rp_frames_unpack (RP_BENCH_REHEARSAL=gloo) -- instead of librp's RCCL all-gather.  Everything else is the N-rank loop
 itself: the gloo bootstrap, balanced shards, three launches in flight on their own streams and workspaces, the barriers
-and the max-over-ranks time, the summed counters, rank 0's single JSON line.
+and the max-over-ranks time, the summed counters, rank 0's single JSON line -- and the frames it assembles, which must
+equal the one-GPU run's bit for bit (per-unit seeding; RP_BENCH_DUMP saves the timed run's last launch).
 """
 import json
 import os
@@ -13,6 +14,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -25,12 +27,25 @@ def _free_port():
         return s.getsockname()[1]
 
 
+ARGS = ["--steps", "4", "--warmup", "2", "--spp", "40", "--samples-per-stream", "32", "--no-cpu-baseline"]
+
+
+@pytest.fixture(scope="module")
+def one_gpu_frames(tmp_path_factory):
+    """The same command on one GPU (no rehearsal): its timed run's last launch, assembled."""
+    out = str(tmp_path_factory.mktemp("n1") / "frames.npy")
+    r = subprocess.run([sys.executable, "bench.py", *ARGS], cwd=REPO, env=dict(os.environ, RP_BENCH_DUMP=out),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return np.load(out)
+
+
 @pytest.mark.parametrize("world", [2, 3])
-def test_bench_rehearsal(gpu, world):
-    env = dict(os.environ, RP_BENCH_REHEARSAL="gloo")
+def test_bench_rehearsal(gpu, world, one_gpu_frames, tmp_path):
+    dump = str(tmp_path / "frames.npy")
+    env = dict(os.environ, RP_BENCH_REHEARSAL="gloo", RP_BENCH_DUMP=dump)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world),
-           "--steps", "4", "--warmup", "2", "--spp", "16", "--no-cpu-baseline"]
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world), *ARGS]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -41,5 +56,9 @@ def test_bench_rehearsal(gpu, world):
     assert d["config"]["samples_per_stream"] == 32 and d["config"]["frames_in_flight"] == 3
     assert d["config"]["shard_map"] == "balanced"
     # the counters the unpack sums over the ranks: every pixel of the 1920 x 1080 frame once per sample
-    assert d["config"]["rays_per_frame"] >= 1920 * 1080 * 16
+    assert d["config"]["rays_per_frame"] >= 1920 * 1080 * 40
     assert d["single_frame"] and d["single_frame"]["ms_per_frame"] > 0
+    # the N-rank frames (balanced shards of 3 launches in flight, packed, gathered, assembled) = the one-GPU frames
+    frames = np.load(dump)
+    assert frames.shape == one_gpu_frames.shape and frames.size >= 1920 * 1080 * 4
+    assert np.array_equal(frames, one_gpu_frames)
