@@ -307,7 +307,8 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("gloo")  # bootstrap + barrier + max-time only; frames move over librp's RCCL
+        with stdout_to_stderr():  # gloo logs its peer connections on stdout
+            dist.init_process_group("gloo")  # bootstrap + barrier + max-time only; frames move over librp's RCCL
 
     from dataclasses import replace
     from rtpotato import _ffi as F

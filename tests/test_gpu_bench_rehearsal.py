@@ -48,8 +48,8 @@ def test_bench_rehearsal(gpu, world, one_gpu_frames, tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(world), *ARGS]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-4000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout[-2000:]  # rank 0 alone prints
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout[-2000:]  # rank 0 alone prints: one JSON line
     d = json.loads(lines[0])
     assert d["rehearsal"] is True and "REHEARSAL" in d["config"]["parallelism"]
     assert d["n_gpus"] == world and d["steps"] == 4 and d["value"] > 0 and d["scaling"] == "strong"
