@@ -592,7 +592,9 @@ def main():
                     "active_quad_cycles_per_ray": round(vb[0], 2),
                     "basis": "AMD's VALUBusy: SQ_ACTIVE_INST_VALU (quad-cycles, summed over the SIMDs) per ray of the record "
                              "x this launch's rays / (CUs x clock x launch duration); lane_utilisation = "
-                             "SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)",
+                             "SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64).  It counts one quad-cycle per VALU "
+                             "instruction (calibrated: profiles/r6/valu_rates_gfx950.json), and full-rate ops may pair two "
+                             "per quad-cycle (C3: SQ_ACTIVE_INST_VALU2 0.08), so it reads VALU issue, not pipe saturation",
                     "sensitivity": "16 extra VALU instructions per node visit cost 0.45 of their pipe time (v_fma_f32 "
                                    "+0.96 %, v_max_f32 +1.88 %; profiles/r6/c3_v58_valu_sensitivity_ab.json): VALU work "
                                    "the kernel sheds pays back about half its issue time"}
