@@ -603,7 +603,7 @@ def main():
                 else ("hbm_traffic", tr_frac)
             roof["binding"] = {"resource": binding[0], "frac": round(binding[1], 4),
                                "unweighted_valu_issue": round(valu_frac, 4),
-                               "note": "the VALU pipe is ~0.9 busy at ~0.47 lane utilisation (idle lanes of divergent "
+                               "note": "VALU instructions issue in ~0.8-0.9 of the quad-cycles at ~0.47 lane utilisation (idle lanes of divergent "
                                        "traversal and shading); memory-side traffic is ~0.2 of HBM"}
         ref_bpr = reference_equivalent(args.config)
         roof["reference_equivalent"] = {
