@@ -295,6 +295,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rank 0's stdout is the one JSON line: every other write to fd 1 (torch, gloo, RCCL, HIP -- on every rank) goes to
+    # stderr for the whole run, and the line goes out through a private copy of the original stdout
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
     # Rehearsal (tests/test_gpu_bench_rehearsal.py): RP_BENCH_REHEARSAL=gloo runs the N-rank loop with every rank on
@@ -650,7 +655,8 @@ def main():
             if "full_host_extrapolated" in cb:
                 ratios["vs_full_host_extrapolated"] = round(value / cb["full_host_extrapolated"]["value"], 1)
             out["gpu_over_cpu"] = ratios
-        print(json.dumps(out), flush=True)
+        line_out.write(json.dumps(out) + "\n")
+        line_out.flush()
     if comm is not None:
         comm.close()
     ds.close()
